@@ -1,0 +1,178 @@
+"""ctypes mirror of include/art.h, include/art_device.h and include/art_synth.h.
+
+Struct layouts are byte-identical to the C# structs of the reference (2-byte packing):
+  ColliderAABBStruct   DataTypes/Collider Structs/ColliderAABBStruct.cs:10-14   (20 B)
+  ColliderOBBStruct    DataTypes/Collider Structs/ColliderOBBStruct.cs:10-24    (26 B)
+  ColliderSphereStruct DataTypes/Collider Structs/ColliderSphereStruct.cs:10-14 (16 B)
+  AudioTargetRTSettings DataTypes/AudioTargetRTSettings.cs:11-16               (24 B)
+The numpy dtypes below are the same layouts, so collider arrays can be handed to the C ABI as
+raw pointers (NativeArray.GetUnsafePtr() in the Unity host).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+# ----------------------------------------------------------------------------- numpy dtypes
+HALF3 = np.dtype([("x", "<u2"), ("y", "<u2"), ("z", "<u2")])
+MATERIAL = np.dtype([("absorption", "<u2"), ("density", "<u2"), ("echo", "<u2")])
+AABB = np.dtype([("center", "<u2", 3), ("size", "<u2", 3), ("material", "<u2", 3), ("audio_target_id", "<i2")])
+OBB = np.dtype([("center", "<u2", 3), ("size", "<u2", 3), ("rot", "<u2", 3), ("material", "<u2", 3),
+                ("audio_target_id", "<i2")])
+SPHERE = np.dtype([("center", "<u2", 3), ("radius", "<u2"), ("material", "<u2", 3), ("audio_target_id", "<i2")])
+SETTINGS = np.dtype([("muffle_strength", "<f4"), ("reverb_strength", "<f4"), ("reverb_volume", "<f4"),
+                     ("perceived_position", "<f4", 3)])
+DSP_PARAMS = np.dtype([("dry_level", "<f4"), ("dry_boost", "<f4"), ("muffle_cutoff", "<f4"), ("muffle_alpha", "<f4"),
+                       ("muffle_active", "<i4"), ("reserved", "<i4")])
+assert AABB.itemsize == 20 and OBB.itemsize == 26 and SPHERE.itemsize == 16
+assert SETTINGS.itemsize == 24 and DSP_PARAMS.itemsize == 24
+
+# ----------------------------------------------------------------------------- constants
+ART_STAGE_RAYTRACE = 0x1
+ART_STAGE_PERMEATE = 0x2
+ART_STAGE_REDUCE = 0x4
+ART_STAGE_DSP_PARAMS = 0x8
+ART_STAGE_ALL = 0xF
+
+ART_OK = 0
+ART_E_INVALID = -1
+ART_E_DEVICE = -2
+ART_E_UNSUPPORTED = -3
+ART_E_NOMEM = -4
+ART_E_STATE = -5
+ERROR_NAMES = {ART_E_INVALID: "ART_E_INVALID", ART_E_DEVICE: "ART_E_DEVICE", ART_E_UNSUPPORTED: "ART_E_UNSUPPORTED",
+               ART_E_NOMEM: "ART_E_NOMEM", ART_E_STATE: "ART_E_STATE"}
+
+ART_CTX_COUNT_TESTS = 0x1
+ART_CTX_TIME_KERNELS = 0x2
+ART_OUT_HIT_RESULTS = 0x1
+
+ART_OWN_SPHERE, ART_OWN_AABB, ART_OWN_OBB = 0, 1, 2
+
+
+# ----------------------------------------------------------------------------- ctypes structs
+class art_curve(C.Structure):
+    _fields_ = [("baked", C.POINTER(C.c_float)), ("sample_count", C.c_int32), ("length", C.c_float)]
+
+
+class art_dsp_desc(C.Structure):
+    _fields_ = [("reverb_dry_level_min", C.c_float), ("reverb_dry_level_max", C.c_float),
+                ("reverb_dry_boost_min", C.c_float), ("reverb_dry_boost_max", C.c_float),
+                ("muffle_cutoff_min", C.c_float), ("muffle_cutoff_max", C.c_float),
+                ("reverb_volume_curve", art_curve), ("muffle_curve", art_curve), ("sample_rate", C.c_int32)]
+
+
+class art_frame_desc(C.Structure):
+    _fields_ = [("ray_directions", C.c_void_p), ("ray_count", C.c_int32),
+                ("aabb_colliders", C.c_void_p), ("aabb_count", C.c_int32),
+                ("obb_colliders", C.c_void_p), ("obb_count", C.c_int32),
+                ("sphere_colliders", C.c_void_p), ("sphere_count", C.c_int32),
+                ("audio_target_positions", C.c_void_p), ("audio_target_count", C.c_int32),
+                ("max_ray_life", C.c_float), ("max_hits_per_ray", C.c_int32),
+                ("max_muffle_hit_distance", C.c_float), ("muffle_effectiveness", C.c_float),
+                ("permeation_strength_per_ray", C.c_float), ("permeation_effectiveness", C.c_float),
+                ("max_reverb_distance", C.c_float), ("batch_size", C.c_int32), ("batch_slots", C.c_int32),
+                ("stages", C.c_uint32), ("dsp", C.POINTER(art_dsp_desc))]
+
+
+class art_fan(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("echo_ray_distances", C.c_void_p), ("muffle_ray_hits", C.c_void_p),
+                ("permeation_power_remains", C.c_void_p), ("settings", C.c_void_p), ("dsp_params", C.c_void_p),
+                ("ray_hit_points", C.c_void_p), ("ray_hit_counts", C.c_void_p)]
+
+
+class art_test_counts(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("rt_sphere", "rt_aabb", "rt_obb", "perm_hit_sphere", "perm_hit_aabb",
+                                           "perm_hit_obb", "perm_loss_sphere", "perm_loss_aabb", "perm_loss_obb")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class art_fan_layout(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("stride", "settings_off", "dsp_off", "muffle_off", "perm_off", "echo_off",
+                                           "hit_points_off", "hit_counts_off")]
+
+
+class art_kernel_times(C.Structure):
+    _fields_ = [("raytrace_ms", C.c_double), ("permeate_ms", C.c_double), ("reduce_ms", C.c_double),
+                ("launches", C.c_int32)]
+
+
+class art_synth_config(C.Structure):
+    _fields_ = [("sphere_count", C.c_int32), ("aabb_count", C.c_int32), ("obb_count", C.c_int32),
+                ("target_count", C.c_int32), ("fan_count", C.c_int32), ("ray_count", C.c_int32),
+                ("owned_type", C.c_int32), ("seed", C.c_uint64)]
+
+
+# Every symbol include/*.h declares, with its ctypes signature.
+VP, I32, U32, U64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64
+SIGNATURES = {
+    # art.h
+    "art_create": (I32, [U32, C.POINTER(VP)]),
+    "art_destroy": (None, [VP]),
+    "art_last_error": (C.c_char_p, [VP]),
+    "art_schedule": (I32, [VP, C.POINTER(art_frame_desc), C.POINTER(art_fan), I32, C.POINTER(U64)]),
+    "art_is_completed": (I32, [VP, U64]),
+    "art_complete": (I32, [VP, U64]),
+    "art_set_flags": (I32, [VP, U32]),
+    "art_last_test_counts": (I32, [VP, C.POINTER(art_test_counts)]),
+    "art_version": (U32, []),
+    # art_device.h
+    "art_fan_layout_get": (I32, [C.POINTER(art_frame_desc), U32, C.POINTER(art_fan_layout)]),
+    "art_scene_bind": (I32, [VP, C.POINTER(art_frame_desc)]),
+    "art_launch_device": (I32, [VP, VP, I32, VP, U32, VP]),
+    "art_count_device": (I32, [VP, VP, I32, VP, U32, VP, C.POINTER(art_test_counts)]),
+    "art_kernel_timing": (I32, [VP, C.POINTER(art_kernel_times)]),
+    "art_device_count": (I32, []),
+    # art_synth.h
+    "art_synth_scene": (I32, [C.POINTER(art_synth_config), VP, VP, VP, VP, VP, VP]),
+    "art_fibonacci_directions": (None, [I32, VP]),
+    "art_f32tof16": (C.c_uint16, [C.c_float]),
+    "art_f16tof32": (C.c_float, [C.c_uint16]),
+}
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libart.so")
+
+_lib = None
+
+
+def _preload_torch_hip_runtime():
+    """One HIP runtime per process. torch ships its own libamdhip64.so (SONAME libamdhip64.so.7,
+    the same SONAME as /opt/rocm's). If libart.so loaded /opt/rocm's copy first, a later
+    `import torch` would map a second runtime and torch would see no GPU. Loading torch's copy
+    by path first makes libart.so bind to it (SONAME match) and lets torch reuse it (same file).
+    ART_HIP_RUNTIME=system keeps /opt/rocm's runtime."""
+    if os.environ.get("ART_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        C.CDLL(cand, mode=C.RTLD_GLOBAL)
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load libart.so (the HIP extension). Fails loudly when it has not been built: there is no
+    CPU fallback for the product path."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    _preload_torch_hip_runtime()
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"libart.so not found at {p}: build it with `make -C audio-raytracer_amd` "
+                          "(or __graft_entry__.build()); the GPU path has no CPU fallback")
+    lib = C.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib

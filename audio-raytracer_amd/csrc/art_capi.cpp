@@ -1,0 +1,717 @@
+// art_capi.cpp — the C ABI (include/art.h, include/art_device.h) over the HIP kernels.
+//
+// Replaces the reference's per-frame job scheduling in Audio/AudioRayTracer.cs:161-237:
+//   AudioRaytracerJobBatched.Schedule(rayCount, batchSize)           (:191)
+//   + AudioPermeationJobBatched.Schedule(rayCount, batchSize)        (:213)
+//   + ProcessAudioDataJob.Schedule(handleA), CombineDependencies     (:237)
+//   -> art_schedule: H2D of the frame's inputs, prep + raytrace + permeate + reduce kernels on
+//      one HIP stream per device, D2H of the packed per-fan result blocks; one event per device.
+//   JobHandle.IsCompleted (:95) -> art_is_completed; JobHandle.Complete() (:97) -> art_complete.
+// Fans are sharded contiguously over the context's devices (SURVEY.md §8 e); each device holds
+// a full copy of the scene. There is no CPU backend: without a HIP device art_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/art.h"
+#include "../../include/art_device.h"
+#include "art_internal.hpp"
+#include "unity_math.hpp"
+
+#include <cmath>
+
+using namespace art;
+
+namespace {
+
+constexpr uint32_t kAbiVersion = (1u << 16) | 0u;
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, std::max<size_t>(n, 256)) != hipSuccess) { p = nullptr; return false; }
+    cap = std::max<size_t>(n, 256);
+    return true;
+  }
+  void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(&p, std::max<size_t>(n, 256), hipHostMallocDefault) != hipSuccess) { p = nullptr; return false; }
+    cap = std::max<size_t>(n, 256);
+    return true;
+  }
+  void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+// Scalars of one frame that the kernels need, plus the derived batch tables.
+struct Frame {
+  int R = 0, H = 0, T = 0, TC = 0, bs = 0, nb = 0;
+  int ns = 0, na = 0, no = 0;
+  uint32_t stages = 0;
+  FrameParams fp{};
+  FanLayout L{};
+  std::vector<int2> slot_batch;        // permeation: [TC] ray range of the last batch writing slot s
+  std::vector<uint8_t> muffle_reset;   // raytrace: [TC] 1 if some batch resets slot s
+  std::vector<int> ray_order;          // lane slot -> ray index (direction-coherent at TC == 1)
+  // input staging layout (bytes)
+  size_t off_sph = 0, off_aabb = 0, off_obb = 0, off_tgt = 0, off_dirs = 0, off_vol = 0, off_muf = 0, off_tab = 0,
+         off_reset = 0, off_order = 0, raw_bytes = 0;
+  size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_bytes = 0;
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  DevBuf raw, soa, origins, block, acc, counts;
+  int fan_begin = 0, fan_count = 0;
+  DevScene sc{};
+  bool bound = false;
+  std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
+  std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
+};
+
+}  // namespace
+
+struct art_ctx {
+  std::vector<Device> devs;
+  std::string err;
+  uint32_t flags = 0;
+  HostBuf h_in, h_block;
+  Frame fr;                      // frame of the bound scene / last schedule
+  // in-flight frame
+  bool inflight = false;
+  art_handle handle = 0;
+  uint64_t next_handle = 1;
+  std::vector<art_fan> fans;
+  bool counted = false;
+  art_test_counts last_counts{};
+  bool has_counts = false;
+  std::vector<uint64_t> nonowned;  // per type (s, a, o): sum over targets of non-owned colliders
+};
+
+namespace {
+
+int fail(art_ctx* c, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail(art_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                          \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
+    if (e_ != hipSuccess) return fail(ctx, ART_E_DEVICE, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+int validate_desc(art_ctx* c, const art_frame_desc* d) {
+  if (!d) return fail(c, ART_E_INVALID, "desc is NULL");
+  if (d->ray_count <= 0 || !d->ray_directions) return fail(c, ART_E_INVALID, "ray_count must be > 0 with directions");
+  if (d->ray_count > (1 << 20)) return fail(c, ART_E_UNSUPPORTED, "ray_count > 2^20");
+  if (d->audio_target_count <= 0 || !d->audio_target_positions)
+    return fail(c, ART_E_INVALID, "audio_target_count must be > 0 (the reference skips frames without targets, AudioRayTracer.cs:95)");
+  if (d->audio_target_count > kMaxTargets) return fail(c, ART_E_UNSUPPORTED, "audio_target_count > %d", kMaxTargets);
+  if (d->max_hits_per_ray <= 0 || d->max_hits_per_ray > 32)
+    return fail(c, ART_E_UNSUPPORTED, "max_hits_per_ray must be in [1, 32] (reference maxBounces <= 25, AudioRayTracer.cs:14)");
+  if ((long long)d->ray_count * d->max_hits_per_ray > (1 << 24)) return fail(c, ART_E_UNSUPPORTED, "R*H > 2^24");
+  if (d->batch_size <= 0 || d->batch_slots <= 0) return fail(c, ART_E_INVALID, "batch_size and batch_slots must be > 0");
+  if (d->aabb_count < 0 || d->obb_count < 0 || d->sphere_count < 0) return fail(c, ART_E_INVALID, "negative collider count");
+  if ((d->aabb_count && !d->aabb_colliders) || (d->obb_count && !d->obb_colliders) || (d->sphere_count && !d->sphere_colliders))
+    return fail(c, ART_E_INVALID, "collider pointer is NULL with a non-zero count");
+  if (d->stages & ~ART_STAGE_ALL) return fail(c, ART_E_INVALID, "unknown stage bits");
+  if (d->stages & ART_STAGE_DSP_PARAMS) {
+    if (!d->dsp) return fail(c, ART_E_INVALID, "ART_STAGE_DSP_PARAMS needs desc->dsp");
+    if (!(d->stages & ART_STAGE_REDUCE)) return fail(c, ART_E_INVALID, "ART_STAGE_DSP_PARAMS needs ART_STAGE_REDUCE");
+    const art_dsp_desc* p = d->dsp;
+    if (!p->reverb_volume_curve.baked || p->reverb_volume_curve.sample_count < 2 || !p->muffle_curve.baked ||
+        p->muffle_curve.sample_count < 2)
+      return fail(c, ART_E_INVALID, "DSP curves need >= 2 baked samples");
+    if (p->reverb_volume_curve.sample_count > 4096 || p->muffle_curve.sample_count > 4096)
+      return fail(c, ART_E_UNSUPPORTED, "DSP curves > 4096 samples");
+  }
+  return ART_OK;
+}
+
+FanLayout make_layout(const art_frame_desc* d, uint32_t out_flags) {
+  FanLayout L{};
+  const size_t T = d->audio_target_count, TC = d->batch_slots, RH = (size_t)d->ray_count * d->max_hits_per_ray;
+  L.has_dsp = (d->stages & ART_STAGE_DSP_PARAMS) ? 1 : 0;
+  L.has_hits = (out_flags & ART_OUT_HIT_RESULTS) ? 1 : 0;
+  size_t off = 0;
+  L.settings_off = (uint32_t)off; off = align_up(off + T * sizeof(art_target_settings), 16);
+  L.dsp_off = (uint32_t)off; off = align_up(off + (L.has_dsp ? T * sizeof(art_dsp_params) : 0), 16);
+  L.muffle_off = (uint32_t)off; off = align_up(off + TC * T * 2, 16);
+  L.perm_off = (uint32_t)off; off = align_up(off + TC * T * 4, 16);
+  L.echo_off = (uint32_t)off; off = align_up(off + RH * 2, 16);
+  L.hit_points_off = (uint32_t)off; off = align_up(off + (L.has_hits ? RH * sizeof(art_half3) : 0), 16);
+  L.hit_counts_off = (uint32_t)off; off = align_up(off + (L.has_hits ? (size_t)d->ray_count : 0), 16);
+  L.stride = (uint32_t)off;
+  return L;
+}
+
+// Direction-coherent visiting order of the rays: octahedral map of each direction, quantised
+// to 16 bits per axis, Morton-interleaved, sorted. 64 consecutive slots then cover a compact
+// patch of the sphere, so a wave's echo / muffle rays see the same blockers. Only the lane
+// assignment changes; every output is written at the ray's own index.
+void coherent_order(const art_half3* dirs, int R, std::vector<int>& order) {
+  std::vector<std::pair<uint32_t, int>> keys((size_t)R);
+  for (int i = 0; i < R; ++i) {
+    float x = art_f16tof32_host(dirs[i].x), y = art_f16tof32_host(dirs[i].y), z = art_f16tof32_host(dirs[i].z);
+    float n = std::fabs(x) + std::fabs(y) + std::fabs(z);
+    float u = 0.0f, v = 0.0f;
+    if (n > 0.0f && n == n) {
+      x /= n; y /= n; z /= n;
+      if (z < 0.0f) {
+        float ux = (1.0f - std::fabs(y)) * (x >= 0.0f ? 1.0f : -1.0f);
+        float vy = (1.0f - std::fabs(x)) * (y >= 0.0f ? 1.0f : -1.0f);
+        u = ux; v = vy;
+      } else {
+        u = x; v = y;
+      }
+    }
+    auto q = [](float a) {
+      float t = (a + 1.0f) * 0.5f * 65535.0f;
+      t = t < 0.0f ? 0.0f : (t > 65535.0f ? 65535.0f : t);
+      return (uint32_t)t;
+    };
+    auto spread = [](uint32_t a) {
+      a &= 0xFFFFu;
+      a = (a | (a << 8)) & 0x00FF00FFu;
+      a = (a | (a << 4)) & 0x0F0F0F0Fu;
+      a = (a | (a << 2)) & 0x33333333u;
+      a = (a | (a << 1)) & 0x55555555u;
+      return a;
+    };
+    keys[(size_t)i] = {spread(q(u)) | (spread(q(v)) << 1), i};
+  }
+  std::stable_sort(keys.begin(), keys.end(), [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
+    return a.first < b.first;
+  });
+  order.resize((size_t)R);
+  for (int i = 0; i < R; ++i) order[(size_t)i] = keys[(size_t)i].second;
+}
+
+// Frame scalars + batch tables (Audio/AudioRayTracer.cs:161, Jobs/*:63-64, :36-37).
+void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
+  f = Frame();
+  f.R = d->ray_count; f.H = d->max_hits_per_ray; f.T = d->audio_target_count;
+  f.TC = d->batch_slots; f.bs = d->batch_size; f.nb = (f.R + f.bs - 1) / f.bs;
+  f.ns = d->sphere_count; f.na = d->aabb_count; f.no = d->obb_count;
+  f.stages = d->stages;
+  f.L = make_layout(d, out_flags);
+  f.slot_batch.assign(f.TC, make_int2(0, 0));
+  f.muffle_reset.assign(f.TC, 0);
+  for (int start = 0; start < f.R; start += f.bs) {
+    const int cnt = std::min(f.bs, f.R - start);
+    // raytracer: batchCount = MuffleRayHits.Length / T = TC; batchId = start * TC / R
+    const long long rid = (long long)start * f.TC / f.R;
+    f.muffle_reset[rid] = 1;
+    // permeation: batchCount = PPR.Length / totalRays / T (integer division, Q7)
+    const int pbc = (f.TC * f.T) / cnt / f.T;
+    const long long pid = (long long)start * pbc / f.R;
+    f.slot_batch[pid] = make_int2(start, start + cnt);  // later batches overwrite earlier ones
+  }
+  if (f.TC == 1) {
+    coherent_order(d->ray_directions, f.R, f.ray_order);
+  } else {  // per-batch muffle slots: keep rays in index order
+    f.ray_order.resize((size_t)f.R);
+    for (int i = 0; i < f.R; ++i) f.ray_order[(size_t)i] = i;
+  }
+  FrameParams& p = f.fp;
+  p.R = f.R; p.H = f.H; p.T = f.T; p.TC = f.TC; p.bs = f.bs; p.nb = f.nb;
+  p.max_life = d->max_ray_life; p.max_muffle = d->max_muffle_hit_distance;
+  p.muffle_eff = d->muffle_effectiveness; p.perm_strength = d->permeation_strength_per_ray;
+  p.perm_eff = d->permeation_effectiveness; p.max_reverb = d->max_reverb_distance;
+  p.stages = d->stages;
+  if ((d->stages & ART_STAGE_DSP_PARAMS) && d->dsp) {
+    const art_dsp_desc* q = d->dsp;
+    p.dl_min = q->reverb_dry_level_min; p.dl_max = q->reverb_dry_level_max;
+    p.db_min = q->reverb_dry_boost_min; p.db_max = q->reverb_dry_boost_max;
+    p.mc_min = q->muffle_cutoff_min; p.mc_max = q->muffle_cutoff_max;
+    p.vol_n = q->reverb_volume_curve.sample_count; p.vol_len = q->reverb_volume_curve.length;
+    p.muf_n = q->muffle_curve.sample_count; p.muf_len = q->muffle_curve.length;
+    p.sample_rate = q->sample_rate;
+  }
+  // input staging layout (16-B aligned sections)
+  size_t o = 0;
+  f.off_sph = o; o = align_up(o + (size_t)f.ns * sizeof(art_sphere), 16);
+  f.off_aabb = o; o = align_up(o + (size_t)f.na * sizeof(art_aabb), 16);
+  f.off_obb = o; o = align_up(o + (size_t)f.no * sizeof(art_obb), 16);
+  f.off_tgt = o; o = align_up(o + (size_t)f.T * 12, 16);
+  f.off_dirs = o; o = align_up(o + (size_t)f.R * sizeof(art_half3), 16);
+  f.off_vol = o; o = align_up(o + (size_t)p.vol_n * 4, 16);
+  f.off_muf = o; o = align_up(o + (size_t)p.muf_n * 4, 16);
+  f.off_tab = o; o = align_up(o + (size_t)f.TC * sizeof(int2), 16);
+  f.off_reset = o; o = align_up(o + (size_t)f.TC, 16);
+  f.off_order = o; o = align_up(o + (size_t)f.R * 4, 16);
+  f.raw_bytes = o;
+  size_t s = 0;
+  f.soa_sph = s; s = align_up(s + (size_t)f.ns * sizeof(SphereRec), 256);
+  f.soa_aabb = s; s = align_up(s + (size_t)f.na * sizeof(AabbRec), 256);
+  f.soa_obb = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
+  f.soa_bytes = s;
+}
+
+void pack_inputs(const art_frame_desc* d, const Frame& f, uint8_t* h) {
+  if (f.ns) memcpy(h + f.off_sph, d->sphere_colliders, (size_t)f.ns * sizeof(art_sphere));
+  if (f.na) memcpy(h + f.off_aabb, d->aabb_colliders, (size_t)f.na * sizeof(art_aabb));
+  if (f.no) memcpy(h + f.off_obb, d->obb_colliders, (size_t)f.no * sizeof(art_obb));
+  memcpy(h + f.off_tgt, d->audio_target_positions, (size_t)f.T * 12);
+  memcpy(h + f.off_dirs, d->ray_directions, (size_t)f.R * sizeof(art_half3));
+  if (f.fp.vol_n) memcpy(h + f.off_vol, d->dsp->reverb_volume_curve.baked, (size_t)f.fp.vol_n * 4);
+  if (f.fp.muf_n) memcpy(h + f.off_muf, d->dsp->muffle_curve.baked, (size_t)f.fp.muf_n * 4);
+  memcpy(h + f.off_tab, f.slot_batch.data(), (size_t)f.TC * sizeof(int2));
+  memcpy(h + f.off_reset, f.muffle_reset.data(), (size_t)f.TC);
+  memcpy(h + f.off_order, f.ray_order.data(), (size_t)f.R * 4);
+}
+
+// Upload the packed inputs to one device and build its SoA records (async on dv.stream).
+int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
+  HIP_TRY(c, hipSetDevice(dv.id));
+  if (!dv.raw.reserve(f.raw_bytes) || !dv.soa.reserve(f.soa_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
+  HIP_TRY(c, hipMemcpyAsync(dv.raw.p, h_in, f.raw_bytes, hipMemcpyHostToDevice, dv.stream));
+  uint8_t* raw = static_cast<uint8_t*>(dv.raw.p);
+  uint8_t* soa = static_cast<uint8_t*>(dv.soa.p);
+  launch_prep(reinterpret_cast<const art_sphere*>(raw + f.off_sph), f.ns, reinterpret_cast<const art_aabb*>(raw + f.off_aabb),
+              f.na, reinterpret_cast<const art_obb*>(raw + f.off_obb), f.no, reinterpret_cast<SphereRec*>(soa + f.soa_sph),
+              reinterpret_cast<AabbRec*>(soa + f.soa_aabb), reinterpret_cast<ObbRec*>(soa + f.soa_obb), dv.stream);
+  HIP_TRY(c, hipGetLastError());
+  DevScene& sc = dv.sc;
+  sc.sph = reinterpret_cast<const SphereRec*>(soa + f.soa_sph); sc.ns = f.ns;
+  sc.aabb = reinterpret_cast<const AabbRec*>(soa + f.soa_aabb); sc.na = f.na;
+  sc.obb = reinterpret_cast<const ObbRec*>(soa + f.soa_obb); sc.no = f.no;
+  sc.targets = reinterpret_cast<const float*>(raw + f.off_tgt); sc.T = f.T;
+  sc.dirs = reinterpret_cast<const uint16_t*>(raw + f.off_dirs); sc.R = f.R;
+  dv.bound = true;
+  return ART_OK;
+}
+
+// Per-type sum over targets of colliders NOT owned by the target (permeation loss test counts).
+void count_nonowned(art_ctx* c, const art_frame_desc* d) {
+  c->nonowned.assign(3, 0);
+  for (int t = 0; t < d->audio_target_count; ++t) {
+    uint64_t os = 0, oa = 0, oo = 0;
+    for (int i = 0; i < d->sphere_count; ++i) os += d->sphere_colliders[i].audio_target_id == t;
+    for (int i = 0; i < d->aabb_count; ++i) oa += d->aabb_colliders[i].audio_target_id == t;
+    for (int i = 0; i < d->obb_count; ++i) oo += d->obb_colliders[i].audio_target_id == t;
+    c->nonowned[0] += d->sphere_count - os;
+    c->nonowned[1] += d->aabb_count - oa;
+    c->nonowned[2] += d->obb_count - oo;
+  }
+}
+
+hipEvent_t pool_event(Device& dv, size_t i) {
+  while (dv.ev_pool.size() <= i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    dv.ev_pool.push_back(e);
+  }
+  return dv.ev_pool[i];
+}
+
+// Enqueue the kernels of one frame for fan_count fans on stream st.
+int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origins, int fan_count, uint8_t* d_block,
+                    hipStream_t st, bool count) {
+  if (fan_count == 0) return ART_OK;
+  const bool timing = (c->flags & ART_CTX_TIME_KERNELS) && !count;
+  FrameParams fp = f.fp;
+  fp.S = fan_count;
+  const uint8_t* raw = static_cast<const uint8_t*>(dv.raw.p);
+  fp.vol_curve = reinterpret_cast<const float*>(raw + f.off_vol);
+  fp.muf_curve = reinterpret_cast<const float*>(raw + f.off_muf);
+  const int2* slot_batch = reinterpret_cast<const int2*>(raw + f.off_tab);
+  const uint8_t* muffle_reset = raw + f.off_reset;
+  const size_t acc_bytes = (size_t)fan_count * f.TC * f.T * sizeof(uint32_t);
+  if (!dv.acc.reserve(acc_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
+  uint32_t* acc = static_cast<uint32_t*>(dv.acc.p);
+  DevCounts* counts = nullptr;
+  unsigned long long* nhit = nullptr;
+  if (count) {
+    if (!dv.counts.reserve(sizeof(DevCounts) + 16)) return fail(c, ART_E_NOMEM, "device allocation failed");
+    counts = static_cast<DevCounts*>(dv.counts.p);
+    nhit = reinterpret_cast<unsigned long long*>(static_cast<uint8_t*>(dv.counts.p) + sizeof(DevCounts));
+    HIP_TRY(c, hipMemsetAsync(dv.counts.p, 0, sizeof(DevCounts) + 16, st));
+  }
+  auto tstart = [&](int kind) -> size_t {
+    size_t i = dv.ev_used.size() * 2;
+    hipEvent_t e = pool_event(dv, i);
+    pool_event(dv, i + 1);
+    if (e) (void)hipEventRecord(e, st);
+    dv.ev_used.push_back({kind, i});
+    return i;
+  };
+  auto tstop = [&](size_t i) { hipEvent_t e = pool_event(dv, i + 1); if (e) (void)hipEventRecord(e, st); };
+
+  if (f.stages & ART_STAGE_RAYTRACE) {
+    HIP_TRY(c, hipMemsetAsync(acc, 0, acc_bytes, st));
+    size_t ti = timing ? tstart(0) : 0;
+    // The counting variant sweeps colliders in exact reference order per lane (its per-lane
+    // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
+    if (count || f.T > 31 || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER))
+      launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
+    else
+      launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, reinterpret_cast<const int*>(raw + f.off_order), st);
+    if (timing) tstop(ti);
+    HIP_TRY(c, hipGetLastError());
+  }
+  if (f.stages & ART_STAGE_PERMEATE) {
+    size_t ti = timing ? tstart(1) : 0;
+    launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, st);
+    if (timing) tstop(ti);
+    HIP_TRY(c, hipGetLastError());
+    if (count) {
+      launch_perm_count(dv.sc, fp, d_origins, counts, nhit, st);
+      HIP_TRY(c, hipGetLastError());
+    }
+  }
+  if (f.stages & (ART_STAGE_RAYTRACE | ART_STAGE_REDUCE)) {
+    size_t ti = timing ? tstart(2) : 0;
+    launch_reduce(dv.sc, fp, f.L, d_block, acc, muffle_reset, st);
+    if (timing) tstop(ti);
+    HIP_TRY(c, hipGetLastError());
+  }
+  return ART_OK;
+}
+
+int read_counts(art_ctx* c, Device& dv, hipStream_t st, art_test_counts* out, bool accumulate) {
+  DevCounts h{};
+  unsigned long long nhit = 0;
+  HIP_TRY(c, hipMemcpyAsync(&h, dv.counts.p, sizeof h, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(&nhit, static_cast<uint8_t*>(dv.counts.p) + sizeof(DevCounts), 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  if (!accumulate) memset(out, 0, sizeof *out);
+  out->rt_sphere += h.v[0]; out->rt_aabb += h.v[1]; out->rt_obb += h.v[2];
+  out->perm_hit_sphere += h.v[3]; out->perm_hit_aabb += h.v[4]; out->perm_hit_obb += h.v[5];
+  if (c->nonowned.size() == 3) {
+    out->perm_loss_sphere += nhit * c->nonowned[0];
+    out->perm_loss_aabb += nhit * c->nonowned[1];
+    out->perm_loss_obb += nhit * c->nonowned[2];
+  }
+  return ART_OK;
+}
+
+bool fan_wants_hits(const art_fan* fans, int n) {
+  for (int i = 0; i < n; ++i)
+    if (fans[i].ray_hit_points || fans[i].ray_hit_counts) return true;
+  return false;
+}
+
+}  // namespace
+
+// ============================================================================================
+// C ABI
+// ============================================================================================
+extern "C" {
+
+ART_API uint32_t art_version(void) { return kAbiVersion; }
+
+ART_API int art_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+ART_API int art_create(uint32_t device_mask, art_ctx** out) {
+  if (!out) return ART_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ART_E_DEVICE;
+  art_ctx* c = new (std::nothrow) art_ctx();
+  if (!c) return ART_E_NOMEM;
+  if (device_mask == 0) device_mask = 1;
+  for (int i = 0; i < 32; ++i) {
+    if (!(device_mask & (1u << i))) continue;
+    if (i >= n) { delete c; return ART_E_DEVICE; }
+    Device dv;
+    dv.id = i;
+    if (hipSetDevice(i) != hipSuccess || hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&dv.done, hipEventDisableTiming) != hipSuccess) {
+      delete c;
+      return ART_E_DEVICE;
+    }
+    c->devs.push_back(dv);
+  }
+  *out = c;
+  return ART_OK;
+}
+
+ART_API void art_destroy(art_ctx* c) {
+  if (!c) return;
+  for (Device& dv : c->devs) {
+    (void)hipSetDevice(dv.id);
+    if (dv.stream) (void)hipStreamSynchronize(dv.stream);
+    dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
+    for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
+    if (dv.done) (void)hipEventDestroy(dv.done);
+    if (dv.stream) (void)hipStreamDestroy(dv.stream);
+  }
+  c->h_in.release();
+  c->h_block.release();
+  delete c;
+}
+
+ART_API const char* art_last_error(const art_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+ART_API int art_set_flags(art_ctx* c, uint32_t flags) {
+  if (!c) return ART_E_INVALID;
+  c->flags = flags;
+  return ART_OK;
+}
+
+ART_API int art_fan_layout_get(const art_frame_desc* d, uint32_t out_flags, art_fan_layout* out) {
+  if (!out) return ART_E_INVALID;
+  int rc = validate_desc(nullptr, d);
+  if (rc) return rc;
+  FanLayout L = make_layout(d, out_flags);
+  out->stride = L.stride; out->settings_off = L.settings_off; out->dsp_off = L.dsp_off; out->muffle_off = L.muffle_off;
+  out->perm_off = L.perm_off; out->echo_off = L.echo_off; out->hit_points_off = L.hit_points_off;
+  out->hit_counts_off = L.hit_counts_off;
+  return ART_OK;
+}
+
+ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fans, int32_t fan_count, art_handle* out) {
+  if (!c) return ART_E_INVALID;
+  if (!out) return fail(c, ART_E_INVALID, "handle pointer is NULL");
+  if (c->inflight) return fail(c, ART_E_STATE, "a frame is in flight: call art_complete first (AudioRayTracer.cs:97)");
+  int rc = validate_desc(c, d);
+  if (rc) return rc;
+  if (fan_count < 0 || (fan_count > 0 && !fans)) return fail(c, ART_E_INVALID, "bad fans array");
+  const bool hits = fan_wants_hits(fans, fan_count);
+  for (int i = 0; i < fan_count; ++i) {
+    const art_fan& f = fans[i];
+    if (!f.echo_ray_distances || !f.muffle_ray_hits || !f.permeation_power_remains || !f.settings)
+      return fail(c, ART_E_INVALID, "fan %d: echo/muffle/permeation/settings arrays are required", i);
+  }
+  Frame& f = c->fr;
+  make_frame(d, hits ? ART_OUT_HIT_RESULTS : 0u, f);
+  const FanLayout& L = f.L;
+  if (!c->h_in.reserve(f.raw_bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  const size_t origins_off = align_up(f.raw_bytes, 16);
+  if (!c->h_in.reserve(origins_off + (size_t)fan_count * 12)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  if (!c->h_block.reserve((size_t)fan_count * L.stride)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  uint8_t* hin = static_cast<uint8_t*>(c->h_in.p);
+  uint8_t* hb = static_cast<uint8_t*>(c->h_block.p);
+  pack_inputs(d, f, hin);
+  float* horg = reinterpret_cast<float*>(hin + origins_off);
+  // In/out arrays (the reference's persistent NativeArrays): slots no batch resets keep their
+  // contents, so their current values travel to the device with the frame.
+  const size_t RH = (size_t)f.R * f.H;
+  const bool need_echo = f.TC > 1 || !(f.stages & ART_STAGE_RAYTRACE);
+  for (int i = 0; i < fan_count; ++i) {
+    const art_fan& fn = fans[i];
+    memcpy(horg + 3 * i, fn.origin, 12);
+    uint8_t* rec = hb + (size_t)i * L.stride;
+    memcpy(rec + L.muffle_off, fn.muffle_ray_hits, (size_t)f.TC * f.T * 2);
+    memcpy(rec + L.perm_off, fn.permeation_power_remains, (size_t)f.TC * f.T * 4);
+    if (need_echo) {
+      memcpy(rec + L.echo_off, fn.echo_ray_distances, RH * 2);
+      if (L.has_hits) {
+        if (fn.ray_hit_points) memcpy(rec + L.hit_points_off, fn.ray_hit_points, RH * sizeof(art_half3));
+        else memset(rec + L.hit_points_off, 0, RH * sizeof(art_half3));
+      }
+    }
+    if (L.has_hits) {
+      if (fn.ray_hit_counts) memcpy(rec + L.hit_counts_off, fn.ray_hit_counts, (size_t)f.R);
+      else memset(rec + L.hit_counts_off, 0, (size_t)f.R);
+    }
+  }
+  const bool count = (c->flags & ART_CTX_COUNT_TESTS) != 0;
+  if (count) count_nonowned(c, d);
+  // shard fans over devices
+  const int nd = (int)c->devs.size();
+  for (int k = 0; k < nd; ++k) {
+    Device& dv = c->devs[k];
+    dv.fan_begin = (int)((long long)fan_count * k / nd);
+    dv.fan_count = (int)((long long)fan_count * (k + 1) / nd) - dv.fan_begin;
+  }
+  for (Device& dv : c->devs) {
+    rc = upload_scene(c, dv, f, hin);
+    if (rc) return rc;
+    if (dv.fan_count == 0) { HIP_TRY(c, hipEventRecord(dv.done, dv.stream)); continue; }
+    const size_t bbytes = (size_t)dv.fan_count * L.stride;
+    if (!dv.origins.reserve((size_t)dv.fan_count * 12) || !dv.block.reserve(bbytes))
+      return fail(c, ART_E_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(dv.origins.p, horg + 3 * dv.fan_begin, (size_t)dv.fan_count * 12, hipMemcpyHostToDevice, dv.stream));
+    uint8_t* hbs = hb + (size_t)dv.fan_begin * L.stride;
+    if (need_echo || L.has_hits) {
+      HIP_TRY(c, hipMemcpyAsync(dv.block.p, hbs, bbytes, hipMemcpyHostToDevice, dv.stream));
+    } else {  // only the muffle + permeation slot arrays (adjacent in the record)
+      HIP_TRY(c, hipMemcpy2DAsync(static_cast<uint8_t*>(dv.block.p) + L.muffle_off, L.stride, hbs + L.muffle_off, L.stride,
+                                  L.echo_off - L.muffle_off, dv.fan_count, hipMemcpyHostToDevice, dv.stream));
+    }
+    rc = enqueue_kernels(c, dv, f, static_cast<const float*>(dv.origins.p), dv.fan_count, static_cast<uint8_t*>(dv.block.p),
+                         dv.stream, count);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(hbs, dv.block.p, bbytes, hipMemcpyDeviceToHost, dv.stream));
+    HIP_TRY(c, hipEventRecord(dv.done, dv.stream));
+  }
+  c->fans.assign(fans, fans + fan_count);
+  c->counted = count;
+  c->inflight = true;
+  c->handle = c->next_handle++;
+  *out = c->handle;
+  return ART_OK;
+}
+
+ART_API int art_is_completed(art_ctx* c, art_handle h) {
+  if (!c) return ART_E_INVALID;
+  if (!c->inflight || h != c->handle) return (h != 0 && h < c->next_handle) ? 1 : fail(c, ART_E_STATE, "unknown handle");
+  for (Device& dv : c->devs) {
+    (void)hipSetDevice(dv.id);
+    hipError_t e = hipEventQuery(dv.done);
+    if (e == hipErrorNotReady) return 0;
+    if (e != hipSuccess) return fail(c, ART_E_DEVICE, "hipEventQuery: %s", hipGetErrorString(e));
+  }
+  return 1;
+}
+
+ART_API int art_complete(art_ctx* c, art_handle h) {
+  if (!c) return ART_E_INVALID;
+  if (!c->inflight || h != c->handle) {
+    if (h != 0 && h < c->next_handle) return ART_OK;  // already completed (JobHandle.Complete is idempotent)
+    return fail(c, ART_E_STATE, "unknown handle");
+  }
+  c->inflight = false;
+  for (Device& dv : c->devs) {
+    HIP_TRY(c, hipSetDevice(dv.id));
+    HIP_TRY(c, hipEventSynchronize(dv.done));
+  }
+  const Frame& f = c->fr;
+  const FanLayout& L = f.L;
+  const size_t RH = (size_t)f.R * f.H;
+  const uint8_t* hb = static_cast<const uint8_t*>(c->h_block.p);
+  for (size_t i = 0; i < c->fans.size(); ++i) {
+    const art_fan& fn = c->fans[i];
+    const uint8_t* rec = hb + i * L.stride;
+    if (f.stages & ART_STAGE_REDUCE)  // otherwise AudioTargetSettings keep the caller's contents
+      memcpy(fn.settings, rec + L.settings_off, (size_t)f.T * sizeof(art_target_settings));
+    if (L.has_dsp && fn.dsp_params) memcpy(fn.dsp_params, rec + L.dsp_off, (size_t)f.T * sizeof(art_dsp_params));
+    memcpy(fn.muffle_ray_hits, rec + L.muffle_off, (size_t)f.TC * f.T * 2);
+    memcpy(fn.permeation_power_remains, rec + L.perm_off, (size_t)f.TC * f.T * 4);
+    memcpy(fn.echo_ray_distances, rec + L.echo_off, RH * 2);
+    if (L.has_hits && fn.ray_hit_points) memcpy(fn.ray_hit_points, rec + L.hit_points_off, RH * sizeof(art_half3));
+    if (L.has_hits && fn.ray_hit_counts) memcpy(fn.ray_hit_counts, rec + L.hit_counts_off, (size_t)f.R);
+  }
+  if (c->counted) {
+    memset(&c->last_counts, 0, sizeof c->last_counts);
+    for (Device& dv : c->devs) {
+      if (dv.fan_count == 0) continue;
+      HIP_TRY(c, hipSetDevice(dv.id));
+      int rc = read_counts(c, dv, dv.stream, &c->last_counts, true);
+      if (rc) return rc;
+    }
+    c->has_counts = true;
+  }
+  return ART_OK;
+}
+
+ART_API int art_last_test_counts(art_ctx* c, art_test_counts* out) {
+  if (!c || !out) return ART_E_INVALID;
+  if (!c->has_counts) return fail(c, ART_E_STATE, "no counted frame yet (set ART_CTX_COUNT_TESTS)");
+  *out = c->last_counts;
+  return ART_OK;
+}
+
+// ---------------------------------------------------------------------------- device-resident
+ART_API int art_scene_bind(art_ctx* c, const art_frame_desc* d) {
+  if (!c) return ART_E_INVALID;
+  int rc = validate_desc(c, d);
+  if (rc) return rc;
+  Frame& f = c->fr;
+  make_frame(d, 0u, f);
+  if (!c->h_in.reserve(f.raw_bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  pack_inputs(d, f, static_cast<uint8_t*>(c->h_in.p));
+  count_nonowned(c, d);
+  for (Device& dv : c->devs) {
+    rc = upload_scene(c, dv, f, static_cast<const uint8_t*>(c->h_in.p));
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(dv.stream));
+  }
+  return ART_OK;
+}
+
+static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, void* d_block, uint32_t out_flags,
+                         void* stream, bool count, art_test_counts* out) {
+  if (!c) return ART_E_INVALID;
+  if (c->devs.empty() || !c->devs[0].bound) return fail(c, ART_E_STATE, "no scene bound (art_scene_bind)");
+  if (fan_count < 0 || (fan_count > 0 && (!d_origins || !d_block))) return fail(c, ART_E_INVALID, "bad device buffers");
+  Device& dv = c->devs[0];
+  HIP_TRY(c, hipSetDevice(dv.id));
+  Frame& f = c->fr;
+  // the bound frame's layout is for out_flags = 0; refresh for the requested outputs
+  f.L.has_hits = (out_flags & ART_OUT_HIT_RESULTS) ? 1 : 0;
+  {
+    art_frame_desc tmp{};
+    tmp.ray_count = f.R; tmp.max_hits_per_ray = f.H; tmp.audio_target_count = f.T; tmp.batch_slots = f.TC;
+    tmp.stages = f.stages;
+    f.L = make_layout(&tmp, out_flags);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL is the HIP default stream (torch's default)
+  int rc = enqueue_kernels(c, dv, f, d_origins, fan_count, static_cast<uint8_t*>(d_block), st, count);
+  if (rc) return rc;
+  if (count) return read_counts(c, dv, st, out, false);
+  return ART_OK;
+}
+
+ART_API int art_launch_device(art_ctx* c, const float* d_origins, int32_t fan_count, void* d_block, uint32_t out_flags,
+                              void* stream) {
+  return launch_common(c, d_origins, fan_count, d_block, out_flags, stream, false, nullptr);
+}
+
+ART_API int art_count_device(art_ctx* c, const float* d_origins, int32_t fan_count, void* d_block, uint32_t out_flags,
+                             void* stream, art_test_counts* out) {
+  if (!out) return ART_E_INVALID;
+  return launch_common(c, d_origins, fan_count, d_block, out_flags, stream, true, out);
+}
+
+ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {
+  if (!c || !out) return ART_E_INVALID;
+  memset(out, 0, sizeof *out);
+  for (Device& dv : c->devs) {
+    HIP_TRY(c, hipSetDevice(dv.id));
+    int frames = 0;
+    for (auto& u : dv.ev_used) {
+      hipEvent_t a = dv.ev_pool[u.second], b = dv.ev_pool[u.second + 1];
+      HIP_TRY(c, hipEventSynchronize(b));
+      float ms = 0.0f;
+      HIP_TRY(c, hipEventElapsedTime(&ms, a, b));
+      if (u.first == 0) { out->raytrace_ms += ms; frames++; }
+      else if (u.first == 1) out->permeate_ms += ms;
+      else out->reduce_ms += ms;
+    }
+    dv.ev_used.clear();
+    out->launches += frames;
+  }
+  return ART_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// art_internal.hpp — device-side records and kernel launch interface (internal to libart.so).
+//
+// Data layout in HBM (one scene = one contiguous device allocation):
+//   SphereRec[ns] | AabbRec[na] | ObbRec[no] | targets float3[T] | dirs half3[R] | curves
+// Records are 16-B aligned so the wave-uniform collider loop fetches them with scalar
+// (SMEM) loads: every lane of a wave tests the same collider at the same time, so the collider
+// lives in SGPRs and costs no VGPRs, LDS traffic or vector-memory bandwidth.
+#pragma once
+
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/art.h"
+
+namespace art {
+
+constexpr int kMaxTargets = 256;
+constexpr int kRtBlock = 256;
+
+enum : int { kNone = 0, kAabb = 1, kObb = 2, kSphere = 3 };  // Enums/ColliderType.cs:4-10
+
+// Hot fields first (read in the intersection loops), cold fields after (reflection / echo).
+struct alignas(16) SphereRec {  // 32 B
+  float cx, cy, cz, r2;         // r2 = Radius * Radius (AudioRaytracerJobBatched.cs:328)
+  int tid;                      // AudioTargetId
+  float density, absorption, echo;
+};
+struct alignas(16) AabbRec {  // 64 B
+  float mnx, mny, mnz;        // Center - halfExtents (:286)
+  int tid;
+  float mxx, mxy, mxz;        // Center + halfExtents (:287)
+  float density;
+  float cx, cy, cz, absorption;
+  float hx, hy, hz, echo;
+};
+struct alignas(16) ObbRec {  // 96 B
+  float cx, cy, cz;
+  int tid;
+  float qx, qy, qz, qw;        // stored rotation, decoded + normalized (halfQuaternion.cs:34-46)
+  float lmnx, lmny, lmnz;      // float3.zero - halfExtents (:319 -> :286)
+  float density;
+  float lmxx, lmxy, lmxz;      // float3.zero + halfExtents
+  float absorption;
+  float iqx, iqy, iqz, iqw;    // inverse(stored) (ReflectRay :489, permeation ShootRayCast :174)
+  float hx, hy, hz, echo;
+};
+
+struct DevScene {
+  const SphereRec* sph; int ns;
+  const AabbRec* aabb; int na;
+  const ObbRec* obb; int no;
+  const float* targets; int T;    // float3[T]
+  const uint16_t* dirs; int R;    // half3[R] as 3 x u16
+};
+
+// Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
+struct FanLayout {
+  uint32_t stride;
+  uint32_t settings_off, dsp_off, muffle_off, perm_off, echo_off, hit_points_off, hit_counts_off;
+  int has_dsp, has_hits;
+};
+
+struct FrameParams {
+  int S;          // fans in this launch
+  int R, H, T, TC, bs, nb;
+  float max_life, max_muffle;
+  float muffle_eff, perm_strength, perm_eff, max_reverb;
+  uint32_t stages;
+  // DSP
+  float dl_min, dl_max, db_min, db_max, mc_min, mc_max;
+  const float* vol_curve; int vol_n; float vol_len;
+  const float* muf_curve; int muf_n; float muf_len;
+  int sample_rate;
+};
+
+// Device counters for the counting variant, in art_test_counts order.
+struct DevCounts { unsigned long long v[9]; };
+
+// --- launchers (art_kernels.hip) ---
+void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, const art_obb* obb, int no,
+                 SphereRec* osph, AabbRec* oaabb, ObbRec* oobb, hipStream_t st);
+void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                     uint8_t* block, uint32_t* muffle_acc, DevCounts* counts, hipStream_t st);
+void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st);
+int fast_split(int S, int R);
+void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                     uint8_t* block, const int2* slot_batch, hipStream_t st);
+void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,
+                       unsigned long long* nhit, hipStream_t st);
+void launch_reduce(const DevScene& sc, const FrameParams& fp, const FanLayout& L, uint8_t* block,
+                   const uint32_t* muffle_acc, const uint8_t* muffle_reset, hipStream_t st);
+
+}  // namespace art

@@ -1,0 +1,490 @@
+// art_kernels.hip — CDNA4 (gfx950) kernels for the audio ray-tracing hot path.
+//
+//   prep_kernel      half AoS colliders -> fp32 SoA records (decode + per-collider precompute)
+//   raytrace_kernel  AudioRaytracerJobBatched.Execute   (Jobs/AudioRaytracerJobBatched.cs:61-215)
+//   permeate_kernel  AudioPermeationJobBatched.Execute  (Jobs/AudioPermeationJobBatched.cs:34-91)
+//   reduce_kernel    ProcessAudioDataJob.Execute        (Jobs/ProcessAudioDataJob.cs:32-76)
+//                    + DSP parameters                   (AudioSpatializer.cs:58, ReverbDSP.cs:105,
+//                                                        MuffleDSP.cs:140-160)
+//
+// Mapping: one lane per (fan, ray). All lanes of a wave sweep the collider arrays in the same
+// order, so every collider record is wave-uniform and is fetched with scalar loads into SGPRs.
+// Any-hit loops (echo / muffle visibility) exit per lane at the first blocker; the wave leaves
+// the loop as soon as its last lane has exited (exec mask empty).
+//
+// Bit-exactness: compiled with -ffp-contract=off, IEEE division/sqrt, f32 denormals on.
+// See unity_math.hpp and DESIGN.md §5 for the arguments behind each deviation from a literal
+// transcription (hoisted 1/d, per-collider precompute, IEEE minNum/maxNum in sweep loops).
+#include <float.h>
+#include <hip/hip_runtime.h>
+
+#include "art_device_fns.hpp"
+
+#pragma clang fp contract(off)
+
+namespace art {
+
+// ------------------------------------------------------------------------------------------
+// prep: decode colliders once per upload. Every value is computed exactly as the reference
+// computes it per access (Center - Size, Radius * Radius, halfQuaternion decode, inverse), so
+// hoisting is bit-identical.
+// ------------------------------------------------------------------------------------------
+__global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const art_aabb* __restrict__ aabb, int na,
+                            const art_obb* __restrict__ obb, int no, SphereRec* __restrict__ osph,
+                            AabbRec* __restrict__ oaabb, ObbRec* __restrict__ oobb) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < ns) {
+    art_sphere s = sph[i];
+    SphereRec r;
+    r.cx = f16tof32(s.center.x); r.cy = f16tof32(s.center.y); r.cz = f16tof32(s.center.z);
+    float rad = f16tof32(s.radius);
+    r.r2 = rad * rad;
+    r.tid = s.audio_target_id;
+    r.density = f16tof32(s.material.density);
+    r.absorption = f16tof32(s.material.absorption);
+    r.echo = f16tof32(s.material.echo);
+    osph[i] = r;
+    return;
+  }
+  i -= ns;
+  if (i < na) {
+    art_aabb a = aabb[i];
+    AabbRec r;
+    r.cx = f16tof32(a.center.x); r.cy = f16tof32(a.center.y); r.cz = f16tof32(a.center.z);
+    r.hx = f16tof32(a.size.x); r.hy = f16tof32(a.size.y); r.hz = f16tof32(a.size.z);
+    r.mnx = r.cx - r.hx; r.mny = r.cy - r.hy; r.mnz = r.cz - r.hz;
+    r.mxx = r.cx + r.hx; r.mxy = r.cy + r.hy; r.mxz = r.cz + r.hz;
+    r.tid = a.audio_target_id;
+    r.density = f16tof32(a.material.density);
+    r.absorption = f16tof32(a.material.absorption);
+    r.echo = f16tof32(a.material.echo);
+    oaabb[i] = r;
+    return;
+  }
+  i -= na;
+  if (i < no) {
+    art_obb b = obb[i];
+    ObbRec r;
+    r.cx = f16tof32(b.center.x); r.cy = f16tof32(b.center.y); r.cz = f16tof32(b.center.z);
+    r.hx = f16tof32(b.size.x); r.hy = f16tof32(b.size.y); r.hz = f16tof32(b.size.z);
+    r.lmnx = 0.0f - r.hx; r.lmny = 0.0f - r.hy; r.lmnz = 0.0f - r.hz;
+    r.lmxx = 0.0f + r.hx; r.lmxy = 0.0f + r.hy; r.lmxz = 0.0f + r.hz;
+    quat q = half_quaternion_value(b.rot_x, b.rot_y, b.rot_z);
+    quat qi = qinverse(q);
+    r.qx = q.x; r.qy = q.y; r.qz = q.z; r.qw = q.w;
+    r.iqx = qi.x; r.iqy = qi.y; r.iqz = qi.z; r.iqw = qi.w;
+    r.tid = b.audio_target_id;
+    r.density = f16tof32(b.material.density);
+    r.absorption = f16tof32(b.material.absorption);
+    r.echo = f16tof32(b.material.echo);
+    oobb[i] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// raytrace — AudioRaytracerJobBatched.Execute :61-215. grid = (ray blocks, fans).
+// ------------------------------------------------------------------------------------------
+template <bool COUNT, bool HITS>
+__global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FrameParams fp, FanLayout L,
+                                                            const float* __restrict__ origins, uint8_t* __restrict__ block,
+                                                            uint32_t* __restrict__ muffle_acc, DevCounts* counts) {
+  __shared__ uint32_t s_muf[kMaxTargets];
+  const int fan = blockIdx.y;
+  const int ray = blockIdx.x * blockDim.x + threadIdx.x;
+  const int T = fp.T;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) s_muf[t] = 0;
+  // batch slot of this block's rays (batchId = rayStart * TC / R, :63-64)
+  const int first_ray = blockIdx.x * blockDim.x;
+  const int last_ray = min(first_ray + (int)blockDim.x, fp.R) - 1;
+  auto slot_of = [&](int r) { int st = (r / fp.bs) * fp.bs; return (int)(((long long)st * fp.TC) / fp.R); };
+  const bool uniform_slot = slot_of(first_ray) == slot_of(last_ray);
+  __syncthreads();
+
+  LaneCounts lc = {0, 0, 0};
+  uint8_t* fb = block + (size_t)fan * L.stride;
+  if (ray < fp.R) {
+    uint16_t* echo = reinterpret_cast<uint16_t*>(fb + L.echo_off);
+    art_half3* hpo = reinterpret_cast<art_half3*>(fb + L.hit_points_off);
+    const int H = fp.H;  // <= 32 (validated on the host)
+    const int my_slot = slot_of(ray);
+    // Reset of this ray's slots (:72-80) under sequential-batch semantics. At TC == 1 every slot
+    // is reset and nothing is frozen. frozen bit k: a later batch's reset zeroes slot k after
+    // this ray wrote it, so the ray's own write must not land.
+    uint32_t frozen = 0;
+    {
+      const int my_batch = ray / fp.bs;
+      const art_half3 z = {0, 0, 0};
+      for (int k = 0; k < H; ++k) {
+        const int j = ray * H + k;
+        bool any_reset;
+        const int keep = batch_slot_state(fp, j, my_batch, any_reset);
+        if (!keep) frozen |= 1u << k;
+        if (!keep || any_reset) {
+          echo[j] = 0;
+          if (HITS) hpo[j] = z;
+        }
+      }
+    }
+    const vec3 O = load3(origins, fan);
+    vec3 o = O;
+    vec3 d = load_dir(sc.dirs, ray);
+    float life = fp.max_life;
+    int hits = 0;
+    bool alive = true;
+
+    while (alive) {
+      Seg s = make_seg(o, d);
+      Hit h = nearest<false, COUNT>(sc, s, lc);
+      if (h.type == kNone) break;                       // :200-207
+      o = o + d * h.dist;                               // :111
+      life -= h.dist;                                   // :112
+      hits += 1;                                        // :113
+      const int k = hits - 1;
+      const int rid = ray * H + k;                      // :115
+      const bool live_slot = !((frozen >> k) & 1u);
+      if (HITS && live_slot) {                          // :118, :197
+        art_half3 p;
+        p.x = f32tof16(o.x); p.y = f32tof16(o.y); p.z = f32tof16(o.z);
+        hpo[rid] = p;
+      }
+      // Echo — :124-145
+      vec3 off = o - d * kEps;
+      vec3 rdir = normalize(O - off);
+      float dist0 = distance(O, o);
+      if (visible<false, COUNT>(sc, make_seg(off, rdir), dist0, -1, lc) && live_slot) {
+        float em = h.type == kSphere ? sc.sph[h.idx].echo : (h.type == kAabb ? sc.aabb[h.idx].echo : sc.obb[h.idx].echo);
+        echo[rid] = f32tof16(dist0 * em);               // Half.Multiply, HalfDataTypesUtility.cs:86-90
+      }
+      // Muffle — :150-173
+      for (int t = 0; t < T; ++t) {
+        vec3 tp = load3(sc.targets, t);
+        vec3 tdir = normalize(tp - off);
+        float dt = distance(off, tp);
+        if (dt < fp.max_muffle && visible<true, COUNT>(sc, make_seg(off, tdir), dt, t, lc)) {
+          if (uniform_slot) atomicAdd(&s_muf[t], 1u);
+          else atomicAdd(&muffle_acc[((size_t)fan * fp.TC + my_slot) * T + t], 1u);
+        }
+      }
+      // Termination / reflection — :179-193, ReflectRay :456-532
+      if (hits >= H || life <= 0.0f) {
+        alive = false;
+      } else {
+        vec3 n = mk3(0.0f, 0.0f, 0.0f);
+        float absorption = 0.0f;
+        if (h.type == kAabb) {
+          const AabbRec b = sc.aabb[h.idx];
+          vec3 lp = o - mk3(b.cx, b.cy, b.cz);
+          vec3 ap = abs3(lp);
+          float dx = b.hx - ap.x, dy = b.hy - ap.y, dz = b.hz - ap.z;
+          if (dx < dy && dx < dz) n.x = usign(lp.x);
+          else if (dy < dx && dy < dz) n.y = usign(lp.y);
+          else n.z = usign(lp.z);
+          absorption = b.absorption;
+        } else if (h.type == kObb) {
+          const ObbRec b = sc.obb[h.idx];
+          vec3 lh = qmul(inverse_q(b), o - mk3(b.cx, b.cy, b.cz));
+          vec3 ap = abs3(lh);
+          vec3 df = mk3(b.hx, b.hy, b.hz) - ap;
+          vec3 ln = mk3(0.0f, 0.0f, 0.0f);
+          if (df.x < df.y && df.x < df.z) ln.x = usign(lh.x);
+          else if (df.y < df.x && df.y < df.z) ln.y = usign(lh.y);
+          else ln.z = usign(lh.z);
+          n = qmul(stored_q(b), ln);
+          absorption = b.absorption;
+        } else {
+          const SphereRec c = sc.sph[h.idx];
+          n = normalize(o - mk3(c.cx, c.cy, c.cz));
+          absorption = c.absorption;
+        }
+        d = reflect(d, n);                               // :525
+        o = o + d * kEps;                                // :528
+        life -= fp.max_life * absorption;                // :531
+        if (life < 0.0f) alive = false;                  // :189
+      }
+    }
+    if (HITS) fb[L.hit_counts_off + ray] = (uint8_t)hits;  // :204, :212
+  }
+
+  __syncthreads();
+  if (uniform_slot) {
+    const int slot = slot_of(first_ray);
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+      if (s_muf[t]) atomicAdd(&muffle_acc[((size_t)fan * fp.TC + slot) * T + t], s_muf[t]);
+  }
+  if (COUNT) {
+    unsigned long long vs = wave_sum_u32(lc.s), va = wave_sum_u32(lc.a), vo = wave_sum_u32(lc.o);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&counts->v[0], vs); atomicAdd(&counts->v[1], va); atomicAdd(&counts->v[2], vo);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// permeate — AudioPermeationJobBatched.Execute :34-91. grid = (slots TC, fans), 256 threads.
+// Each hitting ray OVERWRITES PermeationPowerRemains[slot*T+t] (:85), so a slot's final value is
+// the one of the highest-index hitting ray of the last batch that maps to it (App. B Q7). The
+// kernel finds that ray by sweeping the batch from its end, then evaluates its T loss rays; the
+// per-collider loss terms are computed in parallel and summed serially in reference order.
+// ------------------------------------------------------------------------------------------
+constexpr int kPermBlock = 256;
+
+__device__ __forceinline__ float perm_term_sphere(const Seg& s, const SphereRec& c) {
+  // RayIntersectsSpherePermeation :303-328
+  vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
+  float b = dot(oc, s.d);
+  float cc = dot(oc, oc) - c.r2;
+  float disc = b * b - cc;
+  if (disc < 0.0f) return 0.0f;
+  float sq = sqrtf(disc);
+  float tEnter = -b - sq, tExit = -b + sq;
+  if (tExit < 0.0f) return 0.0f;
+  float enter = umax(tEnter, 0.0f);
+  return umax(0.0f, tExit - enter) * c.density;
+}
+__device__ __forceinline__ float perm_term_slab(float ox, float oy, float oz, float ix, float iy, float iz, float mnx,
+                                                float mny, float mnz, float mxx, float mxy, float mxz, float density) {
+  // RayIntersectsAABBPermeation :265-288
+  float tEnter, tExit;
+  if (!slab<false>(ox, oy, oz, ix, iy, iz, mnx, mny, mnz, mxx, mxy, mxz, tEnter, tExit)) return 0.0f;
+  float enter = umax(tEnter, 0.0f);
+  return umax(0.0f, tExit - enter) * density;
+}
+
+__global__ __launch_bounds__(kPermBlock) void permeate_kernel(DevScene sc, FrameParams fp, FanLayout L,
+                                                              const float* __restrict__ origins, uint8_t* __restrict__ block,
+                                                              const int2* __restrict__ slot_batch) {
+  __shared__ int s_best;
+  __shared__ Hit s_hit;
+  __shared__ float s_terms[kPermBlock];
+  const int fan = blockIdx.y, slot = blockIdx.x, tid = threadIdx.x;
+  const int2 br = slot_batch[slot];
+  if (br.y <= br.x) return;  // no batch maps to this slot: value stays (stale / uninitialized, Q7)
+  const vec3 O = load3(origins, fan);
+  LaneCounts lc = {0, 0, 0};
+
+  // Phase 1: highest-index ray in [br.x, br.y) whose first hit exists (ShootRayCast :58).
+  int found = -1;
+  for (int end = br.y; end > br.x; end -= kPermBlock) {
+    const int ray = end - 1 - tid;
+    Hit h;
+    h.type = kNone;
+    if (ray >= br.x) h = nearest<true, false>(sc, make_seg(O, load_dir(sc.dirs, ray)), lc);
+    if (tid == 0) s_best = 0x7fffffff;
+    __syncthreads();
+    if (h.type != kNone) atomicMin(&s_best, tid);
+    __syncthreads();
+    const int b = s_best;
+    if (b != 0x7fffffff && tid == b) s_hit = h;
+    __syncthreads();
+    if (b != 0x7fffffff) { found = end - 1 - b; break; }
+  }
+
+  float* ppr = reinterpret_cast<float*>(block + (size_t)fan * L.stride + L.perm_off);
+  const int T = fp.T;
+  if (found < 0) {  // reset (:43-46) and no ray hit: zeros
+    for (int t = tid; t < T; t += kPermBlock) ppr[slot * T + t] = 0.0f;
+    return;
+  }
+  // Phase 2: T loss rays of the found ray (:61-85)
+  const vec3 d = load_dir(sc.dirs, found);
+  const vec3 o = O + d * s_hit.dist;
+  const int ctot = sc.ns + sc.na + sc.no;
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int t = 0; t < T; ++t) {
+    const vec3 off = o - d * kEps;
+    const vec3 tdir = normalize(load3(sc.targets, t) - off);
+    const Seg s = make_seg(off, tdir);
+    float sum = 0.0f;  // uniform in wave 0
+    for (int base = 0; base < ctot; base += kPermBlock) {
+      const int c = base + tid;
+      float term = 0.0f;
+      if (c < sc.ns) {
+        const SphereRec r = sc.sph[c];
+        if (r.tid != t) term = perm_term_sphere(s, r);
+      } else if (c < sc.ns + sc.na) {
+        const AabbRec r = sc.aabb[c - sc.ns];
+        if (r.tid != t) term = perm_term_slab(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.mnx, r.mny, r.mnz, r.mxx, r.mxy, r.mxz, r.density);
+      } else if (c < ctot) {
+        const ObbRec r = sc.obb[c - sc.ns - sc.na];
+        if (r.tid != t) {
+          quat q = stored_q(r);  // RayIntersectsOBBPermeation :294-300 uses the stored rotation
+          vec3 lo = qmul(q, s.o - mk3(r.cx, r.cy, r.cz));
+          vec3 ld = qmul(q, s.d);
+          term = perm_term_slab(lo.x, lo.y, lo.z, 1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z, r.lmnx, r.lmny, r.lmnz, r.lmxx,
+                                r.lmxy, r.lmxz, r.density);
+        }
+      }
+      s_terms[tid] = term;
+      __syncthreads();
+      if (wave == 0) {
+        // Serial, in collider order: only non-zero terms change the sum (x + ±0 == x for x != -0,
+        // and the running sum starts at +0).
+        for (int w = 0; w < kPermBlock / 64; ++w) {
+          float v = s_terms[w * 64 + lane];
+          unsigned long long m = __ballot(v != 0.0f);
+          while (m) {
+            int j = __builtin_ctzll(m);
+            m &= m - 1;
+            sum += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (tid == 0) ppr[slot * T + t] = (float)fp.R * fp.perm_strength - sum;  // :260
+  }
+}
+
+// Counting pass for the permeation job (test-count metric only, never timed): every ray runs
+// ShootRayCast over all colliders (:58); each hitting ray then runs T loss rays over the
+// non-owned colliders (:67-86), whose count the host derives from the number of hitting rays.
+__global__ __launch_bounds__(kPermBlock) void perm_count_kernel(DevScene sc, FrameParams fp, const float* __restrict__ origins,
+                                                                DevCounts* counts, unsigned long long* nhit) {
+  const int fan = blockIdx.y, ray = blockIdx.x * blockDim.x + threadIdx.x;
+  LaneCounts lc = {0, 0, 0};
+  uint32_t hit = 0;
+  if (ray < fp.R) {
+    Hit h = nearest<true, true>(sc, make_seg(load3(origins, fan), load_dir(sc.dirs, ray)), lc);
+    hit = h.type != kNone;
+  }
+  unsigned long long vs = wave_sum_u32(lc.s), va = wave_sum_u32(lc.a), vo = wave_sum_u32(lc.o), vh = wave_sum_u32(hit);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&counts->v[3], vs); atomicAdd(&counts->v[4], va); atomicAdd(&counts->v[5], vo);
+    atomicAdd(nhit, vh);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// reduce — ProcessAudioDataJob.Execute :32-76 + AudioTargetRTSettings ctor + DSP parameters.
+// One wave per fan. The echo sum is sequential in index order (App. A.4): non-zero halves are
+// added one by one in order; zeros are counted as "returned" (Q4).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float curve_eval(const float* baked, int n, float length, float time) {
+  float percent = time / length;
+  float cp = umax(0.0f, umin((float)(n - 1), percent * (float)(n - 1)));
+  int fi = (int)floorf(cp), ci = (int)ceilf(cp);
+  return ulerp(baked[fi], baked[ci], cp - (float)fi);
+}
+
+__global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp, FanLayout L, uint8_t* __restrict__ block,
+                                                    const uint32_t* __restrict__ muffle_acc,
+                                                    const uint8_t* __restrict__ muffle_reset) {
+  const int fan = blockIdx.x, lane = threadIdx.x;
+  uint8_t* fb = block + (size_t)fan * L.stride;
+  const int T = fp.T, TC = fp.TC;
+  uint16_t* muf = reinterpret_cast<uint16_t*>(fb + L.muffle_off);
+  // MuffleRayHits (u16 wrap, :171) from the raytrace accumulators; slots no batch reset keep their value (Q18).
+  if (fp.stages & ART_STAGE_RAYTRACE)
+    for (int i = lane; i < TC * T; i += 64)
+      if (muffle_reset[i / T]) muf[i] = (uint16_t)muffle_acc[(size_t)fan * TC * T + i];
+  if (!(fp.stages & ART_STAGE_REDUCE)) return;
+  __syncthreads();
+
+  const uint16_t* echo = reinterpret_cast<const uint16_t*>(fb + L.echo_off);
+  const int n = fp.R * fp.H;
+  float total = 0.0f;
+  uint32_t zeros = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool in = i < n;
+    const float e = in ? f16tof32(echo[i]) : 0.0f;
+    zeros += __popcll(__ballot(in && e == 0.0f));
+    unsigned long long m = __ballot(in && e != 0.0f);
+    while (m) {
+      int j = __builtin_ctzll(m);
+      m &= m - 1;
+      total += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, e), j));
+    }
+  }
+  // echoRayReturnedHits is a float incremented by 1 (exact below 2^24).
+  const float returned = (float)zeros;
+  const float avg = total / (float)n;
+  const float reverbStrength = avg / fp.max_reverb;
+  const float reverbVolume = returned / (float)n;
+
+  const float* ppr = reinterpret_cast<const float*>(fb + L.perm_off);
+  art_target_settings* st = reinterpret_cast<art_target_settings*>(fb + L.settings_off);
+  art_dsp_params* dp = reinterpret_cast<art_dsp_params*>(fb + L.dsp_off);
+  for (int t = lane; t < T; t += 64) {
+    int hitsum = 0;
+    float psum = 0.0f;
+    for (int i = 0; i < TC; ++i) { hitsum += muf[T * i + t]; psum += ppr[T * i + t]; }
+    float muffle = 1.0f - (float)hitsum / (float)(fp.R * fp.H) * fp.muffle_eff;        // :68
+    float perm = psum / (float)fp.R / fp.perm_strength * fp.perm_eff;                  // :69
+    muffle = usaturate(muffle - perm);                                                 // :71
+    art_target_settings s;
+    s.muffle_strength = usaturate(muffle);
+    s.reverb_strength = usaturate(reverbStrength);
+    s.reverb_volume = usaturate(reverbVolume);
+    s.perceived_position[0] = sc.targets[3 * t + 0];
+    s.perceived_position[1] = sc.targets[3 * t + 1];
+    s.perceived_position[2] = sc.targets[3 * t + 2];
+    st[t] = s;
+    if ((fp.stages & ART_STAGE_DSP_PARAMS) && L.has_dsp) {
+      const float DOUBLE_PI = 2.0f * 3.14159265f;
+      art_dsp_params p;
+      p.dry_level = ulerp(fp.dl_min, fp.dl_max, s.reverb_strength);
+      p.dry_boost = ulerp(fp.db_min, fp.db_max, curve_eval(fp.vol_curve, fp.vol_n, fp.vol_len, s.reverb_volume));
+      p.reserved = 0;
+      if (s.muffle_strength > 0.0f) {
+        float mc = curve_eval(fp.muf_curve, fp.muf_n, fp.muf_len, s.muffle_strength);
+        float cutoff = ulerp(fp.mc_max, fp.mc_min, mc);
+        float rc = 1.0f / (cutoff * DOUBLE_PI);
+        float dt = 1.0f / (float)fp.sample_rate;
+        p.muffle_cutoff = cutoff; p.muffle_alpha = dt / (rc + dt); p.muffle_active = 1;
+      } else {
+        p.muffle_cutoff = 0.0f; p.muffle_alpha = 0.0f; p.muffle_active = 0;
+      }
+      dp[t] = p;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, const art_obb* obb, int no,
+                 SphereRec* osph, AabbRec* oaabb, ObbRec* oobb, hipStream_t st) {
+  int n = ns + na + no;
+  if (n == 0) return;
+  hipLaunchKernelGGL(prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sph, ns, aabb, na, obb, no, osph, oaabb, oobb);
+}
+
+void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,
+                     uint32_t* muffle_acc, DevCounts* counts, hipStream_t st) {
+  if (fp.S == 0) return;
+  // Balance the per-fan ray range over ceil(R/256) blocks, rounded to whole waves.
+  int nblk = (fp.R + kRtBlock - 1) / kRtBlock;
+  int per = (fp.R + nblk - 1) / nblk;
+  int threads = ((per + 63) / 64) * 64;
+  nblk = (fp.R + threads - 1) / threads;
+  dim3 grid(nblk, fp.S), blk(threads);
+  if (counts) {
+    if (L.has_hits) hipLaunchKernelGGL((raytrace_kernel<true, true>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, counts);
+    else hipLaunchKernelGGL((raytrace_kernel<true, false>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, counts);
+  } else {
+    if (L.has_hits) hipLaunchKernelGGL((raytrace_kernel<false, true>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, counts);
+    else hipLaunchKernelGGL((raytrace_kernel<false, false>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, counts);
+  }
+}
+
+void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,
+                     const int2* slot_batch, hipStream_t st) {
+  if (fp.S == 0) return;
+  hipLaunchKernelGGL(permeate_kernel, dim3(fp.TC, fp.S), dim3(kPermBlock), 0, st, sc, fp, L, origins, block, slot_batch);
+}
+
+void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,
+                       unsigned long long* nhit, hipStream_t st) {
+  if (fp.S == 0) return;
+  hipLaunchKernelGGL(perm_count_kernel, dim3((fp.R + kPermBlock - 1) / kPermBlock, fp.S), dim3(kPermBlock), 0, st, sc, fp,
+                     origins, counts, nhit);
+}
+
+void launch_reduce(const DevScene& sc, const FrameParams& fp, const FanLayout& L, uint8_t* block, const uint32_t* muffle_acc,
+                   const uint8_t* muffle_reset, hipStream_t st) {
+  if (fp.S == 0) return;
+  hipLaunchKernelGGL(reduce_kernel, dim3(fp.S), dim3(64), 0, st, sc, fp, L, block, muffle_acc, muffle_reset);
+}
+
+}  // namespace art

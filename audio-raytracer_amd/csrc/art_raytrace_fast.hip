@@ -1,0 +1,368 @@
+// art_raytrace_fast.hip — the throughput raytrace kernel (AudioRaytracerJobBatched.Execute,
+// Jobs/AudioRaytracerJobBatched.cs:61-215), K-way collider split.
+//
+// Work shape: one workgroup = one group of 64 rays of one fan, processed by K waves. Every wave
+// holds the same 64 ray states (lane l <-> ray l of the group) and sweeps 1/K of each collider
+// array, so the colliders stay wave-uniform (SGPR records via scalar loads) while the launch
+// gets K times more waves than rays/64 — config 2 alone is only 2048 ray-waves (2 per SIMD).
+//   * nearest hit: each wave finds the first minimum of its chunk; the K partials are merged
+//     in LDS by (distance, global collider order), which reproduces the reference's strict-<
+//     first-minimum in Sphere, AABB, OBB order (ShootRayCast :225-280);
+//   * visibility (echo :124-145, muffle :150-173): any-hit is an OR over colliders, so each
+//     wave sweeps its chunk (4-way unrolled, no per-lane masking, wave exit once every lane is
+//     blocked) and ORs its verdict into an LDS bit per (ray, query).
+// Ray slots are visited in a direction-coherent order (ray_order) so the 64 rays of a group
+// point into a small solid angle and their visibility sweeps end together; every output is
+// written at the ray's own index, so the order changes no result.
+// This kernel does not count tests; the test-count metric comes from raytrace_kernel<COUNT>.
+#include "art_device_fns.hpp"
+
+namespace art {
+
+constexpr int kU = 4;  // sweep unroll
+constexpr int kNoHit = 0x7fffffff;
+
+__device__ __forceinline__ void chunk_of(int n, int w, int K, int& b, int& e) {
+  b = (int)(((long long)n * w) / K);
+  e = (int)(((long long)n * (w + 1)) / K);
+}
+
+// Sphere test split so the common miss costs no branch: the square root and the two IEEE
+// divisions run only for lanes whose discriminant is non-negative.
+__device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c, float& dist) {
+  vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
+  float b = 2.0f * dot(oc, s.d);
+  float cc = dot(oc, oc) - c.r2;
+  float disc = b * b - s.a4 * cc;
+  bool hit = false;
+  dist = 0.0f;
+  if (disc >= 0.0f) {
+    float sq = sqrtf(disc);
+    float t0 = (-b - sq) / s.a2;
+    float t1 = (-b + sq) / s.a2;
+    hit = (t0 >= 0.0f) || (t1 >= 0.0f);
+    dist = (t0 >= 0.0f) ? t0 : t1;
+  }
+  return hit;
+}
+
+// First minimum of this wave's chunk (ShootRayCast :225-280 restricted to a sub-range).
+// code = type rank (sphere 0, aabb 1, obb 2) << 28 | index: the global reference order.
+__device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, int w, int K, float& best, int& code) {
+  best = FLT_MAX;
+  code = kNoHit;
+  int b, e;
+  chunk_of(sc.ns, w, K, b, e);
+  int i = b;
+  for (; i + kU <= e; i += kU) {
+    SphereRec c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) c[u] = sc.sph[wave_uniform(i + u)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float d;
+      if (sphere_hit_dist(s, c[u], d) && d < best) { best = d; code = i + u; }
+    }
+  }
+  for (; i < e; ++i) {
+    const SphereRec c = sc.sph[wave_uniform(i)];
+    float d;
+    if (sphere_hit_dist(s, c, d) && d < best) { best = d; code = i; }
+  }
+  chunk_of(sc.na, w, K, b, e);
+  i = b;
+  for (; i + kU <= e; i += kU) {
+    AabbRec r[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) r[u] = sc.aabb[wave_uniform(i + u)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float d;
+      if (aabb_test<false>(s, r[u], d) && d < best) { best = d; code = (1 << 28) | (i + u); }
+    }
+  }
+  for (; i < e; ++i) {
+    const AabbRec r = sc.aabb[wave_uniform(i)];
+    float d;
+    if (aabb_test<false>(s, r, d) && d < best) { best = d; code = (1 << 28) | i; }
+  }
+  chunk_of(sc.no, w, K, b, e);
+  for (i = b; i < e; ++i) {
+    const ObbRec r = sc.obb[wave_uniform(i)];
+    float d;
+    if (obb_test<false>(s, r, stored_q(r), d) && d < best) { best = d; code = (2 << 28) | i; }
+  }
+}
+
+// OR over this wave's chunk of "collider blocks the segment before maxd"
+// (CanRaySeePoint :365-397, CanRaySeeAudioTarget :405-449 with the owner skip when SKIP).
+template <bool SKIP>
+__device__ __forceinline__ bool blocked_chunk(const DevScene& sc, const Seg& s, float maxd, int target, int w, int K,
+                                              bool blocked) {
+  if (__all(blocked)) return true;
+  int b, e;
+  chunk_of(sc.ns, w, K, b, e);
+  int i = b;
+  for (; i + kU <= e; i += kU) {
+    SphereRec c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) c[u] = sc.sph[wave_uniform(i + u)];
+    bool h = false;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float d;
+      bool x = sphere_hit_dist(s, c[u], d) && d < maxd;
+      if (SKIP) x = x && c[u].tid != target;
+      h |= x;
+    }
+    blocked |= h;
+    if (__all(blocked)) return true;
+  }
+  for (; i < e; ++i) {
+    const SphereRec c = sc.sph[wave_uniform(i)];
+    float d;
+    bool x = sphere_hit_dist(s, c, d) && d < maxd;
+    if (SKIP) x = x && c.tid != target;
+    blocked |= x;
+  }
+  if (__all(blocked)) return true;
+  chunk_of(sc.na, w, K, b, e);
+  i = b;
+  for (; i + kU <= e; i += kU) {
+    AabbRec r[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) r[u] = sc.aabb[wave_uniform(i + u)];
+    bool h = false;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float d;
+      bool x = aabb_test<false>(s, r[u], d) && d < maxd;
+      if (SKIP) x = x && r[u].tid != target;
+      h |= x;
+    }
+    blocked |= h;
+    if (__all(blocked)) return true;
+  }
+  for (; i < e; ++i) {
+    const AabbRec r = sc.aabb[wave_uniform(i)];
+    float d;
+    bool x = aabb_test<false>(s, r, d) && d < maxd;
+    if (SKIP) x = x && r.tid != target;
+    blocked |= x;
+  }
+  if (__all(blocked)) return true;
+  chunk_of(sc.no, w, K, b, e);
+  for (i = b; i < e; ++i) {
+    const ObbRec r = sc.obb[wave_uniform(i)];
+    float d;
+    bool x = obb_test<false>(s, r, stored_q(r), d) && d < maxd;
+    if (SKIP) x = x && r.tid != target;
+    blocked |= x;
+    if ((i & 3) == 3 && __all(blocked)) return true;
+  }
+  return blocked;
+}
+
+__device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
+  return type == kSphere ? sc.sph[idx].echo : (type == kAabb ? sc.aabb[idx].echo : sc.obb[idx].echo);
+}
+
+template <int K, bool HITS>
+__global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
+                                                               const float* __restrict__ origins,
+                                                               uint8_t* __restrict__ block,
+                                                               uint32_t* __restrict__ muffle_acc,
+                                                               const int* __restrict__ ray_order) {
+  __shared__ float s_dist[K][64];
+  __shared__ int s_code[K][64];
+  __shared__ uint32_t s_blk[64];
+  __shared__ uint32_t s_muf[kMaxTargets];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fan = blockIdx.y;
+  const int slot = blockIdx.x * 64 + lane;
+  const bool valid = slot < fp.R;
+  const int ray = valid ? ray_order[slot] : 0;
+  const int T = fp.T, H = fp.H;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) s_muf[t] = 0;
+  if (w == 0) s_blk[lane] = 0;
+
+  uint8_t* fb = block + (size_t)fan * L.stride;
+  uint16_t* echo = reinterpret_cast<uint16_t*>(fb + L.echo_off);
+  art_half3* hpo = reinterpret_cast<art_half3*>(fb + L.hit_points_off);
+  const bool single_slot = fp.TC == 1;
+  const int my_slot = (int)(((long long)((ray / fp.bs) * fp.bs) * fp.TC) / fp.R);  // batchId (:63-64)
+
+  // Reset (:72-80) with sequential-batch semantics; wave 0 owns every global write.
+  uint32_t frozen = 0;
+  if (valid) {
+    const int my_batch = ray / fp.bs;
+    const art_half3 z = {0, 0, 0};
+    for (int k = 0; k < H; ++k) {
+      const int j = ray * H + k;
+      bool any_reset;
+      const int keep = batch_slot_state(fp, j, my_batch, any_reset);
+      if (!keep) frozen |= 1u << k;
+      if (w == 0 && (!keep || any_reset)) {
+        echo[j] = 0;
+        if (HITS) hpo[j] = z;
+      }
+    }
+  }
+  __syncthreads();
+
+  const vec3 O = load3(origins, fan);
+  vec3 o = O;
+  vec3 d = load_dir(sc.dirs, valid ? ray : 0);
+  float life = fp.max_life;
+  int hits = 0;
+  bool alive = valid;
+
+  while (__any(alive)) {  // identical in every wave of the block -> uniform barriers
+    const Seg s = make_seg(o, d);
+    float best;
+    int code;
+    nearest_chunk(sc, s, w, K, best, code);
+    s_dist[w][lane] = best;
+    s_code[w][lane] = code;
+    __syncthreads();
+    float bd = s_dist[0][lane];
+    int bc = s_code[0][lane];
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+      const float dk = s_dist[k][lane];
+      const int ck = s_code[k][lane];
+      if (dk < bd || (dk == bd && ck < bc)) { bd = dk; bc = ck; }
+    }
+    const bool hit = alive && bc != kNoHit;
+    alive = hit;  // a miss ends the ray (:200-207)
+    int type = kNone, idx = 0;
+    float dist = bd;
+    if (hit) {
+      const int rank = bc >> 28;
+      idx = bc & 0x0fffffff;
+      type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
+      // exact (Unity min/max) re-evaluation: a zero distance keeps the reference's sign
+      if (type == kAabb) aabb_test<true>(s, sc.aabb[idx], dist);
+      if (type == kObb) { const ObbRec r = sc.obb[idx]; obb_test<true>(s, r, stored_q(r), dist); }
+      o = o + d * dist;  // :111
+      life -= dist;      // :112
+      hits += 1;         // :113
+    }
+    const int k = hits - 1;
+    const bool live_slot = hit && !((frozen >> k) & 1u);
+    if (HITS && w == 0 && live_slot) {  // :118, :197
+      art_half3 p;
+      p.x = f32tof16(o.x); p.y = f32tof16(o.y); p.z = f32tof16(o.z);
+      hpo[ray * H + k] = p;
+    }
+
+    // visibility queries: q = 0 echo ray to the origin, q = 1..T muffle rays to the targets
+    const vec3 off = o - d * kEps;                 // :124, :158
+    const float dist0 = distance(O, o);            // :130 (un-offset hit point)
+    uint32_t act = 0;
+    {
+      const Seg qs = make_seg(off, normalize(O - off));
+      const bool blk = blocked_chunk<false>(sc, qs, dist0, -1, w, K, !hit);
+      if (hit) act |= 1u;
+      if (hit && blk) atomicOr(&s_blk[lane], 1u);
+    }
+    for (int t = 0; t < T; ++t) {
+      const vec3 tp = load3(sc.targets, t);
+      const float dt = distance(off, tp);          // :165
+      const bool active = hit && dt < fp.max_muffle;  // :168
+      const Seg qs = make_seg(off, normalize(tp - off));
+      const bool blk = blocked_chunk<true>(sc, qs, dt, t, w, K, !active);
+      if (active) act |= 2u << t;
+      if (active && blk) atomicOr(&s_blk[lane], 2u << t);
+    }
+    __syncthreads();
+    const uint32_t m = s_blk[lane];
+    __syncthreads();
+    if (w == 0) {
+      s_blk[lane] = 0;
+      if (hit && !(m & 1u) && live_slot) echo[ray * H + k] = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
+      const uint32_t clear = act & ~m;
+      for (int t = 0; t < T; ++t) {
+        if ((clear >> (t + 1)) & 1u) {  // :171
+          if (single_slot) atomicAdd(&s_muf[t], 1u);
+          else atomicAdd(&muffle_acc[((size_t)fan * fp.TC + my_slot) * T + t], 1u);
+        }
+      }
+    }
+
+    // termination / reflection — :179-193, ReflectRay :456-532 (every wave, identical state)
+    if (hit) {
+      if (hits >= H || life <= 0.0f) {
+        alive = false;
+      } else {
+        vec3 n = mk3(0.0f, 0.0f, 0.0f);
+        float absorption = 0.0f;
+        if (type == kAabb) {
+          const AabbRec b = sc.aabb[idx];
+          vec3 lp = o - mk3(b.cx, b.cy, b.cz);
+          vec3 ap = abs3(lp);
+          float dx = b.hx - ap.x, dy = b.hy - ap.y, dz = b.hz - ap.z;
+          if (dx < dy && dx < dz) n.x = usign(lp.x);
+          else if (dy < dx && dy < dz) n.y = usign(lp.y);
+          else n.z = usign(lp.z);
+          absorption = b.absorption;
+        } else if (type == kObb) {
+          const ObbRec b = sc.obb[idx];
+          vec3 lh = qmul(inverse_q(b), o - mk3(b.cx, b.cy, b.cz));
+          vec3 ap = abs3(lh);
+          vec3 df = mk3(b.hx, b.hy, b.hz) - ap;
+          vec3 ln = mk3(0.0f, 0.0f, 0.0f);
+          if (df.x < df.y && df.x < df.z) ln.x = usign(lh.x);
+          else if (df.y < df.x && df.y < df.z) ln.y = usign(lh.y);
+          else ln.z = usign(lh.z);
+          n = qmul(stored_q(b), ln);
+          absorption = b.absorption;
+        } else {
+          const SphereRec c = sc.sph[idx];
+          n = normalize(o - mk3(c.cx, c.cy, c.cz));
+          absorption = c.absorption;
+        }
+        d = reflect(d, n);
+        o = o + d * kEps;
+        life -= fp.max_life * absorption;
+        if (life < 0.0f) alive = false;
+      }
+    }
+  }
+  if (HITS && valid && w == 0) fb[L.hit_counts_off + ray] = (uint8_t)hits;  // :204, :212
+  __syncthreads();
+  if (single_slot)
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+      if (s_muf[t]) atomicAdd(&muffle_acc[(size_t)fan * T + t], s_muf[t]);
+}
+
+// Waves per 64-ray group: enough waves to cover the chip (~24 per CU), at most 8.
+int fast_split(int S, int R) {
+  const long long groups = (long long)S * ((R + 63) / 64);
+  int K = 1;
+  while (K < 8 && groups * K < 256LL * 24) K *= 2;
+  return K;
+}
+
+template <int K>
+static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st) {
+  dim3 grid((fp.R + 63) / 64, fp.S), blk(64 * K);
+  if (L.has_hits)
+    hipLaunchKernelGGL((raytrace_fast_kernel<K, true>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, ray_order);
+  else
+    hipLaunchKernelGGL((raytrace_fast_kernel<K, false>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, ray_order);
+}
+
+void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st) {
+  if (fp.S == 0) return;
+  switch (fast_split(fp.S, fp.R)) {
+    case 1: launch_fast_k<1>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
+    case 2: launch_fast_k<2>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
+    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
+    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
+  }
+}
+
+}  // namespace art

@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: ray-collider tests/s + p50 per-frame batch ms (BASELINE.json "metric").
+
+Workload (N=1): BASELINE config 2 — 256 sources (fans) x 512 rays x 4096 colliders
+(2048 AABB + 2048 Sphere), T = 4 audio targets, maxBounces 0, stages raytrace + reduce.
+A "step" = one frame of the hot path over every fan of this rank, inputs resident in HBM,
+launched through the C ABI (art_launch_device) on torch's current HIP stream; with N > 1 each
+rank owns 256 fans (weak scaling) and the per-fan result blocks are all-gathered over RCCL.
+
+value = (tests executed by all ranks per frame, per the reference algorithm's counts) * K / max
+over ranks of the timed region. Test counts come from the counting variant of the kernels
+(art_count_device), which tests/test_parity_gpu.py checks against the oracle's counters.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
+torch.distributed.run (one process per GPU, MASTER_ADDR=127.0.0.1).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "audio-raytracer_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import art  # noqa: E402
+from art import abi  # noqa: E402
+
+# Algorithmic FP32 ops per test (SURVEY.md §8 d; miss path, IEEE add/sub/mul/div/sqrt/min/max/cmp = 1).
+OPS = {"rt_sphere": 26, "rt_aabb": 34, "rt_obb": 118, "perm_hit_sphere": 26, "perm_hit_aabb": 34, "perm_hit_obb": 134,
+       "perm_loss_sphere": 18, "perm_loss_aabb": 33, "perm_loss_obb": 117}
+FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW" (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", type=int, default=2)
+    p.add_argument("--frames", type=int, default=50, help="host-API frames for the p50 frame latency")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-fans", type=int, default=0, help="fans in the CPU-baseline sample (0 = auto)")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, scene, params, org, fans, threads):
+    """The oracle (C restatement of the reference jobs) timed on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle  # CPU baseline leg only
+
+    sub = np.ascontiguousarray(org[:fans])
+    out = art.FanOutputs(fans, cfg.R, cfg.H, cfg.T, 1)
+    oracle.load()
+    t0 = time.perf_counter()
+    _, counts = oracle.run(scene, params, sub, out, threads=threads)
+    dt = time.perf_counter() - t0
+    tests = sum(counts.values())
+    return tests / dt, dt, tests
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    cfg = art.CONFIGS[a.config]
+    S_total = cfg.S * world
+    scene, org_all, params = art.synth(cfg, S=S_total)
+    org = np.ascontiguousarray(org_all[rank * cfg.S:(rank + 1) * cfg.S])
+    S = cfg.S
+    ctx = art.Context(1 << torch.cuda.current_device())
+    out0 = art.FanOutputs(S, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+    frame = art.Frame(scene, params, org, out0)
+    lay = art.fan_layout(frame)
+    ctx.bind(frame)
+    d_org = torch.from_numpy(org).to(dev)
+    d_blk = torch.zeros(S * lay["stride"], dtype=torch.uint8, device=dev)
+    gathered = torch.empty(world * S * lay["stride"], dtype=torch.uint8, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    counts = ctx.count_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+    tests_rank = sum(counts.values())
+    rt_flops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
+
+    def step():
+        ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, d_blk)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
+    ctx.kernel_timing()  # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ktimes = ctx.kernel_timing()
+    ctx.set_flags(0)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tt = torch.tensor([tests_rank], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt)
+        tests_all = float(tt.item())
+    else:
+        tests_all = float(tests_rank)
+
+    # p50 per-frame latency through the Unity-facing API (host arrays, H2D + kernels + D2H)
+    frame_ms = []
+    if rank == 0:
+        for i in range(a.frames + 5):
+            t1 = time.perf_counter()
+            ctx.run(frame)
+            if i >= 5:
+                frame_ms.append((time.perf_counter() - t1) * 1e3)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    n_rt = max(1, ktimes["launches"])
+    rt_ms = ktimes["raytrace_ms"] / n_rt
+    achieved_tflops = rt_flops / (rt_ms * 1e-3) / 1e12
+    # algorithmic HBM bytes of one raytrace launch: collider AoS->SoA records are L2-resident after
+    # the first wave, so the compulsory traffic is the SoA records + dirs + origins + outputs.
+    rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 64 + scene.obbs.size * 96
+    alg_bytes = rec_bytes + cfg.R * 6 + S * 12 + S * lay["stride"]
+    hbm_gbs = alg_bytes / (rt_ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", f"traffic_config{cfg.index}.json")
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get("raytrace_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline:
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        fans = a.cpu_fans or max(threads, 16)
+        v, cdt, ctests = cpu_baseline(cfg, scene, params, org, fans, threads)
+        cpu = {"value": v, "unit": "ray-collider tests/s", "cores": threads, "kind": "port",
+               "sample": f"{fans} of {S} fans of config {cfg.index} ({ctests} tests, {cdt:.1f} s) through the C "
+                         f"oracle (oracle/art_oracle.c, gcc -O3 -ffp-contract=off), one fan per task"}
+
+    value = tests_all * a.steps / dt
+    res = {
+        "metric": "ray-collider tests/sec + p50 per-frame batch ms, 256src x 512ray x 4096col",
+        "value": value,
+        "unit": "ray-collider tests/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "p50_frame_ms": statistics.median(frame_ms) if frame_ms else None,
+        "p50_frame_ms_note": "art_schedule..art_complete on rank 0, host arrays, H2D + kernels + D2H (PCIe-inclusive)",
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"config{cfg.index}: {cfg.description}", "fans_per_gpu": S, "rays": cfg.R,
+                   "colliders": cfg.C, "targets": cfg.T, "max_hits_per_ray": cfg.H, "tests_per_frame_per_gpu": tests_rank,
+                   "parallelism": f"fan-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+        "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "raytrace_kernel", "kernel_ms": rt_ms,
+                     "note": "FP32 VALU roof (no MFMA-shaped work); algorithmic ops per test per SURVEY.md 8(d)",
+                     "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
+                             "algorithmic_bytes": alg_bytes}},
+        "kernel_ms": {"raytrace": rt_ms, "permeate": ktimes["permeate_ms"] / n_rt, "reduce": ktimes["reduce_ms"] / n_rt},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+/*
+ * art_device.h — device-resident extension of the art C ABI.
+ *
+ * The Unity drop-in surface is art.h (host arrays in, host arrays out). This header adds the
+ * entry points a one-process-per-GPU host (bench.py, or a server that keeps scenes resident in
+ * HBM and exchanges results with RCCL) needs: bind a scene once, then launch frames whose fan
+ * origins and packed per-fan result blocks are DEVICE pointers on a caller-supplied HIP stream.
+ *
+ * Packed per-fan result block (art_fan_layout): fan f's record starts at f * stride inside the
+ * block and holds, at the given byte offsets, exactly the arrays art_fan points to
+ * (settings, dsp params, muffle, permeation, echo, hit points, hit counts). One contiguous block
+ * per rank is what the multi-GPU path all-gathers (SURVEY.md §8 e).
+ */
+#ifndef ART_DEVICE_H
+#define ART_DEVICE_H
+
+#include "art.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ART_OUT_HIT_RESULTS 0x1u /* also produce ray_hit_points / ray_hit_counts */
+
+typedef struct {
+    uint32_t stride;          /* bytes per fan record, multiple of 16 */
+    uint32_t settings_off;    /* art_target_settings[T] */
+    uint32_t dsp_off;         /* art_dsp_params[T] (valid iff stages & ART_STAGE_DSP_PARAMS) */
+    uint32_t muffle_off;      /* uint16_t[TC*T] */
+    uint32_t perm_off;        /* float[TC*T] */
+    uint32_t echo_off;        /* uint16_t (half) [R*H] */
+    uint32_t hit_points_off;  /* art_half3[R*H] (iff ART_OUT_HIT_RESULTS) */
+    uint32_t hit_counts_off;  /* uint8_t[R]     (iff ART_OUT_HIT_RESULTS) */
+} art_fan_layout;
+
+typedef struct {
+    double raytrace_ms, permeate_ms, reduce_ms; /* summed hipEvent durations */
+    int32_t launches;                           /* frames timed */
+} art_kernel_times;
+
+/* Record hipEvents around every kernel of art_launch_device (art_set_flags). */
+#define ART_CTX_TIME_KERNELS 0x2u
+/* Use the reference-order (one ray per lane) raytrace kernel instead of the K-way split one. */
+#define ART_CTX_FORCE_REFERENCE_ORDER 0x4u
+
+ART_API int art_fan_layout_get(const art_frame_desc* desc, uint32_t out_flags, art_fan_layout* out);
+
+/* Upload the scene (colliders, directions, targets, curves) to every device of the context and
+ * build the device SoA records. Synchronous. Pointers in desc are host pointers. */
+ART_API int art_scene_bind(art_ctx* ctx, const art_frame_desc* desc);
+
+/* Enqueue one frame on the context's first device: d_origins = float3[fan_count] (device),
+ * d_block = fan_count * stride bytes (device, in/out), stream = the hipStream_t to enqueue on
+ * (NULL = the HIP default stream, e.g. torch's default stream). Kernels only; returns without
+ * synchronizing. */
+ART_API int art_launch_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
+                              uint32_t out_flags, void* stream);
+
+/* Same frame with the test-counting kernels (for the tests/s metric); synchronizes. */
+ART_API int art_count_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
+                             uint32_t out_flags, void* stream, art_test_counts* out);
+
+/* Sum of kernel times since the last call (needs ART_CTX_TIME_KERNELS); synchronizes. */
+ART_API int art_kernel_timing(art_ctx* ctx, art_kernel_times* out);
+
+/* Number of HIP devices visible (0 when none); never fails. */
+ART_API int art_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ART_DEVICE_H */

@@ -1,0 +1,210 @@
+"""GPU parity: libart.so (HIP, through the C ABI) against the CPU oracle, bit-exact.
+
+Every output array of the reference jobs is compared byte for byte: EchoRayDistances (half),
+MuffleRayHits (u16), PermeationPowerRemains (f32 bits), AudioTargetSettings (f32 bits),
+DSP parameters, RayHitResults / RayHitResultCounts. Floating-point outputs are required to be
+bit-identical (tolerance 0 ULP), which is stricter than north_star's 1e-5 absolute bound.
+Test counts (the tests/s metric's numerator) must equal the oracle's per-kind counts.
+"""
+import numpy as np
+import pytest
+
+import art
+from art import abi
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _diff_report(a: art.FanOutputs, b: art.FanOutputs) -> str:
+    lines = []
+    for name in ("echo", "muffle", "perm", "settings", "dsp", "hit_points", "hit_counts"):
+        x, y = getattr(a, name), getattr(b, name)
+        if x is None or y is None:
+            continue
+        xv = x.view(np.uint8).reshape(x.shape[0], -1)
+        yv = y.view(np.uint8).reshape(y.shape[0], -1)
+        bad = np.argwhere(xv != yv)
+        if bad.size:
+            f = bad[0][0]
+            lines.append(f"{name}: {len(np.unique(bad[:, 0]))} fans differ; first fan {f}: gpu={x[f].ravel()[:12]} "
+                         f"ref={y[f].ravel()[:12]}")
+    return "\n".join(lines)
+
+
+def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True):
+    """Run the frame through both raytrace kernels — the throughput (K-way split, coherent ray
+    order) kernel and the reference-order counting kernel — and require both to equal the
+    oracle bit for bit; the counting run's test counts must equal the oracle's."""
+    S = org.shape[0]
+    o_gpu = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, params.thread_count, hits=hits,
+                           dsp=params.dsp is not None)
+    if stale is not None:
+        o_gpu.fill_random(stale)
+    o_ref = o_gpu.copy()
+    o_cnt = o_gpu.copy()
+    cref = oracle.run_frame(art.Frame(scene, params, org, o_ref), threads=16)
+    ctx.set_flags(0)
+    ctx.run(art.Frame(scene, params, org, o_gpu))
+    eq = o_gpu.equal(o_ref)
+    assert all(eq.values()), f"fast kernel: {eq}\n{_diff_report(o_gpu, o_ref)}"
+    if counts:
+        ctx.set_flags(abi.ART_CTX_COUNT_TESTS)
+        ctx.run(art.Frame(scene, params, org, o_cnt))
+        ctx.set_flags(0)
+        eq = o_cnt.equal(o_ref)
+        assert all(eq.values()), f"counting kernel: {eq}\n{_diff_report(o_cnt, o_ref)}"
+        assert ctx.last_test_counts() == cref
+    return o_gpu, cref
+
+
+# Reduced sizes of BASELINE.json's five configs: (S, R, collider scale)
+REDUCED = {1: (8, 64, None), 2: (16, 128, 0.25), 3: (8, 96, 0.125), 4: (8, 128, 1 / 16), 5: (8, 128, 0.25)}
+
+
+@pytest.mark.parametrize("ci", [1, 2, 3, 4, 5])
+def test_config_reduced(ctx, ci):
+    S, R, cs = REDUCED[ci]
+    scene, org, params = art.synth(art.CONFIGS[ci], S=S, R=R, C_scale=cs)
+    out, counts = gpu_vs_oracle(ctx, scene, params, org, hits=(ci in (1, 5)))
+    # the case must exercise the path: some echoes returned, some muffle rays clear
+    assert (out.echo != 0).any() and (out.muffle != 0).any()
+    assert counts["rt_sphere"] + counts["rt_aabb"] + counts["rt_obb"] > 0
+
+
+@pytest.mark.parametrize("tc,R", [(3, 64), (4, 9), (2, 31), (5, 64)])
+def test_thread_count_batches(ctx, tc, R):
+    """TC > 1: per-batch muffle slots, permeation slot collapse (Q7), mis-indexed echo reset (Q1),
+    never-reset slots keep stale contents (Q18) — sequential-batch semantics."""
+    scene, org, params = art.synth(art.CONFIGS[1], S=4, R=R)
+    params.thread_count = tc
+    gpu_vs_oracle(ctx, scene, params, org, hits=True, stale=7)
+
+
+def test_stale_single_batch(ctx):
+    """TC = 1: every output slot is reset, so stale contents must not leak."""
+    scene, org, params = art.synth(art.CONFIGS[5], S=4, R=64, C_scale=0.1)
+    gpu_vs_oracle(ctx, scene, params, org, hits=True, stale=3)
+
+
+def test_stage_subsets(ctx):
+    scene, org, params = art.synth(art.CONFIGS[5], S=4, R=64, C_scale=0.1)
+    for stages in (abi.ART_STAGE_RAYTRACE, abi.ART_STAGE_PERMEATE, abi.ART_STAGE_REDUCE,
+                   abi.ART_STAGE_PERMEATE | abi.ART_STAGE_REDUCE, abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE):
+        params.stages = stages
+        params.dsp = None
+        gpu_vs_oracle(ctx, scene, params, org, stale=11)
+
+
+def test_no_colliders(ctx):
+    """Every ray misses: no echoes, no muffle hits, permeation reset to 0 (reference :43-46)."""
+    scene, org, params = art.synth(art.CONFIGS[1], S=2, R=64)
+    scene.aabbs = scene.aabbs[:0]
+    out, _ = gpu_vs_oracle(ctx, scene, params, org, hits=True, stale=5)
+    assert not out.echo.any() and not out.muffle.any() and not out.perm.any()
+
+
+def test_single_type_scenes(ctx):
+    for ci, cs in ((2, 0.05), (3, 0.05)):
+        scene, org, params = art.synth(art.CONFIGS[ci], S=4, R=64, C_scale=cs)
+        params.max_hits_per_ray = 26  # maxBounces 25, the reference's slider maximum (AudioRayTracer.cs:14)
+        params.stages = abi.ART_STAGE_ALL
+        params.dsp = art.DspSettings.default()
+        gpu_vs_oracle(ctx, scene, params, org, hits=True)
+
+
+def test_one_target_many_targets(ctx):
+    scene, org, params = art.synth(art.CONFIGS[5], S=4, R=64, C_scale=0.1)
+    one = art.Scene(dirs=scene.dirs, targets=scene.targets[:1].copy(), spheres=scene.spheres, aabbs=scene.aabbs,
+                    obbs=scene.obbs)
+    gpu_vs_oracle(ctx, one, params, org)
+    rng = np.random.default_rng(0)
+    many = art.Scene(dirs=scene.dirs, targets=rng.uniform(-10, 10, (37, 3)).astype(np.float32), spheres=scene.spheres,
+                     aabbs=scene.aabbs, obbs=scene.obbs)
+    gpu_vs_oracle(ctx, many, params, org)
+
+
+def test_full_size_config2_sampled(ctx):
+    """Config 2 at full size (256 x 512 x 4096): every 8th fan checked against the oracle, the
+    rest through size-independent properties (determinism, fan-permutation invariance)."""
+    cfg = art.CONFIGS[2]
+    scene, org, params = art.synth(cfg)
+    out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1)
+    ctx.run(art.Frame(scene, params, org, out))
+    sub = np.arange(0, cfg.S, 8)
+    ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1)
+    oracle.run(scene, params, org[sub], ref, threads=16)
+    for name in ("echo", "muffle", "perm", "settings"):
+        assert np.array_equal(getattr(out, name)[sub].view(np.uint8), getattr(ref, name).view(np.uint8)), name
+    # determinism
+    out2 = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1)
+    ctx.run(art.Frame(scene, params, org, out2))
+    assert all(out.equal(out2).values())
+    # permutation invariance: fans are independent
+    perm = np.random.default_rng(1).permutation(cfg.S)
+    out3 = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1)
+    ctx.run(art.Frame(scene, params, np.ascontiguousarray(org[perm]), out3))
+    assert np.array_equal(out3.echo, out.echo[perm]) and np.array_equal(out3.settings.view(np.uint8),
+                                                                         out.settings[perm].view(np.uint8))
+
+
+@pytest.mark.parametrize("ci", [3, 5])
+def test_full_size_sampled(ctx, ci):
+    cfg = art.CONFIGS[ci]
+    scene, org, params = art.synth(cfg)
+    dsp = params.dsp is not None
+    out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1, dsp=dsp)
+    ctx.run(art.Frame(scene, params, org, out))
+    sub = np.arange(0, cfg.S, 32)
+    ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1, dsp=dsp)
+    oracle.run(scene, params, np.ascontiguousarray(org[sub]), ref, threads=16)
+    for name in ("echo", "muffle", "perm", "settings") + (("dsp",) if dsp else ()):
+        assert np.array_equal(getattr(out, name)[sub].view(np.uint8), getattr(ref, name).view(np.uint8)), name
+
+
+def test_device_resident_path(ctx):
+    """art_scene_bind + art_launch_device on torch-allocated HBM buffers gives the same bytes as
+    art_schedule/art_complete."""
+    torch = pytest.importorskip("torch")
+    cfg = art.CONFIGS[5]
+    scene, org, params = art.synth(cfg, S=16, R=128, C_scale=0.25)
+    out = art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True, hits=True)
+    fr = art.Frame(scene, params, org, out)
+    ctx.run(fr)
+    lay = art.fan_layout(fr, abi.ART_OUT_HIT_RESULTS)
+    ctx.bind(fr)
+    d_org = torch.from_numpy(org.copy()).cuda()
+    d_blk = torch.zeros(16 * lay["stride"], dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    ctx.launch_device(d_org.data_ptr(), 16, d_blk.data_ptr(), abi.ART_OUT_HIT_RESULTS, st.cuda_stream)
+    st.synchronize()
+    got = art.unpack_block(d_blk.cpu().numpy(), lay, 16, 128, cfg.H, cfg.T, 1, hits=True, dsp=True)
+    assert all(got.equal(out).values())
+    counts = ctx.count_device(d_org.data_ptr(), 16, d_blk.data_ptr(), 0, st.cuda_stream)
+    ref = art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True)
+    assert counts == oracle.run(scene, params, org, ref, threads=16)[1]
+
+
+def test_schedule_is_completed_complete(ctx):
+    scene, org, params = art.synth(art.CONFIGS[1])
+    out = art.FanOutputs(8, 64, 5, 4, 1)
+    h = ctx.schedule(art.Frame(scene, params, org, out))
+    with pytest.raises(art.ArtError):  # one frame in flight per context (AudioRayTracer.cs:95-97)
+        ctx.schedule(art.Frame(scene, params, org, art.FanOutputs(8, 64, 5, 4, 1)))
+    while not h.is_completed:
+        pass
+    h.complete()
+    h.complete()  # idempotent, like JobHandle.Complete
+    assert (out.echo != 0).any()
+
+
+def test_invalid_arguments(ctx):
+    scene, org, params = art.synth(art.CONFIGS[1], S=2)
+    bad = art.Scene(dirs=scene.dirs, targets=scene.targets[:0], aabbs=scene.aabbs)
+    with pytest.raises(art.ArtError) as e:
+        ctx.run(art.Frame(bad, params, org, art.FanOutputs(2, 64, 5, 1, 1)))
+    assert e.value.code == abi.ART_E_INVALID
+    params.max_hits_per_ray = 40
+    with pytest.raises(art.ArtError) as e:
+        ctx.run(art.Frame(scene, params, org, art.FanOutputs(2, 64, 40, 4, 1)))
+    assert e.value.code == abi.ART_E_UNSUPPORTED
