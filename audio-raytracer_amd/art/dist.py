@@ -1,0 +1,38 @@
+"""Fan sharding across ranks (one process per GPU) and the all-gather of per-fan result blocks.
+
+Fans are independent (SURVEY.md §8 e): rank r of W owns fans [S*r//W, S*(r+1)//W). Colliders,
+directions and targets are replicated per rank. Each rank's packed fan records (include/
+art_device.h art_fan_layout) form one contiguous block; one all_gather_into_tensor over RCCL
+(torch.distributed "nccl") — or gloo on CPU — assembles the [S * stride] result on every rank.
+Uneven shards are padded to ceil(S/W) records and trimmed after the gather.
+"""
+from __future__ import annotations
+
+
+def shard_range(S: int, world: int, rank: int) -> tuple[int, int]:
+    return (S * rank) // world, (S * (rank + 1)) // world
+
+
+def all_gather_fan_blocks(local_block, S: int, stride: int, world: int, group=None):
+    """local_block: uint8 tensor [n_local * stride] of this rank's fans (n_local from shard_range).
+    Returns a uint8 tensor [S * stride] with every fan's record in global fan order."""
+    import torch
+    import torch.distributed as dist
+
+    per = (S + world - 1) // world
+    n_local = local_block.numel() // stride
+    if world == 1:
+        return local_block
+    if n_local == per and S == per * world:
+        out = torch.empty(S * stride, dtype=torch.uint8, device=local_block.device)
+        dist.all_gather_into_tensor(out, local_block, group=group)
+        return out
+    padded = torch.zeros(per * stride, dtype=torch.uint8, device=local_block.device)
+    padded[: n_local * stride] = local_block
+    full = torch.empty(world * per * stride, dtype=torch.uint8, device=local_block.device)
+    dist.all_gather_into_tensor(full, padded, group=group)
+    parts = []
+    for r in range(world):
+        b, e = shard_range(S, world, r)
+        parts.append(full[r * per * stride: (r * per + (e - b)) * stride])
+    return torch.cat(parts)

@@ -320,3 +320,25 @@ def unpack_block(block: np.ndarray, layout: dict, S: int, R: int, H: int, T: int
         out.hit_points[:] = sec(layout["hit_points_off"], R * H * 6, np.uint16).reshape(S, R * H, 3)
         out.hit_counts[:] = sec(layout["hit_counts_off"], R, np.uint8)
     return out
+
+
+def pack_block(out: FanOutputs, layout: dict) -> np.ndarray:
+    """Inverse of unpack_block: FanOutputs -> packed per-fan records (uint8 [S * stride])."""
+    S, R, H, T, TC = out.S, out.R, out.H, out.T, out.TC
+    st = layout["stride"]
+    b = np.zeros((S, st), np.uint8)
+
+    def put(off, arr):
+        v = np.ascontiguousarray(arr).reshape(S, -1).view(np.uint8)
+        b[:, off:off + v.shape[1]] = v
+
+    put(layout["settings_off"], out.settings)
+    if out.dsp is not None:
+        put(layout["dsp_off"], out.dsp)
+    put(layout["muffle_off"], out.muffle)
+    put(layout["perm_off"], out.perm)
+    put(layout["echo_off"], out.echo)
+    if out.hit_points is not None:
+        put(layout["hit_points_off"], out.hit_points)
+        put(layout["hit_counts_off"], out.hit_counts)
+    return b.reshape(-1)

@@ -28,6 +28,14 @@
 
 using namespace art;
 
+// The ABI structs are byte-identical to the C# structs (App. C of SURVEY.md).
+static_assert(sizeof(art_half3) == 6, "half3");
+static_assert(sizeof(art_aabb) == 20, "ColliderAABBStruct");
+static_assert(sizeof(art_obb) == 26, "ColliderOBBStruct");
+static_assert(sizeof(art_sphere) == 16, "ColliderSphereStruct");
+static_assert(sizeof(art_target_settings) == 24, "AudioTargetRTSettings");
+static_assert(sizeof(art_dsp_params) == 24, "art_dsp_params");
+
 namespace {
 
 constexpr uint32_t kAbiVersion = (1u << 16) | 0u;

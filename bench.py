@@ -91,7 +91,6 @@ def main():
     ctx.bind(frame)
     d_org = torch.from_numpy(org).to(dev)
     d_blk = torch.zeros(S * lay["stride"], dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * S * lay["stride"], dtype=torch.uint8, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
@@ -102,7 +101,7 @@ def main():
     def step():
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, d_blk)
+            art.dist.all_gather_fan_blocks(d_blk, S_total, lay["stride"], world)
 
     for _ in range(a.warmup):
         step()
@@ -164,7 +163,7 @@ def main():
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        fans = a.cpu_fans or max(threads, 16)
+        fans = a.cpu_fans or S  # the full frame of this config (no extrapolation)
         v, cdt, ctests = cpu_baseline(cfg, scene, params, org, fans, threads)
         cpu = {"value": v, "unit": "ray-collider tests/s", "cores": threads, "kind": "port",
                "sample": f"{fans} of {S} fans of config {cfg.index} ({ctests} tests, {cdt:.1f} s) through the C "

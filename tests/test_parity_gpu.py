@@ -208,3 +208,39 @@ def test_invalid_arguments(ctx):
     with pytest.raises(art.ArtError) as e:
         ctx.run(art.Frame(scene, params, org, art.FanOutputs(2, 64, 40, 4, 1)))
     assert e.value.code == abi.ART_E_UNSUPPORTED
+
+
+# ---------------------------------------------------------------- known answers and fixtures
+import golden_util as G  # noqa: E402
+import kat_scenes as K  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(K.KATS))
+def test_kats_on_gpu(ctx, name):
+    """Hand-derived answers hold on the HIP path, through both kernels."""
+    sc, p, org, expect = K.KATS[name]()
+    out, _ = gpu_vs_oracle(ctx, sc, p, org, hits=True)
+    expect(out)
+
+
+def test_k9_reduce_on_gpu(ctx):
+    sc, p, org, expect, prime = K.k9_reduce()
+    out = art.FanOutputs(1, sc.R, p.max_hits_per_ray, sc.T, 1)
+    prime(out)
+    ctx.run(art.Frame(sc, p, org, out))
+    expect(out)
+
+
+@pytest.mark.parametrize("name", G.names())
+def test_golden_on_gpu(ctx, name):
+    """The HIP path reproduces the committed fixtures (and their test counts) bit for bit."""
+    scene, org, params, fresh, expected, counts = G.load(name)
+    cnt_out = fresh.copy()
+    ctx.set_flags(0)
+    ctx.run(art.Frame(scene, params, org, fresh))
+    assert all(fresh.equal(expected).values()), _diff_report(fresh, expected)
+    ctx.set_flags(abi.ART_CTX_COUNT_TESTS)
+    ctx.run(art.Frame(scene, params, org, cnt_out))
+    ctx.set_flags(0)
+    assert all(cnt_out.equal(expected).values())
+    assert ctx.last_test_counts() == counts
