@@ -164,7 +164,7 @@ def load_library(path: str | None = None) -> C.CDLL:
     if _lib is not None and path is None:
         return _lib
     _preload_torch_hip_runtime()
-    p = path or LIB_PATH
+    p = path or os.environ.get("ART_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise ImportError(f"libart.so not found at {p}: build it with `make -C audio-raytracer_amd` "
                           "(or __graft_entry__.build()); the GPU path has no CPU fallback")

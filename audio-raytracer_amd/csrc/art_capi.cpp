@@ -86,7 +86,7 @@ struct Frame {
   // input staging layout (bytes)
   size_t off_sph = 0, off_aabb = 0, off_obb = 0, off_tgt = 0, off_dirs = 0, off_vol = 0, off_muf = 0, off_tab = 0,
          off_reset = 0, off_order = 0, raw_bytes = 0;
-  size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_bytes = 0;
+  size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_bytes = 0;
 };
 
 struct Device {
@@ -286,6 +286,9 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
   f.soa_sph = s; s = align_up(s + (size_t)f.ns * sizeof(SphereRec), 256);
   f.soa_aabb = s; s = align_up(s + (size_t)f.na * sizeof(AabbRec), 256);
   f.soa_obb = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
+  f.soa_sphc = s; s = align_up(s + (size_t)f.ns * sizeof(SphereCold), 256);
+  f.soa_aabbc = s; s = align_up(s + (size_t)f.na * sizeof(AabbCold), 256);
+  f.soa_obbc = s; s = align_up(s + (size_t)f.no * sizeof(ObbCold), 256);
   f.soa_bytes = s;
 }
 
@@ -311,12 +314,17 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   uint8_t* soa = static_cast<uint8_t*>(dv.soa.p);
   launch_prep(reinterpret_cast<const art_sphere*>(raw + f.off_sph), f.ns, reinterpret_cast<const art_aabb*>(raw + f.off_aabb),
               f.na, reinterpret_cast<const art_obb*>(raw + f.off_obb), f.no, reinterpret_cast<SphereRec*>(soa + f.soa_sph),
-              reinterpret_cast<AabbRec*>(soa + f.soa_aabb), reinterpret_cast<ObbRec*>(soa + f.soa_obb), dv.stream);
+              reinterpret_cast<SphereCold*>(soa + f.soa_sphc), reinterpret_cast<AabbRec*>(soa + f.soa_aabb),
+              reinterpret_cast<AabbCold*>(soa + f.soa_aabbc), reinterpret_cast<ObbRec*>(soa + f.soa_obb),
+              reinterpret_cast<ObbCold*>(soa + f.soa_obbc), dv.stream);
   HIP_TRY(c, hipGetLastError());
   DevScene& sc = dv.sc;
   sc.sph = reinterpret_cast<const SphereRec*>(soa + f.soa_sph); sc.ns = f.ns;
   sc.aabb = reinterpret_cast<const AabbRec*>(soa + f.soa_aabb); sc.na = f.na;
   sc.obb = reinterpret_cast<const ObbRec*>(soa + f.soa_obb); sc.no = f.no;
+  sc.sphc = reinterpret_cast<const SphereCold*>(soa + f.soa_sphc);
+  sc.aabbc = reinterpret_cast<const AabbCold*>(soa + f.soa_aabbc);
+  sc.obbc = reinterpret_cast<const ObbCold*>(soa + f.soa_obbc);
   sc.targets = reinterpret_cast<const float*>(raw + f.off_tgt); sc.T = f.T;
   sc.dirs = reinterpret_cast<const uint16_t*>(raw + f.off_dirs); sc.R = f.R;
   dv.bound = true;
@@ -384,7 +392,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     size_t ti = timing ? tstart(0) : 0;
     // The counting variant sweeps colliders in exact reference order per lane (its per-lane
     // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
-    if (count || f.T > 31 || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER))
+    if (count || f.T > fast_max_targets() || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER))
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
     else
       launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, reinterpret_cast<const int*>(raw + f.off_order), st);

@@ -79,7 +79,7 @@ __device__ __forceinline__ bool obb_test(const Seg& s, const ObbRec& b, quat q, 
 }
 
 __device__ __forceinline__ quat stored_q(const ObbRec& b) { quat q; q.x = b.qx; q.y = b.qy; q.z = b.qz; q.w = b.qw; return q; }
-__device__ __forceinline__ quat inverse_q(const ObbRec& b) { quat q; q.x = b.iqx; q.y = b.iqy; q.z = b.iqz; q.w = b.iqw; return q; }
+__device__ __forceinline__ quat inverse_q(const ObbCold& b) { quat q; q.x = b.iqx; q.y = b.iqy; q.z = b.iqz; q.w = b.iqw; return q; }
 
 // RayIntersectsSphere :323-355 (general quadratic)
 __device__ __forceinline__ bool sphere_test(const Seg& s, const SphereRec& c, float& dist) {
@@ -105,6 +105,19 @@ struct Hit {
   float dist;
 };
 
+// Scene records are read-only for the whole launch. Reading them through the constant address
+// space (4) lets a wave-uniform index become a scalar (SMEM) load into SGPRs; through a generic
+// pointer the compiler must assume the kernel's own stores may alias and emits vector loads.
+template <typename T>
+__device__ __forceinline__ T ldc(const T* p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) T* cptr;
+  return ((cptr)(p))[i];
+#else
+  return p[i];
+#endif
+}
+
 // Wave-uniform collider index: all lanes of a wave sweep the same collider, so the record is
 // fetched with scalar loads (SMEM) into SGPRs even inside divergent control flow.
 __device__ __forceinline__ int wave_uniform(int i) { return __builtin_amdgcn_readfirstlane(i); }
@@ -117,28 +130,29 @@ __device__ __forceinline__ Hit nearest(const DevScene& sc, const Seg& s, LaneCou
   h.type = kNone; h.idx = -1;
   h.dist = PERM ? __builtin_huge_valf() : FLT_MAX;
   for (int i = 0; i < sc.ns; ++i) {
-    const SphereRec c = sc.sph[wave_uniform(i)];
+    const SphereRec c = ldc(sc.sph, wave_uniform(i));
     float d;
     if (COUNT) lc.s++;
     if (sphere_test(s, c, d) && d < h.dist) { h.dist = d; h.type = kSphere; h.idx = i; }
   }
   for (int i = 0; i < sc.na; ++i) {
-    const AabbRec b = sc.aabb[wave_uniform(i)];
+    const AabbRec b = ldc(sc.aabb, wave_uniform(i));
     float d;
     if (COUNT) lc.a++;
     if (aabb_test<false>(s, b, d) && d < h.dist) { h.dist = d; h.type = kAabb; h.idx = i; }
   }
   for (int i = 0; i < sc.no; ++i) {
-    const ObbRec b = sc.obb[wave_uniform(i)];
+    const ObbRec b = ldc(sc.obb, wave_uniform(i));
     float d;
     if (COUNT) lc.o++;
-    if (obb_test<false>(s, b, PERM ? inverse_q(b) : stored_q(b), d) && d < h.dist) { h.dist = d; h.type = kObb; h.idx = i; }
+    const quat q = PERM ? inverse_q(ldc(sc.obbc, wave_uniform(i))) : stored_q(b);
+    if (obb_test<false>(s, b, q, d) && d < h.dist) { h.dist = d; h.type = kObb; h.idx = i; }
   }
   // Re-evaluate the winner with Unity's exact min/max so a zero distance carries the reference sign.
   if (h.type == kAabb) { float d; aabb_test<true>(s, sc.aabb[h.idx], d); h.dist = d; }
   if (h.type == kObb) {
     const ObbRec b = sc.obb[h.idx];
-    float d; obb_test<true>(s, b, PERM ? inverse_q(b) : stored_q(b), d); h.dist = d;
+    float d; obb_test<true>(s, b, PERM ? inverse_q(sc.obbc[h.idx]) : stored_q(b), d); h.dist = d;
   }
   if (PERM && h.dist == __builtin_huge_valf()) h.type = kNone;  // :140 closestDist != INFINITY
   return h;
@@ -151,7 +165,7 @@ template <bool SKIP, bool COUNT>
 __device__ __forceinline__ bool visible(const DevScene& sc, const Seg& s, float maxd, int target, LaneCounts& lc) {
   bool blocked = false;
   for (int i = 0; i < sc.ns; ++i) {
-    const SphereRec c = sc.sph[wave_uniform(i)];
+    const SphereRec c = ldc(sc.sph, wave_uniform(i));
     if (SKIP && c.tid == target) continue;
     if (!blocked) {
       if (COUNT) lc.s++;
@@ -161,7 +175,7 @@ __device__ __forceinline__ bool visible(const DevScene& sc, const Seg& s, float 
     if (__all(blocked)) return false;
   }
   for (int i = 0; i < sc.na; ++i) {
-    const AabbRec b = sc.aabb[wave_uniform(i)];
+    const AabbRec b = ldc(sc.aabb, wave_uniform(i));
     if (SKIP && b.tid == target) continue;
     if (!blocked) {
       if (COUNT) lc.a++;
@@ -171,7 +185,7 @@ __device__ __forceinline__ bool visible(const DevScene& sc, const Seg& s, float 
     if (__all(blocked)) return false;
   }
   for (int i = 0; i < sc.no; ++i) {
-    const ObbRec b = sc.obb[wave_uniform(i)];
+    const ObbRec b = ldc(sc.obb, wave_uniform(i));
     if (SKIP && b.tid == target) continue;
     if (!blocked) {
       if (COUNT) lc.o++;

@@ -20,36 +20,43 @@ constexpr int kRtBlock = 256;
 
 enum : int { kNone = 0, kAabb = 1, kObb = 2, kSphere = 3 };  // Enums/ColliderType.cs:4-10
 
-// Hot fields first (read in the intersection loops), cold fields after (reflection / echo).
+// Hot records hold only what the intersection sweeps read (two records per 64-B line for
+// spheres and AABBs); cold records hold what reflection, echo and permeation read per hit.
 struct alignas(16) SphereRec {  // 32 B
   float cx, cy, cz, r2;         // r2 = Radius * Radius (AudioRaytracerJobBatched.cs:328)
-  int tid;                      // AudioTargetId
-  float density, absorption, echo;
+  int tid, pad0, pad1, pad2;    // AudioTargetId
 };
-struct alignas(16) AabbRec {  // 64 B
+struct alignas(16) SphereCold {  // 16 B
+  float density, absorption, echo, pad;
+};
+struct alignas(16) AabbRec {  // 32 B
   float mnx, mny, mnz;        // Center - halfExtents (:286)
   int tid;
   float mxx, mxy, mxz;        // Center + halfExtents (:287)
-  float density;
+  float pad;
+};
+struct alignas(16) AabbCold {  // 48 B
   float cx, cy, cz, absorption;
   float hx, hy, hz, echo;
+  float density, pad0, pad1, pad2;
 };
-struct alignas(16) ObbRec {  // 96 B
+struct alignas(16) ObbRec {  // 64 B
   float cx, cy, cz;
   int tid;
   float qx, qy, qz, qw;        // stored rotation, decoded + normalized (halfQuaternion.cs:34-46)
-  float lmnx, lmny, lmnz;      // float3.zero - halfExtents (:319 -> :286)
-  float density;
-  float lmxx, lmxy, lmxz;      // float3.zero + halfExtents
-  float absorption;
+  float lmnx, lmny, lmnz, pad0;  // float3.zero - halfExtents (:319 -> :286)
+  float lmxx, lmxy, lmxz, pad1;  // float3.zero + halfExtents
+};
+struct alignas(16) ObbCold {  // 48 B
   float iqx, iqy, iqz, iqw;    // inverse(stored) (ReflectRay :489, permeation ShootRayCast :174)
   float hx, hy, hz, echo;
+  float absorption, density, pad0, pad1;
 };
 
 struct DevScene {
-  const SphereRec* sph; int ns;
-  const AabbRec* aabb; int na;
-  const ObbRec* obb; int no;
+  const SphereRec* sph; const SphereCold* sphc; int ns;
+  const AabbRec* aabb; const AabbCold* aabbc; int na;
+  const ObbRec* obb; const ObbCold* obbc; int no;
   const float* targets; int T;    // float3[T]
   const uint16_t* dirs; int R;    // half3[R] as 3 x u16
 };
@@ -79,12 +86,14 @@ struct DevCounts { unsigned long long v[9]; };
 
 // --- launchers (art_kernels.hip) ---
 void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, const art_obb* obb, int no,
-                 SphereRec* osph, AabbRec* oaabb, ObbRec* oobb, hipStream_t st);
+                 SphereRec* osph, SphereCold* osphc, AabbRec* oaabb, AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc,
+                 hipStream_t st);
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, uint32_t* muffle_acc, DevCounts* counts, hipStream_t st);
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st);
 int fast_split(int S, int R);
+int fast_max_targets();
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, const int2* slot_batch, hipStream_t st);
 void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,

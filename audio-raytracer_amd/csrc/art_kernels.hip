@@ -31,7 +31,8 @@ namespace art {
 // ------------------------------------------------------------------------------------------
 __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const art_aabb* __restrict__ aabb, int na,
                             const art_obb* __restrict__ obb, int no, SphereRec* __restrict__ osph,
-                            AabbRec* __restrict__ oaabb, ObbRec* __restrict__ oobb) {
+                            SphereCold* __restrict__ osphc, AabbRec* __restrict__ oaabb, AabbCold* __restrict__ oaabbc,
+                            ObbRec* __restrict__ oobb, ObbCold* __restrict__ oobbc) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < ns) {
     art_sphere s = sph[i];
@@ -40,44 +41,56 @@ __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const ar
     float rad = f16tof32(s.radius);
     r.r2 = rad * rad;
     r.tid = s.audio_target_id;
-    r.density = f16tof32(s.material.density);
-    r.absorption = f16tof32(s.material.absorption);
-    r.echo = f16tof32(s.material.echo);
+    r.pad0 = r.pad1 = r.pad2 = 0;
+    SphereCold c;
+    c.density = f16tof32(s.material.density);
+    c.absorption = f16tof32(s.material.absorption);
+    c.echo = f16tof32(s.material.echo);
+    c.pad = 0.0f;
     osph[i] = r;
+    osphc[i] = c;
     return;
   }
   i -= ns;
   if (i < na) {
     art_aabb a = aabb[i];
+    AabbCold c;
+    c.cx = f16tof32(a.center.x); c.cy = f16tof32(a.center.y); c.cz = f16tof32(a.center.z);
+    c.hx = f16tof32(a.size.x); c.hy = f16tof32(a.size.y); c.hz = f16tof32(a.size.z);
+    c.density = f16tof32(a.material.density);
+    c.absorption = f16tof32(a.material.absorption);
+    c.echo = f16tof32(a.material.echo);
+    c.pad0 = c.pad1 = c.pad2 = 0.0f;
     AabbRec r;
-    r.cx = f16tof32(a.center.x); r.cy = f16tof32(a.center.y); r.cz = f16tof32(a.center.z);
-    r.hx = f16tof32(a.size.x); r.hy = f16tof32(a.size.y); r.hz = f16tof32(a.size.z);
-    r.mnx = r.cx - r.hx; r.mny = r.cy - r.hy; r.mnz = r.cz - r.hz;
-    r.mxx = r.cx + r.hx; r.mxy = r.cy + r.hy; r.mxz = r.cz + r.hz;
+    r.mnx = c.cx - c.hx; r.mny = c.cy - c.hy; r.mnz = c.cz - c.hz;
+    r.mxx = c.cx + c.hx; r.mxy = c.cy + c.hy; r.mxz = c.cz + c.hz;
     r.tid = a.audio_target_id;
-    r.density = f16tof32(a.material.density);
-    r.absorption = f16tof32(a.material.absorption);
-    r.echo = f16tof32(a.material.echo);
+    r.pad = 0.0f;
     oaabb[i] = r;
+    oaabbc[i] = c;
     return;
   }
   i -= na;
   if (i < no) {
     art_obb b = obb[i];
     ObbRec r;
+    ObbCold c;
     r.cx = f16tof32(b.center.x); r.cy = f16tof32(b.center.y); r.cz = f16tof32(b.center.z);
-    r.hx = f16tof32(b.size.x); r.hy = f16tof32(b.size.y); r.hz = f16tof32(b.size.z);
-    r.lmnx = 0.0f - r.hx; r.lmny = 0.0f - r.hy; r.lmnz = 0.0f - r.hz;
-    r.lmxx = 0.0f + r.hx; r.lmxy = 0.0f + r.hy; r.lmxz = 0.0f + r.hz;
+    c.hx = f16tof32(b.size.x); c.hy = f16tof32(b.size.y); c.hz = f16tof32(b.size.z);
+    r.lmnx = 0.0f - c.hx; r.lmny = 0.0f - c.hy; r.lmnz = 0.0f - c.hz;
+    r.lmxx = 0.0f + c.hx; r.lmxy = 0.0f + c.hy; r.lmxz = 0.0f + c.hz;
+    r.pad0 = r.pad1 = 0.0f;
     quat q = half_quaternion_value(b.rot_x, b.rot_y, b.rot_z);
     quat qi = qinverse(q);
     r.qx = q.x; r.qy = q.y; r.qz = q.z; r.qw = q.w;
-    r.iqx = qi.x; r.iqy = qi.y; r.iqz = qi.z; r.iqw = qi.w;
+    c.iqx = qi.x; c.iqy = qi.y; c.iqz = qi.z; c.iqw = qi.w;
     r.tid = b.audio_target_id;
-    r.density = f16tof32(b.material.density);
-    r.absorption = f16tof32(b.material.absorption);
-    r.echo = f16tof32(b.material.echo);
+    c.density = f16tof32(b.material.density);
+    c.absorption = f16tof32(b.material.absorption);
+    c.echo = f16tof32(b.material.echo);
+    c.pad0 = c.pad1 = 0.0f;
     oobb[i] = r;
+    oobbc[i] = c;
   }
 }
 
@@ -152,7 +165,7 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
       vec3 rdir = normalize(O - off);
       float dist0 = distance(O, o);
       if (visible<false, COUNT>(sc, make_seg(off, rdir), dist0, -1, lc) && live_slot) {
-        float em = h.type == kSphere ? sc.sph[h.idx].echo : (h.type == kAabb ? sc.aabb[h.idx].echo : sc.obb[h.idx].echo);
+        float em = h.type == kSphere ? sc.sphc[h.idx].echo : (h.type == kAabb ? sc.aabbc[h.idx].echo : sc.obbc[h.idx].echo);
         echo[rid] = f32tof16(dist0 * em);               // Half.Multiply, HalfDataTypesUtility.cs:86-90
       }
       // Muffle — :150-173
@@ -172,7 +185,7 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
         vec3 n = mk3(0.0f, 0.0f, 0.0f);
         float absorption = 0.0f;
         if (h.type == kAabb) {
-          const AabbRec b = sc.aabb[h.idx];
+          const AabbCold b = sc.aabbc[h.idx];
           vec3 lp = o - mk3(b.cx, b.cy, b.cz);
           vec3 ap = abs3(lp);
           float dx = b.hx - ap.x, dy = b.hy - ap.y, dz = b.hz - ap.z;
@@ -182,19 +195,20 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
           absorption = b.absorption;
         } else if (h.type == kObb) {
           const ObbRec b = sc.obb[h.idx];
-          vec3 lh = qmul(inverse_q(b), o - mk3(b.cx, b.cy, b.cz));
+          const ObbCold bc = sc.obbc[h.idx];
+          vec3 lh = qmul(inverse_q(bc), o - mk3(b.cx, b.cy, b.cz));
           vec3 ap = abs3(lh);
-          vec3 df = mk3(b.hx, b.hy, b.hz) - ap;
+          vec3 df = mk3(bc.hx, bc.hy, bc.hz) - ap;
           vec3 ln = mk3(0.0f, 0.0f, 0.0f);
           if (df.x < df.y && df.x < df.z) ln.x = usign(lh.x);
           else if (df.y < df.x && df.y < df.z) ln.y = usign(lh.y);
           else ln.z = usign(lh.z);
           n = qmul(stored_q(b), ln);
-          absorption = b.absorption;
+          absorption = bc.absorption;
         } else {
           const SphereRec c = sc.sph[h.idx];
           n = normalize(o - mk3(c.cx, c.cy, c.cz));
-          absorption = c.absorption;
+          absorption = sc.sphc[h.idx].absorption;
         }
         d = reflect(d, n);                               // :525
         o = o + d * kEps;                                // :528
@@ -228,7 +242,7 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
 // ------------------------------------------------------------------------------------------
 constexpr int kPermBlock = 256;
 
-__device__ __forceinline__ float perm_term_sphere(const Seg& s, const SphereRec& c) {
+__device__ __forceinline__ float perm_term_sphere(const Seg& s, const SphereRec& c, float density) {
   // RayIntersectsSpherePermeation :303-328
   vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
   float b = dot(oc, s.d);
@@ -239,7 +253,7 @@ __device__ __forceinline__ float perm_term_sphere(const Seg& s, const SphereRec&
   float tEnter = -b - sq, tExit = -b + sq;
   if (tExit < 0.0f) return 0.0f;
   float enter = umax(tEnter, 0.0f);
-  return umax(0.0f, tExit - enter) * c.density;
+  return umax(0.0f, tExit - enter) * density;
 }
 __device__ __forceinline__ float perm_term_slab(float ox, float oy, float oz, float ix, float iy, float iz, float mnx,
                                                 float mny, float mnz, float mxx, float mxy, float mxz, float density) {
@@ -300,10 +314,12 @@ __global__ __launch_bounds__(kPermBlock) void permeate_kernel(DevScene sc, Frame
       float term = 0.0f;
       if (c < sc.ns) {
         const SphereRec r = sc.sph[c];
-        if (r.tid != t) term = perm_term_sphere(s, r);
+        if (r.tid != t) term = perm_term_sphere(s, r, sc.sphc[c].density);
       } else if (c < sc.ns + sc.na) {
         const AabbRec r = sc.aabb[c - sc.ns];
-        if (r.tid != t) term = perm_term_slab(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.mnx, r.mny, r.mnz, r.mxx, r.mxy, r.mxz, r.density);
+        if (r.tid != t)
+          term = perm_term_slab(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.mnx, r.mny, r.mnz, r.mxx, r.mxy, r.mxz,
+                                sc.aabbc[c - sc.ns].density);
       } else if (c < ctot) {
         const ObbRec r = sc.obb[c - sc.ns - sc.na];
         if (r.tid != t) {
@@ -311,7 +327,7 @@ __global__ __launch_bounds__(kPermBlock) void permeate_kernel(DevScene sc, Frame
           vec3 lo = qmul(q, s.o - mk3(r.cx, r.cy, r.cz));
           vec3 ld = qmul(q, s.d);
           term = perm_term_slab(lo.x, lo.y, lo.z, 1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z, r.lmnx, r.lmny, r.lmnz, r.lmxx,
-                                r.lmxy, r.lmxz, r.density);
+                                r.lmxy, r.lmxz, sc.obbc[c - sc.ns - sc.na].density);
         }
       }
       s_terms[tid] = term;
@@ -444,10 +460,12 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
 // launchers
 // ------------------------------------------------------------------------------------------
 void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, const art_obb* obb, int no,
-                 SphereRec* osph, AabbRec* oaabb, ObbRec* oobb, hipStream_t st) {
+                 SphereRec* osph, SphereCold* osphc, AabbRec* oaabb, AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc,
+                 hipStream_t st) {
   int n = ns + na + no;
   if (n == 0) return;
-  hipLaunchKernelGGL(prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sph, ns, aabb, na, obb, no, osph, oaabb, oobb);
+  hipLaunchKernelGGL(prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sph, ns, aabb, na, obb, no, osph, osphc, oaabb,
+                     oaabbc, oobb, oobbc);
 }
 
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,

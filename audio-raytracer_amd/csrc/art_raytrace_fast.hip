@@ -19,7 +19,10 @@
 
 namespace art {
 
-constexpr int kU = 4;  // sweep unroll
+#ifndef ART_FAST_UNROLL
+#define ART_FAST_UNROLL 4
+#endif
+constexpr int kU = ART_FAST_UNROLL;  // sweep unroll
 constexpr int kNoHit = 0x7fffffff;
 
 __device__ __forceinline__ void chunk_of(int n, int w, int K, int& b, int& e) {
@@ -57,7 +60,7 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
   for (; i + kU <= e; i += kU) {
     SphereRec c[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) c[u] = sc.sph[wave_uniform(i + u)];
+    for (int u = 0; u < kU; ++u) c[u] = ldc(sc.sph, wave_uniform(i + u));
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       float d;
@@ -65,7 +68,7 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
     }
   }
   for (; i < e; ++i) {
-    const SphereRec c = sc.sph[wave_uniform(i)];
+    const SphereRec c = ldc(sc.sph, wave_uniform(i));
     float d;
     if (sphere_hit_dist(s, c, d) && d < best) { best = d; code = i; }
   }
@@ -74,7 +77,7 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
   for (; i + kU <= e; i += kU) {
     AabbRec r[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) r[u] = sc.aabb[wave_uniform(i + u)];
+    for (int u = 0; u < kU; ++u) r[u] = ldc(sc.aabb, wave_uniform(i + u));
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       float d;
@@ -82,101 +85,161 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
     }
   }
   for (; i < e; ++i) {
-    const AabbRec r = sc.aabb[wave_uniform(i)];
+    const AabbRec r = ldc(sc.aabb, wave_uniform(i));
     float d;
     if (aabb_test<false>(s, r, d) && d < best) { best = d; code = (1 << 28) | i; }
   }
   chunk_of(sc.no, w, K, b, e);
   for (i = b; i < e; ++i) {
-    const ObbRec r = sc.obb[wave_uniform(i)];
+    const ObbRec r = ldc(sc.obb, wave_uniform(i));
     float d;
     if (obb_test<false>(s, r, stored_q(r), d) && d < best) { best = d; code = (2 << 28) | i; }
   }
 }
 
-// OR over this wave's chunk of "collider blocks the segment before maxd"
-// (CanRaySeePoint :365-397, CanRaySeeAudioTarget :405-449 with the owner skip when SKIP).
-template <bool SKIP>
-__device__ __forceinline__ bool blocked_chunk(const DevScene& sc, const Seg& s, float maxd, int target, int w, int K,
-                                              bool blocked) {
-  if (__all(blocked)) return true;
-  int b, e;
-  chunk_of(sc.ns, w, K, b, e);
+// ------------------------------------------------------------------------------------------
+// Compacted any-hit visibility (CanRaySeePoint :365-397, CanRaySeeAudioTarget :405-449).
+// Every (ray, query) pair of the block — the echo ray and the T muffle rays of each ray that hit
+// something — goes into an LDS queue. Each wave rotates through the collider chunks in lockstep
+// (the collider index stays wave-uniform, so records stay in SGPRs); a lane holds one pair, tests
+// it against the current chunk, and leaves as soon as the pair is blocked or has seen every
+// chunk; free lanes are refilled from the queue at chunk boundaries. Any-hit is an OR over the
+// colliders, so the cyclic chunk order gives the reference's verdict, and a wave only keeps
+// sweeping for lanes that are still unblocked.
+// ------------------------------------------------------------------------------------------
+constexpr int kChunk = 64;     // colliders per chunk
+constexpr int kMaxQueries = 8; // echo + up to 7 targets per ray (larger T uses raytrace_kernel)
+constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
+
+struct alignas(16) PairSeg {
+  float ox, oy, oz, dx;
+  float dy, dz, ix, iy;
+  float iz, a2, a4, maxd;
+  int owner, pad0, pad1, pad2;
+};
+
+struct ChunkMap {
+  int cs, ca, co;  // chunk counts per type (spheres, AABBs, OBBs)
+  __device__ __forceinline__ int total() const { return cs + ca + co; }
+};
+
+// Test one chunk for this lane's pair. `done` lanes (free or blocked) do not change.
+template <typename Rec, typename Test>
+__device__ __forceinline__ bool sweep_records(const Rec* recs, int b, int e, bool blocked, bool done, Test test) {
   int i = b;
   for (; i + kU <= e; i += kU) {
-    SphereRec c[kU];
+    Rec r[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) c[u] = sc.sph[wave_uniform(i + u)];
-    bool h = false;
+    for (int u = 0; u < kU; ++u) r[u] = ldc(recs, wave_uniform(i + u));
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kU; ++u) blocked |= test(r[u]);
+    if (__all(blocked || done)) return blocked;
+  }
+  for (; i < e; ++i) blocked |= test(ldc(recs, wave_uniform(i)));
+  return blocked;
+}
+
+__device__ __forceinline__ bool sweep_chunk(const DevScene& sc, const ChunkMap& cm, int c, const Seg& s, float maxd,
+                                            int owner, bool blocked, bool done) {
+  if (c < cm.cs) {
+    const int b = c * kChunk, e = min(b + kChunk, sc.ns);
+    return sweep_records(sc.sph, b, e, blocked, done, [&](const SphereRec& r) {
       float d;
-      bool x = sphere_hit_dist(s, c[u], d) && d < maxd;
-      if (SKIP) x = x && c[u].tid != target;
-      h |= x;
-    }
-    blocked |= h;
-    if (__all(blocked)) return true;
+      return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
+    });
   }
-  for (; i < e; ++i) {
-    const SphereRec c = sc.sph[wave_uniform(i)];
-    float d;
-    bool x = sphere_hit_dist(s, c, d) && d < maxd;
-    if (SKIP) x = x && c.tid != target;
-    blocked |= x;
-  }
-  if (__all(blocked)) return true;
-  chunk_of(sc.na, w, K, b, e);
-  i = b;
-  for (; i + kU <= e; i += kU) {
-    AabbRec r[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) r[u] = sc.aabb[wave_uniform(i + u)];
-    bool h = false;
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
+  c -= cm.cs;
+  if (c < cm.ca) {
+    const int b = c * kChunk, e = min(b + kChunk, sc.na);
+    return sweep_records(sc.aabb, b, e, blocked, done, [&](const AabbRec& r) {
       float d;
-      bool x = aabb_test<false>(s, r[u], d) && d < maxd;
-      if (SKIP) x = x && r[u].tid != target;
-      h |= x;
-    }
-    blocked |= h;
-    if (__all(blocked)) return true;
+      return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+    });
   }
-  for (; i < e; ++i) {
-    const AabbRec r = sc.aabb[wave_uniform(i)];
+  c -= cm.ca;
+  const int b = c * kChunk, e = min(b + kChunk, sc.no);
+  for (int i = b; i < e; ++i) {
+    const ObbRec r = ldc(sc.obb, wave_uniform(i));
     float d;
-    bool x = aabb_test<false>(s, r, d) && d < maxd;
-    if (SKIP) x = x && r.tid != target;
-    blocked |= x;
-  }
-  if (__all(blocked)) return true;
-  chunk_of(sc.no, w, K, b, e);
-  for (i = b; i < e; ++i) {
-    const ObbRec r = sc.obb[wave_uniform(i)];
-    float d;
-    bool x = obb_test<false>(s, r, stored_q(r), d) && d < maxd;
-    if (SKIP) x = x && r.tid != target;
-    blocked |= x;
-    if ((i & 3) == 3 && __all(blocked)) return true;
+    blocked |= obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+    if ((i & 3) == 3 && __all(blocked || done)) return blocked;
   }
   return blocked;
 }
 
-__device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
-  return type == kSphere ? sc.sph[idx].echo : (type == kAabb ? sc.aabb[idx].echo : sc.obb[idx].echo);
+// Drain the block's pair queue. Results: s_res[p] = 1 if pair p is blocked.
+__device__ __forceinline__ void visibility_queue(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
+                                                 int np, int w, int K, int lane) {
+  const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
+  const int nchunks = cm.total();
+  if (nchunks == 0 || np == 0) {  // no collider: nothing blocks
+    for (int p = w * 64 + lane; p < np; p += K * 64) s_res[p] = 0;
+    return;
+  }
+  // Every wave starts at chunk 0: the waves on a CU then stream the same records and share the
+  // scalar cache (a per-wave stagger measured 5 % slower on config 2).
+  int c = 0;
+  int my = -1, left = 0;
+  bool blocked = false;
+  Seg s;
+  float maxd = 0.0f;
+  int owner = kNoOwner;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  while (true) {
+    const bool need = my < 0;
+    const unsigned long long m = __ballot(need);
+    if (m) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(s_head, __popcll(m));
+      base = __shfl(base, 0, 64);
+      if (need) {
+        const int p = base + __popcll(m & lt);
+        if (p < np) {
+          const PairSeg g = s_seg[p];
+          s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
+          s.a2 = g.a2; s.a4 = g.a4;
+          maxd = g.maxd; owner = g.owner;
+          my = p; left = nchunks; blocked = false;
+        }
+      }
+    }
+    const bool active = my >= 0;
+    if (__all(!active)) break;
+    blocked = sweep_chunk(sc, cm, c, s, maxd, owner, blocked, !active);
+    if (active) {
+      left -= 1;
+      if (blocked || left == 0) { s_res[my] = blocked ? 1 : 0; my = -1; }
+    }
+    c = (c + 1 == nchunks) ? 0 : c + 1;
+  }
 }
 
+__device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
+  return type == kSphere ? sc.sphc[idx].echo : (type == kAabb ? sc.aabbc[idx].echo : sc.obbc[idx].echo);
+}
+
+#ifndef ART_FAST_WAVES_PER_EU
+#define ART_FAST_WAVES_PER_EU 0
+#endif
+#if ART_FAST_WAVES_PER_EU > 0
+#define ART_FAST_OCC __attribute__((amdgpu_waves_per_eu(ART_FAST_WAVES_PER_EU)))
+#else
+#define ART_FAST_OCC
+#endif
+
 template <int K, bool HITS>
-__global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
+__global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
                                                                uint32_t* __restrict__ muffle_acc,
                                                                const int* __restrict__ ray_order) {
   __shared__ float s_dist[K][64];
   __shared__ int s_code[K][64];
-  __shared__ uint32_t s_blk[64];
+  __shared__ short s_pairof[kMaxQueries][64];
+  __shared__ uint8_t s_res[kMaxQueries * 64];
+  __shared__ int s_head, s_np;
   __shared__ uint32_t s_muf[kMaxTargets];
+  extern __shared__ PairSeg s_seg[];  // [64 * (T + 1)]
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fan = blockIdx.y;
   const int slot = blockIdx.x * 64 + lane;
@@ -184,7 +247,6 @@ __global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, Fram
   const int ray = valid ? ray_order[slot] : 0;
   const int T = fp.T, H = fp.H;
   for (int t = threadIdx.x; t < T; t += blockDim.x) s_muf[t] = 0;
-  if (w == 0) s_blk[lane] = 0;
 
   uint8_t* fb = block + (size_t)fan * L.stride;
   uint16_t* echo = reinterpret_cast<uint16_t*>(fb + L.echo_off);
@@ -202,7 +264,7 @@ __global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, Fram
       bool any_reset;
       const int keep = batch_slot_state(fp, j, my_batch, any_reset);
       if (!keep) frozen |= 1u << k;
-      if (w == 0 && (!keep || any_reset)) {
+      if (w == 0 && !single_slot && (!keep || any_reset)) {  // TC == 1: every slot is written once below
         echo[j] = 0;
         if (HITS) hpo[j] = z;
       }
@@ -256,34 +318,57 @@ __global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, Fram
       hpo[ray * H + k] = p;
     }
 
-    // visibility queries: q = 0 echo ray to the origin, q = 1..T muffle rays to the targets
+    // visibility pairs: q = 0 echo ray to the origin (:124-145), q = 1..T muffle rays (:150-173)
     const vec3 off = o - d * kEps;                 // :124, :158
     const float dist0 = distance(O, o);            // :130 (un-offset hit point)
-    uint32_t act = 0;
-    {
-      const Seg qs = make_seg(off, normalize(O - off));
-      const bool blk = blocked_chunk<false>(sc, qs, dist0, -1, w, K, !hit);
-      if (hit) act |= 1u;
-      if (hit && blk) atomicOr(&s_blk[lane], 1u);
-    }
-    for (int t = 0; t < T; ++t) {
-      const vec3 tp = load3(sc.targets, t);
-      const float dt = distance(off, tp);          // :165
-      const bool active = hit && dt < fp.max_muffle;  // :168
-      const Seg qs = make_seg(off, normalize(tp - off));
-      const bool blk = blocked_chunk<true>(sc, qs, dt, t, w, K, !active);
-      if (active) act |= 2u << t;
-      if (active && blk) atomicOr(&s_blk[lane], 2u << t);
+    if (w == 0) {
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      int np = 0;
+      for (int q = 0; q <= T; ++q) {
+        vec3 qdir;
+        float maxd;
+        bool act;
+        int owner;
+        if (q == 0) {
+          qdir = normalize(O - off); maxd = dist0; act = hit; owner = kNoOwner;
+        } else {
+          const vec3 tp = load3(sc.targets, q - 1);
+          maxd = distance(off, tp);                 // :165
+          act = hit && maxd < fp.max_muffle;        // :168
+          qdir = normalize(tp - off);
+          owner = q - 1;                            // :413, :426, :439
+        }
+        const unsigned long long m = __ballot(act);
+        const int pos = np + __popcll(m & lt);
+        if (act) {
+          const Seg g = make_seg(off, qdir);
+          PairSeg r;
+          r.ox = g.o.x; r.oy = g.o.y; r.oz = g.o.z; r.dx = g.d.x; r.dy = g.d.y; r.dz = g.d.z;
+          r.ix = g.inv.x; r.iy = g.inv.y; r.iz = g.inv.z; r.a2 = g.a2; r.a4 = g.a4; r.maxd = maxd;
+          r.owner = owner; r.pad0 = r.pad1 = r.pad2 = 0;
+          s_seg[pos] = r;
+        }
+        s_pairof[q][lane] = act ? (short)pos : (short)-1;
+        np += __popcll(m);
+      }
+      if (lane == 0) { s_np = np; s_head = 0; }
     }
     __syncthreads();
-    const uint32_t m = s_blk[lane];
+#ifdef ART_DIAG_NO_VISIBILITY  // diagnostic build only: time the nearest-hit phase alone
+    for (int p = w * 64 + lane; p < s_np; p += K * 64) s_res[p] = 0;
+#else
+    visibility_queue(sc, s_seg, s_res, &s_head, s_np, w, K, lane);
+#endif
     __syncthreads();
     if (w == 0) {
-      s_blk[lane] = 0;
-      if (hit && !(m & 1u) && live_slot) echo[ray * H + k] = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
-      const uint32_t clear = act & ~m;
+      const int pe = s_pairof[0][lane];
+      if (hit && live_slot) {
+        if (pe >= 0 && !s_res[pe]) echo[ray * H + k] = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
+        else if (single_slot) echo[ray * H + k] = 0;  // reset value (:76), written once
+      }
       for (int t = 0; t < T; ++t) {
-        if ((clear >> (t + 1)) & 1u) {  // :171
+        const int p = s_pairof[t + 1][lane];
+        if (p >= 0 && !s_res[p]) {  // :171
           if (single_slot) atomicAdd(&s_muf[t], 1u);
           else atomicAdd(&muffle_acc[((size_t)fan * fp.TC + my_slot) * T + t], 1u);
         }
@@ -298,7 +383,7 @@ __global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, Fram
         vec3 n = mk3(0.0f, 0.0f, 0.0f);
         float absorption = 0.0f;
         if (type == kAabb) {
-          const AabbRec b = sc.aabb[idx];
+          const AabbCold b = sc.aabbc[idx];
           vec3 lp = o - mk3(b.cx, b.cy, b.cz);
           vec3 ap = abs3(lp);
           float dx = b.hx - ap.x, dy = b.hy - ap.y, dz = b.hz - ap.z;
@@ -308,19 +393,20 @@ __global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, Fram
           absorption = b.absorption;
         } else if (type == kObb) {
           const ObbRec b = sc.obb[idx];
-          vec3 lh = qmul(inverse_q(b), o - mk3(b.cx, b.cy, b.cz));
+          const ObbCold bc = sc.obbc[idx];
+          vec3 lh = qmul(inverse_q(bc), o - mk3(b.cx, b.cy, b.cz));
           vec3 ap = abs3(lh);
-          vec3 df = mk3(b.hx, b.hy, b.hz) - ap;
+          vec3 df = mk3(bc.hx, bc.hy, bc.hz) - ap;
           vec3 ln = mk3(0.0f, 0.0f, 0.0f);
           if (df.x < df.y && df.x < df.z) ln.x = usign(lh.x);
           else if (df.y < df.x && df.y < df.z) ln.y = usign(lh.y);
           else ln.z = usign(lh.z);
           n = qmul(stored_q(b), ln);
-          absorption = b.absorption;
+          absorption = bc.absorption;
         } else {
           const SphereRec c = sc.sph[idx];
           n = normalize(o - mk3(c.cx, c.cy, c.cz));
-          absorption = c.absorption;
+          absorption = sc.sphc[idx].absorption;
         }
         d = reflect(d, n);
         o = o + d * kEps;
@@ -329,12 +415,23 @@ __global__ __launch_bounds__(64 * K) void raytrace_fast_kernel(DevScene sc, Fram
       }
     }
   }
-  if (HITS && valid && w == 0) fb[L.hit_counts_off + ray] = (uint8_t)hits;  // :204, :212
+  if (valid && w == 0) {
+    if (single_slot) {  // slots past the last hit keep the reset value 0 (:72-80)
+      const art_half3 z = {0, 0, 0};
+      for (int k = hits; k < H; ++k) {
+        echo[ray * H + k] = 0;
+        if (HITS) hpo[ray * H + k] = z;
+      }
+    }
+    if (HITS) fb[L.hit_counts_off + ray] = (uint8_t)hits;  // :204, :212
+  }
   __syncthreads();
   if (single_slot)
     for (int t = threadIdx.x; t < T; t += blockDim.x)
       if (s_muf[t]) atomicAdd(&muffle_acc[(size_t)fan * T + t], s_muf[t]);
 }
+
+int fast_max_targets() { return kMaxQueries - 1; }
 
 // Waves per 64-ray group: enough waves to cover the chip (~24 per CU), at most 8.
 int fast_split(int S, int R) {
@@ -348,10 +445,11 @@ template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st) {
   dim3 grid((fp.R + 63) / 64, fp.S), blk(64 * K);
+  const size_t lds = sizeof(PairSeg) * 64 * (size_t)(fp.T + 1);
   if (L.has_hits)
-    hipLaunchKernelGGL((raytrace_fast_kernel<K, true>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, ray_order);
+    hipLaunchKernelGGL((raytrace_fast_kernel<K, true>), grid, blk, lds, st, sc, fp, L, origins, block, muffle_acc, ray_order);
   else
-    hipLaunchKernelGGL((raytrace_fast_kernel<K, false>), grid, blk, 0, st, sc, fp, L, origins, block, muffle_acc, ray_order);
+    hipLaunchKernelGGL((raytrace_fast_kernel<K, false>), grid, blk, lds, st, sc, fp, L, origins, block, muffle_acc, ray_order);
 }
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,

@@ -149,7 +149,7 @@ def main():
     achieved_tflops = rt_flops / (rt_ms * 1e-3) / 1e12
     # algorithmic HBM bytes of one raytrace launch: collider AoS->SoA records are L2-resident after
     # the first wave, so the compulsory traffic is the SoA records + dirs + origins + outputs.
-    rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 64 + scene.obbs.size * 96
+    rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 32 + scene.obbs.size * 64  # hot records
     alg_bytes = rec_bytes + cfg.R * 6 + S * 12 + S * lay["stride"]
     hbm_gbs = alg_bytes / (rt_ms * 1e-3) / 1e9
     traffic = None
