@@ -47,6 +47,8 @@ ERROR_NAMES = {ART_E_INVALID: "ART_E_INVALID", ART_E_DEVICE: "ART_E_DEVICE", ART
 
 ART_CTX_COUNT_TESTS = 0x1
 ART_CTX_TIME_KERNELS = 0x2
+ART_CTX_FORCE_REFERENCE_ORDER = 0x4
+ART_CTX_WAVEFRONT = 0x8
 ART_OUT_HIT_RESULTS = 0x1
 
 ART_OWN_SPHERE, ART_OWN_AABB, ART_OWN_OBB = 0, 1, 2

@@ -22,9 +22,11 @@
 #include "../../include/art.h"
 #include "../../include/art_device.h"
 #include "art_internal.hpp"
+#include "art_wavefront.hpp"
 #include "unity_math.hpp"
 
 #include <cmath>
+#include <cstdlib>
 
 using namespace art;
 
@@ -94,6 +96,8 @@ struct Device {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
+  DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
+  int wf_blocks = 0;
   int fan_begin = 0, fan_count = 0;
   DevScene sc{};
   bool bound = false;
@@ -345,6 +349,42 @@ void count_nonowned(art_ctx* c, const art_frame_desc* d) {
   }
 }
 
+// Throughput raytrace implementation: the single-launch K-way block kernel (default, targets up
+// to fast_max_targets()) or the per-bounce wavefront pipeline (targets up to 31; selected for all
+// target counts with ART_RAYTRACE_KERNEL=wavefront, for comparisons).
+bool use_block_kernel() {
+  static const int v = [] {
+    const char* e = getenv("ART_RAYTRACE_KERNEL");
+    return (e && strcmp(e, "wavefront") == 0) ? 0 : 1;
+  }();
+  return v == 1;
+}
+
+int enqueue_wavefront(art_ctx* c, Device& dv, const Frame& f, const FrameParams& fp, const float* d_origins, int fan_count,
+                      uint8_t* d_block, uint32_t* acc, const int* ray_order, hipStream_t st) {
+  const size_t nr = (size_t)fan_count * f.R, Q = (size_t)f.T + 1;
+  if (nr * Q >= (1ull << 32)) return fail(c, ART_E_UNSUPPORTED, "fans * rays * (targets + 1) >= 2^32");
+  if (!dv.wf_rays.reserve(nr * sizeof(WfRay)) || !dv.wf_alive.reserve(2 * nr * 4) || !dv.wf_items.reserve(nr * Q * sizeof(WfItem)) ||
+      !dv.wf_flags.reserve(nr * Q) || !dv.wf_cnt.reserve((size_t)(f.H + 1) * sizeof(WfCounters)))
+    return fail(c, ART_E_NOMEM, "device allocation failed");
+  if (dv.wf_blocks == 0) dv.wf_blocks = wf_persistent_blocks();
+  HIP_TRY(c, hipMemsetAsync(dv.wf_cnt.p, 0, (size_t)(f.H + 1) * sizeof(WfCounters), st));
+  HIP_TRY(c, hipMemsetAsync(dv.wf_flags.p, 0, nr * Q, st));
+  WfArgs a{};
+  a.origins = d_origins;
+  a.block = d_block;
+  a.muffle_acc = acc;
+  a.ray_order = ray_order;
+  a.rays = static_cast<WfRay*>(dv.wf_rays.p);
+  a.alive[0] = static_cast<uint32_t*>(dv.wf_alive.p);
+  a.alive[1] = a.alive[0] + nr;
+  a.items = static_cast<WfItem*>(dv.wf_items.p);
+  a.flags = static_cast<uint8_t*>(dv.wf_flags.p);
+  a.cnt = static_cast<WfCounters*>(dv.wf_cnt.p);
+  for (int b = 0; b < f.H; ++b) wf_launch_bounce(dv.sc, fp, f.L, a, b, kWfParts, dv.wf_blocks, st);
+  return ART_OK;
+}
+
 hipEvent_t pool_event(Device& dv, size_t i) {
   while (dv.ev_pool.size() <= i) {
     hipEvent_t e;
@@ -392,10 +432,17 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     size_t ti = timing ? tstart(0) : 0;
     // The counting variant sweeps colliders in exact reference order per lane (its per-lane
     // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
-    if (count || f.T > fast_max_targets() || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER))
+    const int* order = reinterpret_cast<const int*>(raw + f.off_order);
+    if (count || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER)) {
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
-    else
-      launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, reinterpret_cast<const int*>(raw + f.off_order), st);
+    } else if (use_block_kernel() && !(c->flags & ART_CTX_WAVEFRONT) && f.T <= fast_max_targets()) {
+      launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, order, st);
+    } else if (f.T <= 31) {
+      int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);
+      if (rc) return rc;
+    } else {
+      launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
+    }
     if (timing) tstop(ti);
     HIP_TRY(c, hipGetLastError());
   }
@@ -486,6 +533,7 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
+    dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);

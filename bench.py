@@ -47,22 +47,29 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-fans", type=int, default=0, help="fans in the CPU-baseline sample (0 = auto)")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU-baseline sample")
     return p.parse_args()
 
 
-def cpu_baseline(cfg, scene, params, org, fans, threads):
-    """The oracle (C restatement of the reference jobs) timed on this host's cores."""
+def cpu_baseline(cfg, scene, params, org, fans, threads, min_seconds):
+    """The oracle (C restatement of the reference jobs) timed on this host's cores: whole frames
+    of `fans` fans, repeated until at least `min_seconds` of wall time (bounded sample)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle  # CPU baseline leg only
 
     sub = np.ascontiguousarray(org[:fans])
     out = art.FanOutputs(fans, cfg.R, cfg.H, cfg.T, 1)
     oracle.load()
+    tests, frames = 0, 0
     t0 = time.perf_counter()
-    _, counts = oracle.run(scene, params, sub, out, threads=threads)
-    dt = time.perf_counter() - t0
-    tests = sum(counts.values())
-    return tests / dt, dt, tests
+    while True:
+        _, counts = oracle.run(scene, params, sub, out, threads=threads)
+        tests += sum(counts.values())
+        frames += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds or frames >= 100:
+            break
+    return tests / dt, dt, tests, frames
 
 
 def main():
@@ -164,10 +171,10 @@ def main():
     if world == 1 and not a.no_cpu_baseline:
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
         fans = a.cpu_fans or S  # the full frame of this config (no extrapolation)
-        v, cdt, ctests = cpu_baseline(cfg, scene, params, org, fans, threads)
+        v, cdt, ctests, cframes = cpu_baseline(cfg, scene, params, org, fans, threads, a.cpu_seconds)
         cpu = {"value": v, "unit": "ray-collider tests/s", "cores": threads, "kind": "port",
-               "sample": f"{fans} of {S} fans of config {cfg.index} ({ctests} tests, {cdt:.1f} s) through the C "
-                         f"oracle (oracle/art_oracle.c, gcc -O3 -ffp-contract=off), one fan per task"}
+               "sample": f"{cframes} frames x {fans} of {S} fans of config {cfg.index} ({ctests} tests, {cdt:.1f} s) "
+                         f"through the C oracle (oracle/art_oracle.c, gcc -O3 -ffp-contract=off), one fan per task"}
 
     value = tests_all * a.steps / dt
     res = {

@@ -42,6 +42,9 @@ typedef struct {
 #define ART_CTX_TIME_KERNELS 0x2u
 /* Use the reference-order (one ray per lane) raytrace kernel instead of the K-way split one. */
 #define ART_CTX_FORCE_REFERENCE_ORDER 0x4u
+/* Use the per-bounce wavefront pipeline (nearest / compacted visibility queue / finalize) for
+ * frames with up to 31 targets instead of the single-launch K-way block kernel. */
+#define ART_CTX_WAVEFRONT 0x8u
 
 ART_API int art_fan_layout_get(const art_frame_desc* desc, uint32_t out_flags, art_fan_layout* out);
 

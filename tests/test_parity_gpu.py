@@ -32,10 +32,11 @@ def _diff_report(a: art.FanOutputs, b: art.FanOutputs) -> str:
     return "\n".join(lines)
 
 
-def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True):
-    """Run the frame through both raytrace kernels — the throughput (K-way split, coherent ray
-    order) kernel and the reference-order counting kernel — and require both to equal the
-    oracle bit for bit; the counting run's test counts must equal the oracle's."""
+def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True, wavefront=True):
+    """Run the frame through every raytrace implementation — the throughput block kernel (K-way
+    split, coherent ray order), the wavefront pipeline (ART_CTX_WAVEFRONT) and the reference-order
+    counting kernel — and require each to equal the oracle bit for bit; the counting run's test
+    counts must equal the oracle's."""
     S = org.shape[0]
     o_gpu = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, params.thread_count, hits=hits,
                            dsp=params.dsp is not None)
@@ -48,6 +49,13 @@ def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True):
     ctx.run(art.Frame(scene, params, org, o_gpu))
     eq = o_gpu.equal(o_ref)
     assert all(eq.values()), f"fast kernel: {eq}\n{_diff_report(o_gpu, o_ref)}"
+    if wavefront:
+        o_wf = o_cnt.copy()
+        ctx.set_flags(abi.ART_CTX_WAVEFRONT)
+        ctx.run(art.Frame(scene, params, org, o_wf))
+        ctx.set_flags(0)
+        eq = o_wf.equal(o_ref)
+        assert all(eq.values()), f"wavefront pipeline: {eq}\n{_diff_report(o_wf, o_ref)}"
     if counts:
         ctx.set_flags(abi.ART_CTX_COUNT_TESTS)
         ctx.run(art.Frame(scene, params, org, o_cnt))

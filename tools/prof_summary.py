@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Summarise one tools/gpu_round.sh output directory into profiles/ (committed evidence).
+
+  python tools/prof_summary.py gpurun_out/<tag> <tag>
+
+Writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_pmc.csv            per-kernel mean of every PMC counter collected (one pass each)
+  profiles/<tag>_bench.json         the bench line of the same round
+  profiles/traffic_config2.json     HBM bytes per raytrace launch from FETCH_SIZE / WRITE_SIZE,
+                                    corrected as MI355X_MICROARCH.md prescribes (bench.py reads it)
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "profiles")
+HOT = ("raytrace_fast_kernel", "wf_nearest", "wf_visibility", "wf_finalize", "raytrace_kernel", "permeate_kernel",
+       "reduce_kernel")
+
+
+def short(name: str) -> str:
+    base = name.split("(")[0].replace("void ", "").replace("art::", "")
+    return base
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    os.makedirs(PROF, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    bench = os.path.join(src, "bench.json")
+    if os.path.exists(bench):
+        shutil.copy(bench, os.path.join(PROF, f"{tag}_bench.json"))
+
+    # counter_collection.csv: one row per (dispatch, counter)
+    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values per dispatch
+    meta = {}
+    for f in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
+        acc = defaultdict(float)  # (dispatch, kernel, counter) -> sum over dimensions
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if not any(h in k for h in HOT):
+                continue
+            acc[(r["Dispatch_Id"], k, r["Counter_Name"])] += float(r["Counter_Value"])
+            meta[k] = {x: r[x] for x in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+                                         "Accum_VGPR_Count", "SGPR_Count")}
+        for (d, k, c), v in acc.items():
+            per[k][c].append(v)
+    rows = []
+    for k, cs in sorted(per.items()):
+        for c, vals in sorted(cs.items()):
+            rows.append({"kernel": k, "counter": c, "dispatches": len(vals), "mean": sum(vals) / len(vals),
+                         "min": min(vals), "max": max(vals), **meta.get(k, {})})
+    if rows:
+        with open(os.path.join(PROF, f"{tag}_pmc.csv"), "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+            w.writeheader()
+            w.writerows(rows)
+
+    # HBM traffic of the dominant (timed) raytrace kernel, per launch
+    dom = [k for k in per if k.startswith("raytrace_fast_kernel")]
+    if dom:
+        k = dom[0]
+        fetch_kb = sum(per[k]["FETCH_SIZE"]) / max(1, len(per[k]["FETCH_SIZE"]))
+        write_kb = sum(per[k]["WRITE_SIZE"]) / max(1, len(per[k]["WRITE_SIZE"]))
+        rec = {
+            "kernel": k,
+            "fetch_size_kb_raw": fetch_kb,
+            "write_size_kb": write_kb,
+            # MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE reports half the bytes of a
+            # wide read (64 B tallied per 128-B request) -> double it; WRITE_SIZE is exact.
+            "raytrace_bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0,
+            "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024; FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 note",
+            "source": f"profiles/{tag}_pmc.csv (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)",
+        }
+        json.dump(rec, open(os.path.join(PROF, "traffic_config2.json"), "w"), indent=1)
+        print(json.dumps(rec))
+    for r in rows:
+        print(f'{r["kernel"][:48]:48s} {r["counter"]:18s} {r["mean"]:.4g}')
+
+
+if __name__ == "__main__":
+    main()
