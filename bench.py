@@ -197,7 +197,7 @@ def main():
                    "parallelism": f"fan-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
         "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "raytrace_kernel", "kernel_ms": rt_ms,
+                     "kernel": "raytrace_fast_kernel", "kernel_ms": rt_ms,
                      "note": "FP32 VALU roof (no MFMA-shaped work); algorithmic ops per test per SURVEY.md 8(d)",
                      "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
                              "algorithmic_bytes": alg_bytes}},
