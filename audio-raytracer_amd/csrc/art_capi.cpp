@@ -96,6 +96,7 @@ struct Device {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
+  DevBuf work;  // ticket counters of the persistent raytrace kernel (self-rearming, zeroed once)
   DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
   int wf_blocks = 0;
   int fan_begin = 0, fan_count = 0;
@@ -436,7 +437,11 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     if (count || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER)) {
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
     } else if (use_block_kernel() && !(c->flags & ART_CTX_WAVEFRONT) && f.T <= fast_max_targets()) {
-      launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, order, st);
+      if (!dv.work.p) {
+        if (!dv.work.reserve(256)) return fail(c, ART_E_NOMEM, "device allocation failed");
+        HIP_TRY(c, hipMemsetAsync(dv.work.p, 0, 256, st));
+      }
+      launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), st);
     } else if (f.T <= 31) {
       int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);
       if (rc) return rc;
@@ -533,6 +538,7 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
+    dv.work.release();
     dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);

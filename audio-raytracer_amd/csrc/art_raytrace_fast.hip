@@ -232,17 +232,31 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
                                                                uint32_t* __restrict__ muffle_acc,
-                                                               const int* __restrict__ ray_order) {
+                                                               const int* __restrict__ ray_order,
+                                                               uint32_t* __restrict__ work) {
   __shared__ float s_dist[K][64];
   __shared__ int s_code[K][64];
   __shared__ short s_pairof[kMaxQueries][64];
   __shared__ uint8_t s_res[kMaxQueries * 64];
   __shared__ int s_head, s_np;
   __shared__ uint32_t s_muf[kMaxTargets];
+  __shared__ int s_ticket;
   extern __shared__ PairSeg s_seg[];  // [64 * (T + 1)]
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int fan = blockIdx.y;
-  const int slot = blockIdx.x * 64 + lane;
+  // wave index as an SGPR value: chunk bounds and loop counters of the sweeps stay scalar
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nrb = (fp.R + 63) >> 6;  // 64-ray groups per fan
+  const int ngroups = fp.S * nrb;
+  // Persistent grid: the launch holds as many workgroups as are co-resident, and each pulls
+  // 64-ray groups from a global ticket counter until the frame is drained (no partial last
+  // round of workgroups, and uneven visibility work balances itself).
+  for (;;) {
+  __syncthreads();  // the previous group's LDS reads are done
+  if (threadIdx.x == 0) s_ticket = (int)atomicAdd(&work[0], 1u);
+  __syncthreads();
+  const int g = __builtin_amdgcn_readfirstlane(s_ticket);
+  if (g >= ngroups) break;
+  const int fan = g / nrb;
+  const int slot = (g - fan * nrb) * 64 + lane;
   const bool valid = slot < fp.R;
   const int ray = valid ? ray_order[slot] : 0;
   const int T = fp.T, H = fp.H;
@@ -429,6 +443,13 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
   if (single_slot)
     for (int t = threadIdx.x; t < T; t += blockDim.x)
       if (s_muf[t]) atomicAdd(&muffle_acc[(size_t)fan * T + t], s_muf[t]);
+  }
+  // Every workgroup has drawn its final (out-of-range) ticket before it arrives here, so the last
+  // arrival can rearm the counter for the next launch on this stream.
+  if (threadIdx.x == 0 && atomicAdd(&work[1], 1u) == gridDim.x - 1) {
+    atomicExch(&work[0], 0u);
+    atomicExch(&work[1], 0u);
+  }
 }
 
 int fast_max_targets() { return kMaxQueries - 1; }
@@ -441,25 +462,53 @@ int fast_split(int S, int R) {
   return K;
 }
 
+// Co-resident workgroups of one kernel instance on the current device (cached per LDS size).
+template <typename Kern>
+static int resident_blocks(Kern kern, int threads, size_t lds) {
+  static thread_local int dev_cached = -1, cus = 0;
+  static thread_local size_t lds_cached = ~size_t(0);
+  static thread_local int per_cu = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != dev_cached) {
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    dev_cached = dev;
+    lds_cached = ~size_t(0);
+  }
+  if (lds != lds_cached) {
+    per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) per_cu = 0;
+    lds_cached = lds;
+  }
+  return std::max(1, per_cu) * std::max(1, cus);
+}
+
+template <int K, bool HITS>
+static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
+  const size_t lds = sizeof(PairSeg) * 64 * (size_t)(fp.T + 1);
+  const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
+  const int resident = resident_blocks(raytrace_fast_kernel<K, HITS>, 64 * K, lds);
+  const int nblk = (int)std::min<long long>(groups, resident);
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
+                     muffle_acc, ray_order, work);
+}
+
 template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st) {
-  dim3 grid((fp.R + 63) / 64, fp.S), blk(64 * K);
-  const size_t lds = sizeof(PairSeg) * 64 * (size_t)(fp.T + 1);
-  if (L.has_hits)
-    hipLaunchKernelGGL((raytrace_fast_kernel<K, true>), grid, blk, lds, st, sc, fp, L, origins, block, muffle_acc, ray_order);
-  else
-    hipLaunchKernelGGL((raytrace_fast_kernel<K, false>), grid, blk, lds, st, sc, fp, L, origins, block, muffle_acc, ray_order);
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
+  if (L.has_hits) launch_fast_kh<K, true>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+  else launch_fast_kh<K, false>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
 }
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, hipStream_t st) {
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
   if (fp.S == 0) return;
   switch (fast_split(fp.S, fp.R)) {
-    case 1: launch_fast_k<1>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
-    case 2: launch_fast_k<2>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
-    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
-    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, st); break;
+    case 1: launch_fast_k<1>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
+    case 2: launch_fast_k<2>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
+    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
+    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
   }
 }
 
