@@ -107,7 +107,10 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
 // colliders, so the cyclic chunk order gives the reference's verdict, and a wave only keeps
 // sweeping for lanes that are still unblocked.
 // ------------------------------------------------------------------------------------------
-constexpr int kChunk = 64;     // colliders per chunk
+#ifndef ART_FAST_CHUNK
+#define ART_FAST_CHUNK 64
+#endif
+constexpr int kChunk = ART_FAST_CHUNK;  // colliders per chunk
 constexpr int kMaxQueries = 8; // echo + up to 7 targets per ray (larger T uses raytrace_kernel)
 constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
 
@@ -219,7 +222,7 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 }
 
 #ifndef ART_FAST_WAVES_PER_EU
-#define ART_FAST_WAVES_PER_EU 0
+#define ART_FAST_WAVES_PER_EU 7  // <= 72 VGPRs: measured best on config 2/5 (6: -1 %, 8: -1 %, none: -10 %)
 #endif
 #if ART_FAST_WAVES_PER_EU > 0
 #define ART_FAST_OCC __attribute__((amdgpu_waves_per_eu(ART_FAST_WAVES_PER_EU)))
@@ -241,6 +244,9 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
   __shared__ int s_head, s_np;
   __shared__ uint32_t s_muf[kMaxTargets];
   __shared__ int s_ticket;
+#ifdef ART_TEST_NO_OBB
+  sc.no = 0;
+#endif
   extern __shared__ PairSeg s_seg[];  // [64 * (T + 1)]
   // wave index as an SGPR value: chunk bounds and loop counters of the sweeps stay scalar
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -456,6 +462,9 @@ int fast_max_targets() { return kMaxQueries - 1; }
 
 // Waves per 64-ray group: enough waves to cover the chip (~24 per CU), at most 8.
 int fast_split(int S, int R) {
+#ifdef ART_FAST_FORCE_K
+  return ART_FAST_FORCE_K;
+#endif
   const long long groups = (long long)S * ((R + 63) / 64);
   int K = 1;
   while (K < 8 && groups * K < 256LL * 24) K *= 2;

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build libart.so with extra compile flags into variants/libart_<name>.so (A/B experiments;
+# bench.py / tests pick it up through ART_LIB=variants/libart_<name>.so).
+#   tools/build_variant.sh <name> [-DFLAG ...]
+set -euo pipefail
+name=$1; shift
+root=$(cd "$(dirname "$0")/.." && pwd)
+pkg=$root/audio-raytracer_amd
+tmp=$(mktemp -d)
+mkdir -p "$root/variants"
+flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden "$@")
+for f in art_kernels art_raytrace_fast art_wavefront; do
+  hipcc "${flags[@]}" -c "$pkg/csrc/$f.hip" -o "$tmp/$f.o" &
+done
+hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_capi.cpp" -o "$tmp/art_capi.o" &
+hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_synth.cpp" -o "$tmp/art_synth.o" &
+wait
+hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/variants/libart_$name.so" "$tmp"/*.o
+rm -rf "$tmp"
+echo "variants/libart_$name.so"
