@@ -19,10 +19,6 @@
 
 namespace art {
 
-#ifndef ART_FAST_UNROLL
-#define ART_FAST_UNROLL 4
-#endif
-constexpr int kU = ART_FAST_UNROLL;  // sweep unroll
 constexpr int kNoHit = 0x7fffffff;
 
 __device__ __forceinline__ void chunk_of(int n, int w, int K, int& b, int& e) {
@@ -51,18 +47,19 @@ __device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c
 
 // First minimum of this wave's chunk (ShootRayCast :225-280 restricted to a sub-range).
 // code = type rank (sphere 0, aabb 1, obb 2) << 28 | index: the global reference order.
+template <int U>
 __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, int w, int K, float& best, int& code) {
   best = FLT_MAX;
   code = kNoHit;
   int b, e;
   chunk_of(sc.ns, w, K, b, e);
   int i = b;
-  for (; i + kU <= e; i += kU) {
-    SphereRec c[kU];
+  for (; i + U <= e; i += U) {
+    SphereRec c[U];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) c[u] = ldc(sc.sph, wave_uniform(i + u));
+    for (int u = 0; u < U; ++u) c[u] = ldc(sc.sph, wave_uniform(i + u));
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < U; ++u) {
       float d;
       if (sphere_hit_dist(s, c[u], d) && d < best) { best = d; code = i + u; }
     }
@@ -74,12 +71,12 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
   }
   chunk_of(sc.na, w, K, b, e);
   i = b;
-  for (; i + kU <= e; i += kU) {
-    AabbRec r[kU];
+  for (; i + U <= e; i += U) {
+    AabbRec r[U];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) r[u] = ldc(sc.aabb, wave_uniform(i + u));
+    for (int u = 0; u < U; ++u) r[u] = ldc(sc.aabb, wave_uniform(i + u));
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < U; ++u) {
       float d;
       if (aabb_test<false>(s, r[u], d) && d < best) { best = d; code = (1 << 28) | (i + u); }
     }
@@ -107,6 +104,9 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
 // colliders, so the cyclic chunk order gives the reference's verdict, and a wave only keeps
 // sweeping for lanes that are still unblocked.
 // ------------------------------------------------------------------------------------------
+#ifndef ART_FAST_STAGED
+#define ART_FAST_STAGED 0  // 1: visibility records staged through LDS (measured slower: lower occupancy, barrier waits)
+#endif
 #ifndef ART_FAST_CHUNK
 #define ART_FAST_CHUNK 64
 #endif
@@ -114,11 +114,13 @@ constexpr int kChunk = ART_FAST_CHUNK;  // colliders per chunk
 constexpr int kMaxQueries = 8; // echo + up to 7 targets per ray (larger T uses raytrace_kernel)
 constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
 
+// One (ray, query) visibility segment, 48 B (3 x ds_read_b128). a4 = 4a is not stored: it equals
+// 2 * a2 exactly (a power-of-two scaling of the same value).
 struct alignas(16) PairSeg {
   float ox, oy, oz, dx;
   float dy, dz, ix, iy;
-  float iz, a2, a4, maxd;
-  int owner, pad0, pad1, pad2;
+  float iz, a2, maxd;
+  int owner;
 };
 
 struct ChunkMap {
@@ -127,26 +129,45 @@ struct ChunkMap {
 };
 
 // Test one chunk for this lane's pair. `done` lanes (free or blocked) do not change.
-template <typename Rec, typename Test>
+template <int U, typename Rec, typename Test>
 __device__ __forceinline__ bool sweep_records(const Rec* recs, int b, int e, bool blocked, bool done, Test test) {
   int i = b;
-  for (; i + kU <= e; i += kU) {
-    Rec r[kU];
+#ifdef ART_FAST_PIPELINE
+  // software-pipelined: the scalar loads of the next pair are in flight while this pair is tested
+  if (i + 2 <= e) {
+    Rec c0 = ldc(recs, i), c1 = ldc(recs, i + 1);
+    for (; i + 4 <= e; i += 2) {
+      const Rec n0 = ldc(recs, i + 2), n1 = ldc(recs, i + 3);
+      blocked |= test(c0);
+      blocked |= test(c1);
+      c0 = n0; c1 = n1;
+      if (((i - b) & 2) && __all(blocked || done)) return blocked;
+    }
+    blocked |= test(c0);
+    blocked |= test(c1);
+    i += 2;
+  }
+  for (; i < e; ++i) blocked |= test(ldc(recs, i));
+  return blocked;
+#endif
+  for (; i + U <= e; i += U) {
+    Rec r[U];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) r[u] = ldc(recs, wave_uniform(i + u));
+    for (int u = 0; u < U; ++u) r[u] = ldc(recs, wave_uniform(i + u));
 #pragma unroll
-    for (int u = 0; u < kU; ++u) blocked |= test(r[u]);
+    for (int u = 0; u < U; ++u) blocked |= test(r[u]);
     if (__all(blocked || done)) return blocked;
   }
   for (; i < e; ++i) blocked |= test(ldc(recs, wave_uniform(i)));
   return blocked;
 }
 
+template <int U>
 __device__ __forceinline__ bool sweep_chunk(const DevScene& sc, const ChunkMap& cm, int c, const Seg& s, float maxd,
                                             int owner, bool blocked, bool done) {
   if (c < cm.cs) {
     const int b = c * kChunk, e = min(b + kChunk, sc.ns);
-    return sweep_records(sc.sph, b, e, blocked, done, [&](const SphereRec& r) {
+    return sweep_records<U>(sc.sph, b, e, blocked, done, [&](const SphereRec& r) {
       float d;
       return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
     });
@@ -154,7 +175,7 @@ __device__ __forceinline__ bool sweep_chunk(const DevScene& sc, const ChunkMap& 
   c -= cm.cs;
   if (c < cm.ca) {
     const int b = c * kChunk, e = min(b + kChunk, sc.na);
-    return sweep_records(sc.aabb, b, e, blocked, done, [&](const AabbRec& r) {
+    return sweep_records<U>(sc.aabb, b, e, blocked, done, [&](const AabbRec& r) {
       float d;
       return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
     });
@@ -171,6 +192,7 @@ __device__ __forceinline__ bool sweep_chunk(const DevScene& sc, const ChunkMap& 
 }
 
 // Drain the block's pair queue. Results: s_res[p] = 1 if pair p is blocked.
+template <int U>
 __device__ __forceinline__ void visibility_queue(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
                                                  int np, int w, int K, int lane) {
   const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
@@ -200,7 +222,7 @@ __device__ __forceinline__ void visibility_queue(const DevScene& sc, const PairS
         if (p < np) {
           const PairSeg g = s_seg[p];
           s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
-          s.a2 = g.a2; s.a4 = g.a4;
+          s.a2 = g.a2; s.a4 = 2.0f * g.a2;
           maxd = g.maxd; owner = g.owner;
           my = p; left = nchunks; blocked = false;
         }
@@ -208,7 +230,7 @@ __device__ __forceinline__ void visibility_queue(const DevScene& sc, const PairS
     }
     const bool active = my >= 0;
     if (__all(!active)) break;
-    blocked = sweep_chunk(sc, cm, c, s, maxd, owner, blocked, !active);
+    blocked = sweep_chunk<U>(sc, cm, c, s, maxd, owner, blocked, !active);
     if (active) {
       left -= 1;
       if (blocked || left == 0) { s_res[my] = blocked ? 1 : 0; my = -1; }
@@ -217,21 +239,189 @@ __device__ __forceinline__ void visibility_queue(const DevScene& sc, const PairS
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-staged variant of the visibility queue. The block's waves sweep the rotating chunk order
+// together: chunk c+1 is copied global -> LDS (global_load_lds, no VGPR staging) while chunk c is
+// tested, and every wave reads the records of the current chunk from LDS (broadcast ds_read_b128:
+// one LDS cycle per lane group). This takes the collider stream off the scalar path, where about
+// half of all record loads waited for an L2 round trip (SQC_DCACHE_MISSES + _DUPLICATE, r01
+// profile). The per-lane logic (refill at chunk boundaries, leave when blocked or after a full
+// cycle) is that of visibility_queue.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// Bytes of one staging buffer: a chunk of the largest record type present in the scene.
+__host__ __device__ __forceinline__ int stage_stride(const DevScene& sc) {
+  return kChunk * (sc.no > 0 ? (int)sizeof(ObbRec) : (int)sizeof(SphereRec) > (int)sizeof(AabbRec) ? (int)sizeof(SphereRec) : (int)sizeof(AabbRec));
+}
+
+// Copy `bytes` (a multiple of 1 KiB) starting at g into LDS at dst; wave w of K copies KiB w, w+K,
+// ... (one global_load_lds_dwordx4 = 64 lanes x 16 B per KiB).
+__device__ __forceinline__ void stage_chunk(const uint8_t* g, uint8_t* dst, int bytes, int w, int K, int lane) {
+  for (int off = w * 1024; off < bytes; off += K * 1024)
+    __builtin_amdgcn_global_load_lds((const void*)(g + off + lane * 16), (lds_void_t*)(dst + off), 16, 0, 0);
+}
+
+__device__ __forceinline__ void chunk_src(const DevScene& sc, const ChunkMap& cm, int c, const uint8_t*& src, int& n,
+                                          int& bytes) {
+  if (c < cm.cs) {
+    const int b = c * kChunk;
+    n = min(kChunk, sc.ns - b);
+    src = reinterpret_cast<const uint8_t*>(sc.sph + b);
+    bytes = kChunk * (int)sizeof(SphereRec);
+    return;
+  }
+  c -= cm.cs;
+  if (c < cm.ca) {
+    const int b = c * kChunk;
+    n = min(kChunk, sc.na - b);
+    src = reinterpret_cast<const uint8_t*>(sc.aabb + b);
+    bytes = kChunk * (int)sizeof(AabbRec);
+    return;
+  }
+  c -= cm.ca;
+  const int b = c * kChunk;
+  n = min(kChunk, sc.no - b);
+  src = reinterpret_cast<const uint8_t*>(sc.obb + b);
+  bytes = kChunk * (int)sizeof(ObbRec);
+}
+
+template <int U, typename Test>
+__device__ __forceinline__ bool sweep_lds(int n, bool blocked, bool done, Test test) {
+  int i = 0;
+  for (; i + U <= n; i += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) blocked |= test(i + u);
+    if (__all(blocked || done)) return blocked;
+  }
+  for (; i < n; ++i) blocked |= test(i);
+  return blocked;
+}
+
+template <int U>
+__device__ __forceinline__ bool sweep_chunk_lds(const ChunkMap& cm, int c, int n, const uint8_t* buf, const Seg& s,
+                                                float maxd, int owner, bool blocked, bool done) {
+  if (c < cm.cs) {
+    const float4* r4 = reinterpret_cast<const float4*>(buf);
+    return sweep_lds<U>(n, blocked, done, [&](int i) {
+      const float4 a = r4[2 * i];  // cx, cy, cz, r2
+      SphereRec r;
+      r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
+      float d;
+      bool hit = sphere_hit_dist(s, r, d) && d < maxd;
+      if (hit) hit = reinterpret_cast<const int*>(buf)[8 * i + 4] != owner;  // tid, read only on a hit
+      return hit;
+    });
+  }
+  if (c - cm.cs < cm.ca) {
+    const AabbRec* rr = reinterpret_cast<const AabbRec*>(buf);
+    return sweep_lds<U>(n, blocked, done, [&](int i) {
+      const AabbRec r = rr[i];
+      float d;
+      return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+    });
+  }
+  const ObbRec* rr = reinterpret_cast<const ObbRec*>(buf);
+  for (int i = 0; i < n; ++i) {
+    const ObbRec r = rr[i];
+    float d;
+    blocked |= obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+    if ((i & 3) == 3 && __all(blocked || done)) return blocked;
+  }
+  return blocked;
+}
+
+// stage: 2 buffers of kChunk * 64 B (the largest record) after the pair segments.
+template <int U>
+__device__ __forceinline__ void visibility_staged(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
+                                                  int* s_go, uint8_t* stage, int np, int w, int K, int lane) {
+  const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
+  const int nchunks = cm.total();
+  if (nchunks == 0 || np == 0) {  // no collider: nothing blocks
+    for (int p = w * 64 + lane; p < np; p += K * 64) s_res[p] = 0;
+    return;
+  }
+  const int kBuf = stage_stride(sc);
+  int c = 0;
+  {
+    const uint8_t* src; int n, bytes;
+    chunk_src(sc, cm, 0, src, n, bytes);
+    stage_chunk(src, stage, bytes, w, K, lane);
+  }
+  int my = -1, left = 0;
+  bool blocked = false;
+  Seg s;
+  float maxd = 0.0f;
+  int owner = kNoOwner;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int it = 0;; ++it) {
+    // refill free lanes from the block's pair queue
+    const bool need = my < 0;
+    const unsigned long long m = __ballot(need);
+    if (m) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(s_head, __popcll(m));
+      base = __shfl(base, 0, 64);
+      if (need) {
+        const int p = base + __popcll(m & lt);
+        if (p < np) {
+          const PairSeg g = s_seg[p];
+          s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
+          s.a2 = g.a2; s.a4 = 2.0f * g.a2;
+          maxd = g.maxd; owner = g.owner;
+          my = p; left = nchunks; blocked = false;
+        }
+      }
+    }
+    const bool active = my >= 0;
+    const bool wave_active = __any(active);
+    // block vote (triple-buffered flag: slot it%3 is read after this barrier, reset two rounds later)
+    if (threadIdx.x == 0) s_go[(it + 1) % 3] = 0;
+    if (lane == 0 && wave_active) s_go[it % 3] = 1;
+    __syncthreads();  // also retires the staging copy of chunk c (vmcnt drained before the barrier)
+    if (!s_go[it % 3]) break;
+    const int cn = (c + 1 == nchunks) ? 0 : c + 1;
+    const uint8_t* cur = stage + (it & 1) * kBuf;
+    {
+      const uint8_t* src; int n, bytes;
+      chunk_src(sc, cm, cn, src, n, bytes);
+      stage_chunk(src, stage + ((it + 1) & 1) * kBuf, bytes, w, K, lane);
+    }
+    if (wave_active) {
+      const uint8_t* src; int n, bytes;
+      chunk_src(sc, cm, c, src, n, bytes);
+      blocked = sweep_chunk_lds<U>(cm, c, n, cur, s, maxd, owner, blocked, !active);
+      if (active) {
+        left -= 1;
+        if (blocked || left == 0) { s_res[my] = blocked ? 1 : 0; my = -1; }
+      }
+    }
+    c = cn;
+  }
+}
+
 __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
   return type == kSphere ? sc.sphc[idx].echo : (type == kAabb ? sc.aabbc[idx].echo : sc.obbc[idx].echo);
 }
 
-#ifndef ART_FAST_WAVES_PER_EU
-#define ART_FAST_WAVES_PER_EU 7  // <= 72 VGPRs: measured best on config 2/5 (6: -1 %, 8: -1 %, none: -10 %)
+// Occupancy target (amdgpu_waves_per_eu) and sweep unroll per scene kind, chosen by measurement on
+// MI355X: scenes without OBBs (config 2) run best at 6 waves/SIMD with 8 records per scalar-load
+// group (more loads in flight per s_waitcnt); OBB scenes (configs 3-5) at 7 waves/SIMD, unroll 4.
+#ifndef ART_FAST_WPE_NO_OBB
+#define ART_FAST_WPE_NO_OBB 6
 #endif
-#if ART_FAST_WAVES_PER_EU > 0
-#define ART_FAST_OCC __attribute__((amdgpu_waves_per_eu(ART_FAST_WAVES_PER_EU)))
-#else
-#define ART_FAST_OCC
+#ifndef ART_FAST_U_NO_OBB
+#define ART_FAST_U_NO_OBB 8
+#endif
+#ifndef ART_FAST_WPE_OBB
+#define ART_FAST_WPE_OBB 7
+#endif
+#ifndef ART_FAST_U_OBB
+#define ART_FAST_U_OBB 4
 #endif
 
-template <int K, bool HITS>
-__global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
+template <int K, bool HITS, int U, int WPE>
+__global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
                                                                uint32_t* __restrict__ muffle_acc,
@@ -244,10 +434,14 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
   __shared__ int s_head, s_np;
   __shared__ uint32_t s_muf[kMaxTargets];
   __shared__ int s_ticket;
+  __shared__ int s_go[3];  // staged visibility only
+  (void)s_go;
 #ifdef ART_TEST_NO_OBB
   sc.no = 0;
 #endif
-  extern __shared__ PairSeg s_seg[];  // [64 * (T + 1)]
+  extern __shared__ PairSeg s_seg[];  // [64 * (T + 1)], then (staged visibility) 2 chunk buffers
+  uint8_t* s_stage = reinterpret_cast<uint8_t*>(s_seg + 64 * (fp.T + 1));
+  (void)s_stage;
   // wave index as an SGPR value: chunk bounds and loop counters of the sweeps stay scalar
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;  // 64-ray groups per fan
@@ -303,7 +497,7 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
     const Seg s = make_seg(o, d);
     float best;
     int code;
-    nearest_chunk(sc, s, w, K, best, code);
+    nearest_chunk<U>(sc, s, w, K, best, code);
     s_dist[w][lane] = best;
     s_code[w][lane] = code;
     __syncthreads();
@@ -364,8 +558,8 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
           const Seg g = make_seg(off, qdir);
           PairSeg r;
           r.ox = g.o.x; r.oy = g.o.y; r.oz = g.o.z; r.dx = g.d.x; r.dy = g.d.y; r.dz = g.d.z;
-          r.ix = g.inv.x; r.iy = g.inv.y; r.iz = g.inv.z; r.a2 = g.a2; r.a4 = g.a4; r.maxd = maxd;
-          r.owner = owner; r.pad0 = r.pad1 = r.pad2 = 0;
+          r.ix = g.inv.x; r.iy = g.inv.y; r.iz = g.inv.z; r.a2 = g.a2; r.maxd = maxd;
+          r.owner = owner;
           s_seg[pos] = r;
         }
         s_pairof[q][lane] = act ? (short)pos : (short)-1;
@@ -376,8 +570,10 @@ __global__ __launch_bounds__(64 * K) ART_FAST_OCC void raytrace_fast_kernel(DevS
     __syncthreads();
 #ifdef ART_DIAG_NO_VISIBILITY  // diagnostic build only: time the nearest-hit phase alone
     for (int p = w * 64 + lane; p < s_np; p += K * 64) s_res[p] = 0;
+#elif ART_FAST_STAGED
+    visibility_staged<U>(sc, s_seg, s_res, &s_head, s_go, s_stage, s_np, w, K, lane);
 #else
-    visibility_queue(sc, s_seg, s_res, &s_head, s_np, w, K, lane);
+    visibility_queue<U>(sc, s_seg, s_res, &s_head, s_np, w, K, lane);
 #endif
     __syncthreads();
     if (w == 0) {
@@ -471,43 +667,50 @@ int fast_split(int S, int R) {
   return K;
 }
 
-// Co-resident workgroups of one kernel instance on the current device (cached per LDS size).
-template <typename Kern>
-static int resident_blocks(Kern kern, int threads, size_t lds) {
-  static thread_local int dev_cached = -1, cus = 0;
-  static thread_local size_t lds_cached = ~size_t(0);
-  static thread_local int per_cu = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev != dev_cached) {
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    dev_cached = dev;
-    lds_cached = ~size_t(0);
-  }
-  if (lds != lds_cached) {
-    per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) per_cu = 0;
-    lds_cached = lds;
-  }
-  return std::max(1, per_cu) * std::max(1, cus);
+static size_t fast_lds_bytes(const DevScene& sc, int T) {
+  return sizeof(PairSeg) * 64 * (size_t)(T + 1) + (ART_FAST_STAGED ? 2 * (size_t)stage_stride(sc) : 0);
 }
 
-template <int K, bool HITS>
+// Co-resident workgroups of one kernel instance on the current device, cached per (device,
+// kernel, dynamic LDS bytes).
+template <typename Kern>
+static int resident_blocks(Kern kern, int threads, size_t lds) {
+  struct Entry { int dev; const void* fn; size_t lds; int blocks; };
+  static thread_local std::vector<Entry> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const void* fn = reinterpret_cast<const void*>(kern);
+  for (const Entry& e : cache)
+    if (e.dev == dev && e.fn == fn && e.lds == lds) return e.blocks;
+  int cus = 0, per_cu = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) per_cu = 0;
+  const int blocks = std::max(1, per_cu) * std::max(1, cus);
+  cache.push_back({dev, fn, lds, blocks});
+  return blocks;
+}
+
+template <int K, bool HITS, int U, int WPE>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
-  const size_t lds = sizeof(PairSeg) * 64 * (size_t)(fp.T + 1);
+  const size_t lds = fast_lds_bytes(sc, fp.T);
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
-  const int resident = resident_blocks(raytrace_fast_kernel<K, HITS>, 64 * K, lds);
+  const int resident = resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE>, 64 * K, lds);
   const int nblk = (int)std::min<long long>(groups, resident);
-  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
                      muffle_acc, ray_order, work);
 }
 
 template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
-  if (L.has_hits) launch_fast_kh<K, true>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
-  else launch_fast_kh<K, false>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+  if (sc.no > 0) {
+    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+    else launch_fast_kh<K, false, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+  } else {
+    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+    else launch_fast_kh<K, false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+  }
 }
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,

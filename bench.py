@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-fans", type=int, default=0, help="fans in the CPU-baseline sample (0 = auto)")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--collider-scale", type=float, default=None,
+                   help="scale the config's collider count (experiments only; the metric is quoted at 1)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU-baseline sample")
     return p.parse_args()
 
@@ -88,7 +90,7 @@ def main():
 
     cfg = art.CONFIGS[a.config]
     S_total = cfg.S * world
-    scene, org_all, params = art.synth(cfg, S=S_total)
+    scene, org_all, params = art.synth(cfg, S=S_total, C_scale=a.collider_scale)
     org = np.ascontiguousarray(org_all[rank * cfg.S:(rank + 1) * cfg.S])
     S = cfg.S
     ctx = art.Context(1 << torch.cuda.current_device())
