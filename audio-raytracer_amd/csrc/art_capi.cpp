@@ -88,7 +88,7 @@ struct Frame {
   // input staging layout (bytes)
   size_t off_sph = 0, off_aabb = 0, off_obb = 0, off_tgt = 0, off_dirs = 0, off_vol = 0, off_muf = 0, off_tab = 0,
          off_reset = 0, off_order = 0, raw_bytes = 0;
-  size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_bytes = 0;
+  size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_cull = 0, soa_bytes = 0;
 };
 
 struct Device {
@@ -294,6 +294,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
   f.soa_sphc = s; s = align_up(s + (size_t)f.ns * sizeof(SphereCold), 256);
   f.soa_aabbc = s; s = align_up(s + (size_t)f.na * sizeof(AabbCold), 256);
   f.soa_obbc = s; s = align_up(s + (size_t)f.no * sizeof(ObbCold), 256);
+  f.soa_cull = s; s = align_up(s + (size_t)(f.ns + f.na + f.no) * sizeof(CullRec), 256);
   f.soa_bytes = s;
 }
 
@@ -321,7 +322,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
               f.na, reinterpret_cast<const art_obb*>(raw + f.off_obb), f.no, reinterpret_cast<SphereRec*>(soa + f.soa_sph),
               reinterpret_cast<SphereCold*>(soa + f.soa_sphc), reinterpret_cast<AabbRec*>(soa + f.soa_aabb),
               reinterpret_cast<AabbCold*>(soa + f.soa_aabbc), reinterpret_cast<ObbRec*>(soa + f.soa_obb),
-              reinterpret_cast<ObbCold*>(soa + f.soa_obbc), dv.stream);
+              reinterpret_cast<ObbCold*>(soa + f.soa_obbc), reinterpret_cast<CullRec*>(soa + f.soa_cull), dv.stream);
   HIP_TRY(c, hipGetLastError());
   DevScene& sc = dv.sc;
   sc.sph = reinterpret_cast<const SphereRec*>(soa + f.soa_sph); sc.ns = f.ns;
@@ -330,6 +331,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sc.sphc = reinterpret_cast<const SphereCold*>(soa + f.soa_sphc);
   sc.aabbc = reinterpret_cast<const AabbCold*>(soa + f.soa_aabbc);
   sc.obbc = reinterpret_cast<const ObbCold*>(soa + f.soa_obbc);
+  sc.cull = reinterpret_cast<const CullRec*>(soa + f.soa_cull);
   sc.targets = reinterpret_cast<const float*>(raw + f.off_tgt); sc.T = f.T;
   sc.dirs = reinterpret_cast<const uint16_t*>(raw + f.off_dirs); sc.R = f.R;
   dv.bound = true;

@@ -53,12 +53,22 @@ struct alignas(16) ObbCold {  // 48 B
   float absorption, density, pad0, pad1;
 };
 
+// Broad-phase bounds of one collider (global order: spheres, AABBs, OBBs). A segment set whose
+// bounding box B can be blocked by the collider only if [lo - m, hi + m] overlaps B, with the
+// error margin m = factor * (scale + Omax) (Omax bounds |o|_1 + maxd over the set): see
+// DESIGN.md §5 (broad phase). Non-finite colliders get infinite bounds (always candidates).
+struct alignas(16) CullRec {
+  float lox, loy, loz, scale;
+  float hix, hiy, hiz, factor;
+};
+
 struct DevScene {
   const SphereRec* sph; const SphereCold* sphc; int ns;
   const AabbRec* aabb; const AabbCold* aabbc; int na;
   const ObbRec* obb; const ObbCold* obbc; int no;
   const float* targets; int T;    // float3[T]
   const uint16_t* dirs; int R;    // half3[R] as 3 x u16
+  const CullRec* cull;            // [ns + na + no]
 };
 
 // Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
@@ -87,7 +97,7 @@ struct DevCounts { unsigned long long v[9]; };
 // --- launchers (art_kernels.hip) ---
 void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, const art_obb* obb, int no,
                  SphereRec* osph, SphereCold* osphc, AabbRec* oaabb, AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc,
-                 hipStream_t st);
+                 CullRec* cull, hipStream_t st);
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, uint32_t* muffle_acc, DevCounts* counts, hipStream_t st);
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,

@@ -29,11 +29,35 @@ namespace art {
 // computes it per access (Center - Size, Radius * Radius, halfQuaternion decode, inverse), so
 // hoisting is bit-identical.
 // ------------------------------------------------------------------------------------------
+// Broad-phase margins relative to the problem's scale (broad phase): the exact tests'
+// rounding can report a blocking hit at most ~3 eps (boxes) or ~sqrt(20 eps) (sphere discriminant
+// cancellation) times the scale away from the true shape; the factors below exceed those bounds
+// by 10x or more.
+#ifndef ART_CULL_MARGIN_SCALE
+#define ART_CULL_MARGIN_SCALE 1.0f  // test hook: 0 disables the margins (tests/test_broadphase_gpu.py must fail)
+#endif
+constexpr float kCullBox = 1e-4f * ART_CULL_MARGIN_SCALE;
+constexpr float kCullSphere = 4e-3f * ART_CULL_MARGIN_SCALE;
+constexpr float kCullObb = 1e-3f * ART_CULL_MARGIN_SCALE;
+
+__device__ __forceinline__ CullRec make_cull(float lx, float ly, float lz, float hx, float hy, float hz, float scale,
+                                             float factor) {
+  CullRec c;
+  const bool fin = isfinite(lx) && isfinite(ly) && isfinite(lz) && isfinite(hx) && isfinite(hy) && isfinite(hz) &&
+                   isfinite(scale);
+  c.lox = fin ? lx : -INFINITY; c.loy = fin ? ly : -INFINITY; c.loz = fin ? lz : -INFINITY;
+  c.hix = fin ? hx : INFINITY; c.hiy = fin ? hy : INFINITY; c.hiz = fin ? hz : INFINITY;
+  c.scale = fin ? scale : 0.0f;
+  c.factor = factor;
+  return c;
+}
+
 __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const art_aabb* __restrict__ aabb, int na,
                             const art_obb* __restrict__ obb, int no, SphereRec* __restrict__ osph,
                             SphereCold* __restrict__ osphc, AabbRec* __restrict__ oaabb, AabbCold* __restrict__ oaabbc,
-                            ObbRec* __restrict__ oobb, ObbCold* __restrict__ oobbc) {
+                            ObbRec* __restrict__ oobb, ObbCold* __restrict__ oobbc, CullRec* __restrict__ cull) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int gi = i;  // global collider order (spheres, AABBs, OBBs) of the broad-phase bounds
   if (i < ns) {
     art_sphere s = sph[i];
     SphereRec r;
@@ -49,6 +73,9 @@ __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const ar
     c.pad = 0.0f;
     osph[i] = r;
     osphc[i] = c;
+    const float ra = fabsf(rad);
+    cull[gi] = make_cull(r.cx - ra, r.cy - ra, r.cz - ra, r.cx + ra, r.cy + ra, r.cz + ra,
+                         fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + ra, kCullSphere);
     return;
   }
   i -= ns;
@@ -68,6 +95,9 @@ __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const ar
     r.pad = 0.0f;
     oaabb[i] = r;
     oaabbc[i] = c;
+    cull[gi] = make_cull(fminf(r.mnx, r.mxx), fminf(r.mny, r.mxy), fminf(r.mnz, r.mxz), fmaxf(r.mnx, r.mxx),
+                         fmaxf(r.mny, r.mxy), fmaxf(r.mnz, r.mxz),
+                         fabsf(c.cx) + fabsf(c.cy) + fabsf(c.cz) + fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz), kCullBox);
     return;
   }
   i -= na;
@@ -91,6 +121,11 @@ __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const ar
     c.pad0 = c.pad1 = 0.0f;
     oobb[i] = r;
     oobbc[i] = c;
+    // bounding sphere of the box (|h|_1 >= |h|_2), whatever the rotation
+    const float rho = (fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz)) * 1.001f;
+    const bool qok = isfinite(q.x) && isfinite(q.y) && isfinite(q.z) && isfinite(q.w);
+    cull[gi] = make_cull(r.cx - rho, r.cy - rho, r.cz - rho, r.cx + rho, r.cy + rho, r.cz + rho,
+                         qok ? fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + rho : INFINITY, kCullObb);
   }
 }
 
@@ -461,11 +496,11 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
 // ------------------------------------------------------------------------------------------
 void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, const art_obb* obb, int no,
                  SphereRec* osph, SphereCold* osphc, AabbRec* oaabb, AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc,
-                 hipStream_t st) {
+                 CullRec* cull, hipStream_t st) {
   int n = ns + na + no;
   if (n == 0) return;
   hipLaunchKernelGGL(prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sph, ns, aabb, na, obb, no, osph, osphc, oaabb,
-                     oaabbc, oobb, oobbc);
+                     oaabbc, oobb, oobbc, cull);
 }
 
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,

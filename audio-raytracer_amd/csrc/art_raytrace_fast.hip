@@ -104,6 +104,9 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
 // colliders, so the cyclic chunk order gives the reference's verdict, and a wave only keeps
 // sweeping for lanes that are still unblocked.
 // ------------------------------------------------------------------------------------------
+#ifndef ART_FAST_CULL
+#define ART_FAST_CULL 1  // broad-phase visibility (exact; see visibility_culled)
+#endif
 #ifndef ART_FAST_STAGED
 #define ART_FAST_STAGED 0  // 1: visibility records staged through LDS (measured slower: lower occupancy, barrier waits)
 #endif
@@ -400,6 +403,193 @@ __device__ __forceinline__ void visibility_staged(const DevScene& sc, const Pair
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Broad-phase visibility (SURVEY.md §8 f rank 4): results identical to the brute-force sweep.
+// A wave takes a batch of 64 consecutive pairs of the block's queue (same query, direction-
+// coherent rays), reduces the bounding box of their segments [o, o + maxd d] once, and sweeps the
+// collider chunks in order: per chunk the lanes load the 64 colliders' broad-phase bounds
+// (coalesced vector loads) and ballot the candidates whose bounds, widened by the rounding margin
+// of the exact tests, overlap the box; only candidates get the exact wave-uniform test. A
+// collider that is not a candidate cannot block any lane's segment (broad phase),
+// so every pair's verdict equals the brute-force OR. Test counts reported by the metric stay the
+// reference algorithm's (brute-force-equivalent, SURVEY.md §8 d).
+// ------------------------------------------------------------------------------------------
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_mov(float v, float ident) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+// Wave-wide IEEE min / max (NaN lanes ignored), result wave-uniform. row_shr 1,2,4,8 within each
+// row of 16, then row_bcast 15 / 31 fold the rows into lane 63.
+__device__ __forceinline__ float wave_min(float v) {
+  v = fminf(v, dpp_mov<0x111, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x112, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x114, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x118, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x142, 0xa>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x143, 0xc>(v, INFINITY));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp_mov<0x111, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x112, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x114, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x118, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x142, 0xa>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x143, 0xc>(v, -INFINITY));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+struct WaveBox {
+  float lx, ly, lz, hx, hy, hz, om;
+};
+
+// Candidate colliders of a window of up to kCullW chunks of one type: bit i of m[j] = collider
+// b + 64 j + i. Exact tests run U at a time while at least U candidates remain, then one by one.
+#ifndef ART_CULL_U
+#define ART_CULL_U 4
+#endif
+constexpr int kCullW = 1;  // chunks per candidate set (wider windows spill the masks)
+constexpr int kCullU = ART_CULL_U;  // candidate tests per scalar-load group
+
+struct CandSet {
+  unsigned long long m[kCullW];
+  int left;
+  __device__ __forceinline__ int pop() {  // next candidate offset from b (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < kCullW; ++j)
+      if (m[j]) {
+        const int k = j * 64 + (int)__builtin_ctzll(m[j]);
+        m[j] &= m[j] - 1;
+        --left;
+        return k;
+      }
+    return 0;
+  }
+};
+
+template <int U, typename Rec, typename Test>
+__device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet& cs, bool blocked, bool done, Test test) {
+  while (cs.left >= U) {
+    int idx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) idx[u] = b + cs.pop();
+    Rec r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = ldc(recs, wave_uniform(idx[u]));
+#pragma unroll
+    for (int u = 0; u < U; ++u) blocked |= test(r[u]);
+    if (__all(blocked || done)) return blocked;
+  }
+  while (cs.left > 0) {
+    const Rec r = ldc(recs, wave_uniform(b + cs.pop()));
+    blocked |= test(r);
+  }
+  return blocked;
+}
+
+#ifdef ART_DIAG_CULL_STATS
+__device__ unsigned g_diag[8];
+#endif
+
+template <int U>
+__device__ __forceinline__ void visibility_culled(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
+                                                  int np, int lane) {
+  const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
+  const int nchunks = cm.total();
+  for (;;) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(s_head, 64);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+    if (base >= np) break;
+    const int p = base + lane;
+    const bool valid = p < np;
+    Seg s;
+    float maxd = 0.0f;
+    int owner = kNoOwner;
+    WaveBox wb;
+    {
+      PairSeg g = s_seg[valid ? p : base];
+      s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
+      s.a2 = g.a2; s.a4 = 2.0f * g.a2;
+      maxd = g.maxd; owner = g.owner;
+      const vec3 e = s.o + s.d * maxd;
+      const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+      wb.lx = wave_min(valid ? fminf(s.o.x, e.x) : INFINITY);
+      wb.ly = wave_min(valid ? fminf(s.o.y, e.y) : INFINITY);
+      wb.lz = wave_min(valid ? fminf(s.o.z, e.z) : INFINITY);
+      wb.hx = wave_max(valid ? fmaxf(s.o.x, e.x) : -INFINITY);
+      wb.hy = wave_max(valid ? fmaxf(s.o.y, e.y) : -INFINITY);
+      wb.hz = wave_max(valid ? fmaxf(s.o.z, e.z) : -INFINITY);
+      wb.om = wave_max(valid ? om : 0.0f);
+    }
+    bool blocked = false;
+    const bool done = !valid;
+#ifdef ART_DIAG_CULL_STATS
+    {
+      const unsigned nv = (unsigned)__popcll(__ballot(valid));
+      if (lane == 0) { atomicAdd(&g_diag[0], 1u); atomicAdd(&g_diag[3], nv); }
+    }
+#endif
+    // chunk geometry: type, first index within the type, valid count, global index of the bounds
+    auto chunk_at = [&](int c, int& type, int& b, int& n) {
+      if (c < cm.cs) { type = 0; b = c * kChunk; n = min(kChunk, sc.ns - b); return b; }
+      if (c - cm.cs < cm.ca) { type = 1; b = (c - cm.cs) * kChunk; n = min(kChunk, sc.na - b); return sc.ns + b; }
+      type = 2; b = (c - cm.cs - cm.ca) * kChunk; n = min(kChunk, sc.no - b);
+      return sc.ns + sc.na + b;
+    };
+    // software pipeline: the bounds of chunk c + 1 are loaded while chunk c's candidates are tested
+    CullRec nxt;
+    {
+      int t0, b0, n0;
+      const int g0 = chunk_at(0, t0, b0, n0);
+      nxt = sc.cull[g0 + min(lane, n0 - 1)];
+    }
+    for (int c = 0; c < nchunks; ++c) {
+      int type, b, n;
+      chunk_at(c, type, b, n);
+      const CullRec cr = nxt;
+      if (c + 1 < nchunks) {
+        int t1, b1, n1;
+        const int g1 = chunk_at(c + 1, t1, b1, n1);
+        nxt = sc.cull[g1 + min(lane, n1 - 1)];
+      }
+      const float m = cr.factor * (cr.scale + wb.om);
+      const bool cand = (lane < n) & (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) &
+                        (cr.hiy + m >= wb.ly) & (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
+      CandSet cs;
+      cs.m[0] = __ballot(cand);
+      cs.left = __popcll(cs.m[0]);
+#ifdef ART_DIAG_CULL_STATS
+      if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
+#endif
+#ifdef ART_DIAG_CULL_ONLY  // diagnostic build only: broad phase without the exact tests
+      blocked |= (cs.left == -1);
+      continue;
+#endif
+      if (cs.left == 0) continue;
+      if (type == 0) {
+        blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
+          float d;
+          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
+        });
+      } else if (type == 1) {
+        blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
+          float d;
+          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+        });
+      } else {
+        blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
+          float d;
+          return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+        });
+      }
+      if (__all(blocked || done)) break;
+    }
+    if (valid) s_res[p] = blocked ? 1 : 0;
+  }
+}
+
 __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
   return type == kSphere ? sc.sphc[idx].echo : (type == kAabb ? sc.aabbc[idx].echo : sc.obbc[idx].echo);
 }
@@ -570,6 +760,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     __syncthreads();
 #ifdef ART_DIAG_NO_VISIBILITY  // diagnostic build only: time the nearest-hit phase alone
     for (int p = w * 64 + lane; p < s_np; p += K * 64) s_res[p] = 0;
+#elif ART_FAST_CULL
+    visibility_culled<U>(sc, s_seg, s_res, &s_head, s_np, lane);
 #elif ART_FAST_STAGED
     visibility_staged<U>(sc, s_seg, s_res, &s_head, s_go, s_stage, s_np, w, K, lane);
 #else
@@ -651,6 +843,10 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   if (threadIdx.x == 0 && atomicAdd(&work[1], 1u) == gridDim.x - 1) {
     atomicExch(&work[0], 0u);
     atomicExch(&work[1], 0u);
+#ifdef ART_DIAG_CULL_STATS
+    printf("[cull] batches %u pairs %u chunks %u candidates %u\n", atomicExch(&g_diag[0], 0u), atomicExch(&g_diag[3], 0u),
+           atomicExch(&g_diag[1], 0u), atomicExch(&g_diag[2], 0u));
+#endif
   }
 }
 

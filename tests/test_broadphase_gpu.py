@@ -1,0 +1,184 @@
+"""GPU parity of the broad phase on adversarial scenes.
+
+The throughput kernel culls colliders per wave with a bounding box of the wave's segments widened
+by a rounding margin (broad phase). A wrong margin can only show up where the
+reference's float tests report hits that the true geometry does not have: grazing rays on tiny
+or far spheres, rays in the plane of a box face, huge coordinates, degenerate and non-finite
+colliders. Every scene here is compared bit for bit with the brute-force oracle, through the
+block kernel, the wavefront pipeline and the reference-order kernel (gpu_vs_oracle).
+"""
+import numpy as np
+import pytest
+
+import art
+from art import abi
+from art.synth import fibonacci_directions
+from test_parity_gpu import gpu_vs_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def f16bits(x) -> np.ndarray:
+    return np.asarray(x, np.float32).astype(np.float16).view(np.uint16)
+
+
+def spheres(centers, radii, rng, tid=None):
+    n = len(radii)
+    s = np.zeros(n, abi.SPHERE)
+    s["center"] = f16bits(centers).reshape(n, 3)
+    s["radius"] = f16bits(radii)
+    s["material"] = f16bits(rng.uniform(0.0, 1.0, (n, 3)))
+    s["audio_target_id"] = -1 if tid is None else tid
+    return s
+
+
+def aabbs(centers, halves, rng, tid=None):
+    n = len(centers)
+    a = np.zeros(n, abi.AABB)
+    a["center"] = f16bits(centers).reshape(n, 3)
+    a["size"] = f16bits(halves).reshape(n, 3)
+    a["material"] = f16bits(rng.uniform(0.0, 1.0, (n, 3)))
+    a["audio_target_id"] = -1 if tid is None else tid
+    return a
+
+
+def obbs(centers, halves, rng):
+    n = len(centers)
+    b = np.zeros(n, abi.OBB)
+    b["center"] = f16bits(centers).reshape(n, 3)
+    b["size"] = f16bits(halves).reshape(n, 3)
+    q = rng.normal(size=(n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    q[q[:, 3] < 0] *= -1
+    b["rot"] = f16bits(q[:, :3])
+    b["material"] = f16bits(rng.uniform(0.0, 1.0, (n, 3)))
+    b["audio_target_id"] = -1
+    return b
+
+
+def fib_dirs(R):
+    return fibonacci_directions(R)
+
+
+def run(ctx, scene, org, H=2, T_owned=False):
+    params = art.FrameParams(max_hits_per_ray=H, max_ray_life=1e4, max_muffle_hit_distance=1e5,
+                             stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
+    out, counts = gpu_vs_oracle(ctx, scene, params, org, counts=False)
+    return out
+
+
+def test_grazing_tiny_far_spheres(ctx):
+    """Spheres of radius 2^-10..2^-4 placed tangent to (or a hair off) the rays, far away: the
+    discriminant cancels, so the float test reports hits the geometry does not have."""
+    rng = np.random.default_rng(11)
+    R = 128
+    dirs_bits = fib_dirs(R)
+    d = dirs_bits.view(np.float16).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    n = 1500
+    k = rng.integers(0, R, n)
+    dist = rng.uniform(50.0, 900.0, n).astype(np.float32)
+    r = (2.0 ** rng.uniform(-10, -4, n)).astype(np.float32)
+    perp = rng.normal(size=(n, 3)).astype(np.float32)
+    perp -= (perp * d[k]).sum(1, keepdims=True) * d[k]
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True)
+    offset = r * rng.choice([0.999, 1.0, 1.001, 0.9, 1.1], n).astype(np.float32)
+    centers = d[k] * dist[:, None] + perp * offset[:, None]
+    targets = (rng.normal(size=(4, 3)) * 300).astype(np.float32)
+    # a few big walls so that rays hit and spawn echo / muffle segments past the tiny spheres
+    walls = aabbs(rng.uniform(-1000, 1000, (64, 3)), rng.uniform(20, 120, (64, 3)), rng)
+    scene = art.Scene(dirs=dirs_bits, targets=targets, spheres=spheres(centers, r, rng), aabbs=walls)
+    org = np.zeros((6, 3), np.float32)
+    org[1:] = rng.uniform(-5, 5, (5, 3))
+    out = run(ctx, scene, org)
+    assert (out.echo != 0).any()
+
+
+def test_huge_coordinates(ctx):
+    """Coordinates near the half range (|x| up to 3e4) and long segments."""
+    rng = np.random.default_rng(12)
+    R = 96
+    n = 800
+    centers = rng.uniform(-30000, 30000, (n, 3)).astype(np.float32)
+    scene = art.Scene(dirs=fib_dirs(R), targets=rng.uniform(-30000, 30000, (3, 3)).astype(np.float32),
+                      spheres=spheres(centers[:400], rng.uniform(100, 4000, 400), rng),
+                      aabbs=aabbs(centers[400:], rng.uniform(50, 3000, (400, 3)), rng))
+    org = rng.uniform(-20000, 20000, (8, 3)).astype(np.float32)
+    run(ctx, scene, org, H=3)
+
+
+def test_axis_aligned_face_planes(ctx):
+    """Rays along the axes (zero direction components, infinite 1/d) from origins lying exactly in
+    box face planes, and boxes with zero or negative half-extents."""
+    rng = np.random.default_rng(13)
+    axes = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1],
+                     [1, 1, 0], [0, 1, -1], [1, 0, 1]], np.float32)
+    dirs = f16bits(axes / np.linalg.norm(axes, axis=1, keepdims=True)).reshape(-1, 3)
+    n = 600
+    c = rng.integers(-20, 20, (n, 3)).astype(np.float32)
+    hlf = rng.integers(0, 4, (n, 3)).astype(np.float32)
+    hlf[rng.random((n, 3)) < 0.1] *= -1  # negative half-extents swap the slab bounds
+    org = np.array([[0, 0, 0], [1, 1, 1], [2, 0, -3], [0.5, 0, 0]], np.float32)
+    c[:8] = org[0] + np.array([1, 0, 0])  # faces exactly through the origin's planes
+    hlf[:8] = 1
+    scene = art.Scene(dirs=dirs, targets=np.array([[3, 3, 3], [-7, 2, 0]], np.float32),
+                      aabbs=aabbs(c, hlf, rng), spheres=spheres(c[:50] + 0.5, np.full(50, 0.5), rng))
+    run(ctx, scene, org, H=4)
+
+
+def test_nonfinite_and_degenerate_colliders(ctx):
+    """Colliders carrying NaN / inf half values, zero radius and zero size mixed into a normal scene."""
+    rng = np.random.default_rng(14)
+    cfg = art.CONFIGS[5]
+    scene, org, params = art.synth(cfg, S=4, R=64, C_scale=0.1)
+    sp, ab, ob = scene.spheres.copy(), scene.aabbs.copy(), scene.obbs.copy()
+    nan, inf, ninf = np.uint16(0x7E00), np.uint16(0x7C00), np.uint16(0xFC00)
+    sp["radius"][:3] = [nan, inf, 0]
+    sp["center"][3] = [inf, 0, 0]
+    ab["size"][:3] = [[nan, 1, 1], [inf, inf, inf], [0, 0, 0]]
+    ab["center"][3] = [ninf, 0, 0]
+    ob["rot"][:2] = [[nan, 0, 0], [0x3C00, 0x3C00, 0x3C00]]
+    ob["size"][2] = [inf, 1, 1]
+    scene = art.Scene(dirs=scene.dirs, targets=scene.targets, spheres=sp, aabbs=ab, obbs=ob)
+    run(ctx, scene, org, H=3)
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_dense_random_scenes(ctx, seed):
+    """Random mixed scenes with targets inside colliders and origins inside boxes."""
+    rng = np.random.default_rng(seed)
+    R = 128
+    n = 1200
+    c = rng.uniform(-40, 40, (n, 3)).astype(np.float32)
+    scene = art.Scene(dirs=fib_dirs(R), targets=np.concatenate([c[:2], rng.uniform(-40, 40, (2, 3))]).astype(np.float32),
+                      spheres=spheres(c[:500], rng.uniform(0.05, 3, 500), rng, tid=rng.integers(-1, 4, 500)),
+                      aabbs=aabbs(c[500:1000], rng.uniform(0.05, 3, (500, 3)), rng, tid=rng.integers(-1, 4, 500)),
+                      obbs=obbs(c[1000:], rng.uniform(0.05, 3, (200, 3)), rng))
+    org = np.concatenate([c[500:503], rng.uniform(-40, 40, (5, 3))]).astype(np.float32)
+    run(ctx, scene, org, H=3)
+
+
+def test_razor_thin_segments_tiny_spheres(ctx):
+    """The case the margin exists for. Every ray of a fan points along -x, so each wave's segments
+    (echo back to the origin, muffle rays to targets on the x axis) form a box only ~1e-2 thick in
+    y. Tiny spheres (r = 2^-7) sit just above that box: their exact bounds do not overlap it, but
+    the reference's float discriminant (b^2 - 4ac cancels at |oc| ~ 100) still reports many of
+    them as blocking (a float32 restatement finds blocks up to 0.03 off the sphere). A cull
+    without the rounding margin misses those blocks; this scene then differs from the oracle."""
+    rng = np.random.default_rng(31)
+    R = 64
+    dirs = np.tile(np.array([[0xBC00, 0, 0]], np.uint16), (R, 1))  # (-1, 0, 0) exactly
+    deltas = np.array([1e-6, 1e-5, 1e-4, 1e-3, 4e-3, 1e-2, 2e-2, 3e-2], np.float32)
+    org = np.stack([np.zeros(8), -deltas, np.zeros(8)], 1).astype(np.float32)
+    targets = np.array([[100, -1e-5, 0], [100, -3e-3, 0], [100, -1.5e-2, 0], [60, -2.5e-2, 0]], np.float32)
+    r = 2.0 ** -7
+    cx = np.arange(-95, 96, 1.0, dtype=np.float32)
+    centers = np.stack([cx, np.full_like(cx, r), np.zeros_like(cx)], 1)
+    sp = spheres(centers, np.full(cx.size, r, np.float32), rng)
+    wall = aabbs(np.array([[-101, 0, 0]], np.float32), np.array([[1, 50, 50]], np.float32), rng)
+    scene = art.Scene(dirs=dirs, targets=targets, spheres=sp, aabbs=wall)
+    params = art.FrameParams(max_hits_per_ray=1, max_ray_life=1e4, max_muffle_hit_distance=1e5,
+                             stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
+    out, _ = gpu_vs_oracle(ctx, scene, params, org, counts=False)
+    # the scene must contain both verdicts: some muffle rays blocked by a sphere, some clear
+    assert (out.muffle != 0).any() and (out.muffle != R).any()
