@@ -19,6 +19,10 @@
 
 namespace art {
 
+#ifdef ART_DIAG_CULL_STATS
+__device__ unsigned g_diag[8];  // diagnostic build only: broad-phase statistics, printed per launch
+#endif
+
 constexpr int kNoHit = 0x7fffffff;
 
 __device__ __forceinline__ void chunk_of(int n, int w, int K, int& b, int& e) {
@@ -91,6 +95,166 @@ __device__ __forceinline__ void nearest_chunk(const DevScene& sc, const Seg& s, 
     const ObbRec r = ldc(sc.obb, wave_uniform(i));
     float d;
     if (obb_test<false>(s, r, stored_q(r), d) && d < best) { best = d; code = (2 << 28) | i; }
+  }
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_mov(float v, float ident) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+// Wave-wide IEEE min / max (NaN lanes ignored), result wave-uniform. row_shr 1,2,4,8 within each
+// row of 16, then row_bcast 15 / 31 fold the rows into lane 63.
+__device__ __forceinline__ float wave_min(float v) {
+  v = fminf(v, dpp_mov<0x111, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x112, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x114, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x118, 0xf>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x142, 0xa>(v, INFINITY));
+  v = fminf(v, dpp_mov<0x143, 0xc>(v, INFINITY));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp_mov<0x111, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x112, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x114, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x118, 0xf>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x142, 0xa>(v, -INFINITY));
+  v = fmaxf(v, dpp_mov<0x143, 0xc>(v, -INFINITY));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// Candidate colliders of a window of up to kCullW chunks of one type: bit i of m[j] = collider
+// b + 64 j + i. Exact tests run U at a time while at least U candidates remain, then one by one.
+#ifndef ART_CULL_U
+#define ART_CULL_U 4
+#endif
+constexpr int kCullW = 1;  // chunks per candidate set (wider windows spill the masks)
+constexpr int kCullU = ART_CULL_U;  // candidate tests per scalar-load group
+
+struct CandSet {
+  unsigned long long m[kCullW];
+  int left;
+  __device__ __forceinline__ int pop() {  // next candidate offset from b (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < kCullW; ++j)
+      if (m[j]) {
+        const int k = j * 64 + (int)__builtin_ctzll(m[j]);
+        m[j] &= m[j] - 1;
+        --left;
+        return k;
+      }
+    return 0;
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// Broad-phase nearest hit for rays that share their origin O (the first segment of every ray of a
+// fan). The wave's directions lie in a cone (axis a, half-angle theta); a collider can be hit by
+// one of them only if its bounding sphere, widened by the rounding margin of the exact tests
+// (CullRec), meets the cone. Candidates are tested in increasing index order with
+// the same strict `<`, so the wave's first minimum over its range is unchanged.
+// ------------------------------------------------------------------------------------------
+struct WaveCone {
+  float ox, oy, oz, om;   // shared origin, |O|_1
+  float ax, ay, az;       // unit axis
+  float cos_t, sin_t;     // half-angle (with slack); cos_t <= 0: no culling
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__device__ __forceinline__ WaveCone make_cone(vec3 O, vec3 d, bool alive) {
+  WaveCone wc;
+  wc.ox = O.x; wc.oy = O.y; wc.oz = O.z;
+  wc.om = fabsf(O.x) + fabsf(O.y) + fabsf(O.z);
+  const float n2 = d.x * d.x + d.y * d.y + d.z * d.z;
+  const bool ok = alive && n2 > 0.0f && isfinite(n2);
+  const float inv = ok ? 1.0f / sqrtf(n2) : 0.0f;
+  const float dx = d.x * inv, dy = d.y * inv, dz = d.z * inv;
+  float sx = wave_sum(dx), sy = wave_sum(dy), sz = wave_sum(dz);
+  const float sn = sqrtf(sx * sx + sy * sy + sz * sz);
+  // a wave with a degenerate (non-finite or zero) direction is not culled
+  const bool bad = __any(alive && !ok);
+  if (!(sn > 0.0f) || bad) {
+    wc.ax = 1.0f; wc.ay = 0.0f; wc.az = 0.0f; wc.cos_t = -1.0f; wc.sin_t = 0.0f;
+    return wc;
+  }
+  wc.ax = sx / sn; wc.ay = sy / sn; wc.az = sz / sn;
+  float c = wave_min(ok ? dx * wc.ax + dy * wc.ay + dz * wc.az : INFINITY);
+  c = fminf(c, 1.0f);
+  // slack of 2e-3 rad for the rounding of the normalisations and dot products
+  const float s0 = sqrtf(fmaxf(0.0f, 1.0f - c * c));
+  constexpr float ce = 0.999998f, se = 0.002f;  // cos / sin of the slack angle
+  wc.cos_t = c * ce - s0 * se;
+  wc.sin_t = s0 * ce + c * se;
+  return wc;
+}
+
+// Candidate test of collider bounds against the cone (lane = collider).
+__device__ __forceinline__ bool cone_candidate(const WaveCone& wc, const CullRec& cr) {
+  if (!(wc.cos_t > 0.0f)) return true;
+  const float cx = 0.5f * (cr.lox + cr.hix), cy = 0.5f * (cr.loy + cr.hiy), cz = 0.5f * (cr.loz + cr.hiz);
+  // bounding-sphere radius of the bounds box (|half diagonal|_1 >= |half diagonal|_2), widened
+  const float rho = 0.5f * ((cr.hix - cr.lox) + (cr.hiy - cr.loy) + (cr.hiz - cr.loz)) * 1.001f +
+                    cr.factor * (cr.scale + wc.om);
+  const float vx = cx - wc.ox, vy = cy - wc.oy, vz = cz - wc.oz;
+  const float L2 = vx * vx + vy * vy + vz * vz;
+  if (!(L2 > rho * rho * 1.0001f)) return true;  // origin inside / near the bound (or non-finite)
+  const float L = sqrtf(L2);
+  const float sb = fminf(1.0f, rho / L * 1.0001f);
+  const float cb = sqrtf(fmaxf(0.0f, 1.0f - sb * sb));
+  const float cos_lim = wc.cos_t * cb - wc.sin_t * sb;  // cos(theta + beta), theta + beta < pi
+  // slack (1e-4 L) only ever admits more colliders: cos_lim <= 1 and the threshold is lowered
+  return vx * wc.ax + vy * wc.ay + vz * wc.az >= (cos_lim - 1e-4f) * L;
+}
+
+template <int U>
+__device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, const WaveCone& wc, int w, int K,
+                                             int lane, float& best, int& code) {
+  best = FLT_MAX;
+  code = kNoHit;
+  for (int type = 0; type < 3; ++type) {
+    const int n = type == 0 ? sc.ns : (type == 1 ? sc.na : sc.no);
+    const int gofs = type == 0 ? 0 : (type == 1 ? sc.ns : sc.ns + sc.na);
+    int b, e;
+    chunk_of(n, w, K, b, e);
+    for (int cb = b; cb < e; cb += 64) {
+      const int k = cb + lane;
+      bool cand = false;
+      if (k < e) cand = cone_candidate(wc, sc.cull[gofs + k]);
+      CandSet cs;
+      cs.m[0] = __ballot(cand);
+      cs.left = __popcll(cs.m[0]);
+#ifdef ART_DIAG_CULL_STATS
+      if (lane == 0) { atomicAdd(&g_diag[4], (unsigned)min(64, e - cb)); atomicAdd(&g_diag[5], (unsigned)cs.left); }
+#endif
+      if (type == 0) {
+        while (cs.left > 0) {
+          const int i = cb + cs.pop();
+          const SphereRec c = ldc(sc.sph, wave_uniform(i));
+          float d;
+          if (sphere_hit_dist(s, c, d) && d < best) { best = d; code = i; }
+        }
+      } else if (type == 1) {
+        while (cs.left > 0) {
+          const int i = cb + cs.pop();
+          const AabbRec r = ldc(sc.aabb, wave_uniform(i));
+          float d;
+          if (aabb_test<false>(s, r, d) && d < best) { best = d; code = (1 << 28) | i; }
+        }
+      } else {
+        while (cs.left > 0) {
+          const int i = cb + cs.pop();
+          const ObbRec r = ldc(sc.obb, wave_uniform(i));
+          float d;
+          if (obb_test<false>(s, r, stored_q(r), d) && d < best) { best = d; code = (2 << 28) | i; }
+        }
+      }
+    }
   }
 }
 
@@ -414,58 +578,8 @@ __device__ __forceinline__ void visibility_staged(const DevScene& sc, const Pair
 // so every pair's verdict equals the brute-force OR. Test counts reported by the metric stay the
 // reference algorithm's (brute-force-equivalent, SURVEY.md §8 d).
 // ------------------------------------------------------------------------------------------
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ float dpp_mov(float v, float ident) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
-}
-
-// Wave-wide IEEE min / max (NaN lanes ignored), result wave-uniform. row_shr 1,2,4,8 within each
-// row of 16, then row_bcast 15 / 31 fold the rows into lane 63.
-__device__ __forceinline__ float wave_min(float v) {
-  v = fminf(v, dpp_mov<0x111, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x112, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x114, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x118, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x142, 0xa>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x143, 0xc>(v, INFINITY));
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ float wave_max(float v) {
-  v = fmaxf(v, dpp_mov<0x111, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x112, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x114, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x118, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x142, 0xa>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x143, 0xc>(v, -INFINITY));
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-
 struct WaveBox {
   float lx, ly, lz, hx, hy, hz, om;
-};
-
-// Candidate colliders of a window of up to kCullW chunks of one type: bit i of m[j] = collider
-// b + 64 j + i. Exact tests run U at a time while at least U candidates remain, then one by one.
-#ifndef ART_CULL_U
-#define ART_CULL_U 4
-#endif
-constexpr int kCullW = 1;  // chunks per candidate set (wider windows spill the masks)
-constexpr int kCullU = ART_CULL_U;  // candidate tests per scalar-load group
-
-struct CandSet {
-  unsigned long long m[kCullW];
-  int left;
-  __device__ __forceinline__ int pop() {  // next candidate offset from b (wave-uniform)
-#pragma unroll
-    for (int j = 0; j < kCullW; ++j)
-      if (m[j]) {
-        const int k = j * 64 + (int)__builtin_ctzll(m[j]);
-        m[j] &= m[j] - 1;
-        --left;
-        return k;
-      }
-    return 0;
-  }
 };
 
 template <int U, typename Rec, typename Test>
@@ -487,10 +601,6 @@ __device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet&
   }
   return blocked;
 }
-
-#ifdef ART_DIAG_CULL_STATS
-__device__ unsigned g_diag[8];
-#endif
 
 template <int U>
 __device__ __forceinline__ void visibility_culled(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
@@ -683,11 +793,21 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   int hits = 0;
   bool alive = valid;
 
+  int bounce = 0;  // wave-uniform (lanes that stopped keep their own `hits`)
   while (__any(alive)) {  // identical in every wave of the block -> uniform barriers
     const Seg s = make_seg(o, d);
     float best;
     int code;
+#if ART_FAST_CULL
+    if (bounce == 0) {  // first segment: every ray of the fan starts at O
+      const WaveCone wc = make_cone(O, d, alive);
+      nearest_cone<U>(sc, s, wc, w, K, lane, best, code);
+    } else {
+      nearest_chunk<U>(sc, s, w, K, best, code);
+    }
+#else
     nearest_chunk<U>(sc, s, w, K, best, code);
+#endif
     s_dist[w][lane] = best;
     s_code[w][lane] = code;
     __syncthreads();
@@ -822,6 +942,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
         if (life < 0.0f) alive = false;
       }
     }
+    ++bounce;
   }
   if (valid && w == 0) {
     if (single_slot) {  // slots past the last hit keep the reset value 0 (:72-80)
@@ -844,8 +965,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     atomicExch(&work[0], 0u);
     atomicExch(&work[1], 0u);
 #ifdef ART_DIAG_CULL_STATS
-    printf("[cull] batches %u pairs %u chunks %u candidates %u\n", atomicExch(&g_diag[0], 0u), atomicExch(&g_diag[3], 0u),
-           atomicExch(&g_diag[1], 0u), atomicExch(&g_diag[2], 0u));
+    printf("[cull] batches %u pairs %u chunks %u candidates %u | nearest colliders %u candidates %u\n",
+           atomicExch(&g_diag[0], 0u), atomicExch(&g_diag[3], 0u), atomicExch(&g_diag[1], 0u), atomicExch(&g_diag[2], 0u),
+           atomicExch(&g_diag[4], 0u), atomicExch(&g_diag[5], 0u));
 #endif
   }
 }
