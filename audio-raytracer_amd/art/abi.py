@@ -49,6 +49,7 @@ ART_CTX_COUNT_TESTS = 0x1
 ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_WAVEFRONT = 0x8
+ART_CTX_COUNT_EXECUTED = 0x10
 ART_OUT_HIT_RESULTS = 0x1
 
 ART_OWN_SPHERE, ART_OWN_AABB, ART_OWN_OBB = 0, 1, 2
@@ -103,6 +104,11 @@ class art_kernel_times(C.Structure):
                 ("launches", C.c_int32)]
 
 
+class art_exec_counts(C.Structure):
+    _fields_ = [("sphere", C.c_uint64), ("aabb", C.c_uint64), ("obb", C.c_uint64), ("cull_box", C.c_uint64),
+                ("cull_cone", C.c_uint64), ("launches", C.c_uint64)]
+
+
 class art_synth_config(C.Structure):
     _fields_ = [("sphere_count", C.c_int32), ("aabb_count", C.c_int32), ("obb_count", C.c_int32),
                 ("target_count", C.c_int32), ("fan_count", C.c_int32), ("ray_count", C.c_int32),
@@ -128,6 +134,7 @@ SIGNATURES = {
     "art_launch_device": (I32, [VP, VP, I32, VP, U32, VP]),
     "art_count_device": (I32, [VP, VP, I32, VP, U32, VP, C.POINTER(art_test_counts)]),
     "art_kernel_timing": (I32, [VP, C.POINTER(art_kernel_times)]),
+    "art_executed_counts": (I32, [VP, C.POINTER(art_exec_counts)]),
     "art_device_count": (I32, []),
     # art_synth.h
     "art_synth_scene": (I32, [C.POINTER(art_synth_config), VP, VP, VP, VP, VP, VP]),

@@ -273,6 +273,14 @@ class Context:
         return {"raytrace_ms": t.raytrace_ms, "permeate_ms": t.permeate_ms, "reduce_ms": t.reduce_ms,
                 "launches": t.launches}
 
+    def executed_counts(self) -> dict:
+        """Work the throughput kernel executed since the last call (needs ART_CTX_COUNT_EXECUTED)."""
+        t = abi.art_exec_counts()
+        rc = self.lib.art_executed_counts(self.ptr, C.byref(t))
+        if rc:
+            self._raise(rc)
+        return {k: int(getattr(t, k)) for k, _ in abi.art_exec_counts._fields_}
+
     def close(self):
         if getattr(self, "ptr", None):
             self.lib.art_destroy(self.ptr)

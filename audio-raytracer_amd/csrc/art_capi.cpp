@@ -97,6 +97,8 @@ struct Device {
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
   DevBuf work;  // ticket counters of the persistent raytrace kernel (self-rearming, zeroed once)
+  DevBuf exec;  // executed-work counters (ART_CTX_COUNT_EXECUTED)
+  uint64_t exec_launches = 0;
   DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
   int wf_blocks = 0;
   int fan_begin = 0, fan_count = 0;
@@ -443,7 +445,17 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         if (!dv.work.reserve(256)) return fail(c, ART_E_NOMEM, "device allocation failed");
         HIP_TRY(c, hipMemsetAsync(dv.work.p, 0, 256, st));
       }
-      launch_raytrace_fast(dv.sc, fp, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), st);
+      FrameParams fpx = fp;
+      fpx.exec = nullptr;
+      if (c->flags & ART_CTX_COUNT_EXECUTED) {
+        if (!dv.exec.p) {
+          if (!dv.exec.reserve(64)) return fail(c, ART_E_NOMEM, "device allocation failed");
+          HIP_TRY(c, hipMemsetAsync(dv.exec.p, 0, 64, st));
+        }
+        fpx.exec = static_cast<unsigned long long*>(dv.exec.p);
+        dv.exec_launches++;
+      }
+      launch_raytrace_fast(dv.sc, fpx, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), st);
     } else if (f.T <= 31) {
       int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);
       if (rc) return rc;
@@ -540,7 +552,7 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
-    dv.work.release();
+    dv.work.release(); dv.exec.release();
     dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
@@ -763,6 +775,23 @@ ART_API int art_count_device(art_ctx* c, const float* d_origins, int32_t fan_cou
                              void* stream, art_test_counts* out) {
   if (!out) return ART_E_INVALID;
   return launch_common(c, d_origins, fan_count, d_block, out_flags, stream, true, out);
+}
+
+ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
+  if (!c || !out) return ART_E_INVALID;
+  memset(out, 0, sizeof *out);
+  for (Device& dv : c->devs) {
+    if (!dv.exec.p) continue;
+    HIP_TRY(c, hipSetDevice(dv.id));
+    HIP_TRY(c, hipDeviceSynchronize());
+    unsigned long long v[5] = {0, 0, 0, 0, 0};
+    HIP_TRY(c, hipMemcpy(v, dv.exec.p, sizeof v, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemset(dv.exec.p, 0, 64));
+    out->sphere += v[0]; out->aabb += v[1]; out->obb += v[2]; out->cull_box += v[3]; out->cull_cone += v[4];
+    out->launches += dv.exec_launches;
+    dv.exec_launches = 0;
+  }
+  return ART_OK;
 }
 
 ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {

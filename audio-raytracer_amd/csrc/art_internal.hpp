@@ -89,7 +89,11 @@ struct FrameParams {
   const float* vol_curve; int vol_n; float vol_len;
   const float* muf_curve; int muf_n; float muf_len;
   int sample_rate;
+  unsigned long long* exec;  // executed-work counters (ExecSlot order) or nullptr
 };
+
+// Slots of FrameParams::exec (art_exec_counts order).
+enum ExecSlot { kExecSphere = 0, kExecAabb = 1, kExecObb = 2, kExecCullBox = 3, kExecCullCone = 4 };
 
 // Device counters for the counting variant, in art_test_counts order.
 struct DevCounts { unsigned long long v[9]; };

@@ -132,6 +132,12 @@ __device__ __forceinline__ float wave_max(float v) {
 constexpr int kCullW = 1;  // chunks per candidate set (wider windows spill the masks)
 constexpr int kCullU = ART_CULL_U;  // candidate tests per scalar-load group
 
+// Executed-work accounting (ART_CTX_COUNT_EXECUTED): one atomic per call from lane 0, off when
+// `ex` is null (a uniform branch).
+__device__ __forceinline__ void exec_add(unsigned long long* ex, int slot, unsigned long long v) {
+  if (ex && v && (threadIdx.x & 63) == 0) atomicAdd(ex + slot, v);
+}
+
 struct CandSet {
   unsigned long long m[kCullW];
   int left;
@@ -212,11 +218,21 @@ __device__ __forceinline__ bool cone_candidate(const WaveCone& wc, const CullRec
   return vx * wc.ax + vy * wc.ay + vz * wc.az >= (cos_lim - 1e-4f) * L;
 }
 
+// brute-force nearest sweep of this wave's ranges (nearest_chunk): every collider of the range
+__device__ __forceinline__ void exec_brute(const DevScene& sc, int w, int K, unsigned long long* ex) {
+  if (!ex) return;
+  int b, e;
+  chunk_of(sc.ns, w, K, b, e); exec_add(ex, kExecSphere, 64ull * (e - b));
+  chunk_of(sc.na, w, K, b, e); exec_add(ex, kExecAabb, 64ull * (e - b));
+  chunk_of(sc.no, w, K, b, e); exec_add(ex, kExecObb, 64ull * (e - b));
+}
+
 template <int U>
 __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, const WaveCone& wc, int w, int K,
-                                             int lane, float& best, int& code) {
+                                             int lane, float& best, int& code, unsigned long long* ex) {
   best = FLT_MAX;
   code = kNoHit;
+  unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
   for (int type = 0; type < 3; ++type) {
     const int n = type == 0 ? sc.ns : (type == 1 ? sc.na : sc.no);
     const int gofs = type == 0 ? 0 : (type == 1 ? sc.ns : sc.ns + sc.na);
@@ -229,6 +245,8 @@ __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, c
       CandSet cs;
       cs.m[0] = __ballot(cand);
       cs.left = __popcll(cs.m[0]);
+      ++nchk;
+      nt[type] += cs.left;
 #ifdef ART_DIAG_CULL_STATS
       if (lane == 0) { atomicAdd(&g_diag[4], (unsigned)min(64, e - cb)); atomicAdd(&g_diag[5], (unsigned)cs.left); }
 #endif
@@ -256,6 +274,10 @@ __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, c
       }
     }
   }
+  exec_add(ex, kExecSphere, 64ull * nt[0]);
+  exec_add(ex, kExecAabb, 64ull * nt[1]);
+  exec_add(ex, kExecObb, 64ull * nt[2]);
+  exec_add(ex, kExecCullCone, 64ull * nchk);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -583,8 +605,10 @@ struct WaveBox {
 };
 
 template <int U, typename Rec, typename Test>
-__device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet& cs, bool blocked, bool done, Test test) {
+__device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet& cs, bool blocked, bool done, Test test,
+                                                unsigned& nt) {
   while (cs.left >= U) {
+    nt += U;
     int idx[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) idx[u] = b + cs.pop();
@@ -598,13 +622,14 @@ __device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet&
   while (cs.left > 0) {
     const Rec r = ldc(recs, wave_uniform(b + cs.pop()));
     blocked |= test(r);
+    ++nt;
   }
   return blocked;
 }
 
 template <int U>
 __device__ __forceinline__ void visibility_culled(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
-                                                  int np, int lane) {
+                                                  int np, int lane, unsigned long long* ex) {
   const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
   const int nchunks = cm.total();
   for (;;) {
@@ -635,6 +660,7 @@ __device__ __forceinline__ void visibility_culled(const DevScene& sc, const Pair
     }
     bool blocked = false;
     const bool done = !valid;
+    unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
 #ifdef ART_DIAG_CULL_STATS
     {
       const unsigned nv = (unsigned)__popcll(__ballot(valid));
@@ -670,6 +696,7 @@ __device__ __forceinline__ void visibility_culled(const DevScene& sc, const Pair
       CandSet cs;
       cs.m[0] = __ballot(cand);
       cs.left = __popcll(cs.m[0]);
+      ++nchk;
 #ifdef ART_DIAG_CULL_STATS
       if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
 #endif
@@ -682,21 +709,25 @@ __device__ __forceinline__ void visibility_culled(const DevScene& sc, const Pair
         blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
           float d;
           return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
-        });
+        }, nt[0]);
       } else if (type == 1) {
         blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
           float d;
           return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
-        });
+        }, nt[1]);
       } else {
         blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
           float d;
           return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
-        });
+        }, nt[2]);
       }
       if (__all(blocked || done)) break;
     }
     if (valid) s_res[p] = blocked ? 1 : 0;
+    exec_add(ex, kExecSphere, 64ull * nt[0]);
+    exec_add(ex, kExecAabb, 64ull * nt[1]);
+    exec_add(ex, kExecObb, 64ull * nt[2]);
+    exec_add(ex, kExecCullBox, 64ull * nchk);
   }
 }
 
@@ -801,12 +832,14 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #if ART_FAST_CULL
     if (bounce == 0) {  // first segment: every ray of the fan starts at O
       const WaveCone wc = make_cone(O, d, alive);
-      nearest_cone<U>(sc, s, wc, w, K, lane, best, code);
+      nearest_cone<U>(sc, s, wc, w, K, lane, best, code, fp.exec);
     } else {
       nearest_chunk<U>(sc, s, w, K, best, code);
+      exec_brute(sc, w, K, fp.exec);
     }
 #else
     nearest_chunk<U>(sc, s, w, K, best, code);
+    exec_brute(sc, w, K, fp.exec);
 #endif
     s_dist[w][lane] = best;
     s_code[w][lane] = code;
@@ -881,7 +914,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #ifdef ART_DIAG_NO_VISIBILITY  // diagnostic build only: time the nearest-hit phase alone
     for (int p = w * 64 + lane; p < s_np; p += K * 64) s_res[p] = 0;
 #elif ART_FAST_CULL
-    visibility_culled<U>(sc, s_seg, s_res, &s_head, s_np, lane);
+    visibility_culled<U>(sc, s_seg, s_res, &s_head, s_np, lane, fp.exec);
 #elif ART_FAST_STAGED
     visibility_staged<U>(sc, s_seg, s_res, &s_head, s_go, s_stage, s_np, w, K, lane);
 #else

@@ -30,6 +30,10 @@ import torch  # noqa: E402
 import art  # noqa: E402
 from art import abi  # noqa: E402
 
+# Broad-phase bound tests, same counting rule: segment box vs collider bounds (margin 2, 6 widened
+# bounds, 6 compares) and shared-origin cone vs bounding sphere (centre 6, radius 8, distance 9,
+# angle terms 10, compare 2).
+CULL_OPS = {"cull_box": 14, "cull_cone": 35}
 # Algorithmic FP32 ops per test (SURVEY.md §8 d; miss path, IEEE add/sub/mul/div/sqrt/min/max/cmp = 1).
 OPS = {"rt_sphere": 26, "rt_aabb": 34, "rt_obb": 118, "perm_hit_sphere": 26, "perm_hit_aabb": 34, "perm_hit_obb": 134,
        "perm_loss_sphere": 18, "perm_loss_aabb": 33, "perm_loss_obb": 117}
@@ -128,6 +132,12 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     ktimes = ctx.kernel_timing()
+    # work the kernel actually executed in one frame (broad phase: fewer exact tests than counted)
+    ctx.set_flags(abi.ART_CTX_COUNT_EXECUTED)
+    ctx.executed_counts()  # reset
+    ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+    torch.cuda.synchronize()
+    executed = ctx.executed_counts()
     ctx.set_flags(0)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -156,6 +166,11 @@ def main():
     n_rt = max(1, ktimes["launches"])
     rt_ms = ktimes["raytrace_ms"] / n_rt
     achieved_tflops = rt_flops / (rt_ms * 1e-3) / 1e12
+    ex_launches = max(1, executed["launches"])
+    ex_ops = (executed["sphere"] * OPS["rt_sphere"] + executed["aabb"] * OPS["rt_aabb"] + executed["obb"] * OPS["rt_obb"] +
+              executed["cull_box"] * CULL_OPS["cull_box"] + executed["cull_cone"] * CULL_OPS["cull_cone"]) / ex_launches
+    ex_tests = (executed["sphere"] + executed["aabb"] + executed["obb"]) / ex_launches
+    ex_tflops = ex_ops / (rt_ms * 1e-3) / 1e12
     # algorithmic HBM bytes of one raytrace launch: collider AoS->SoA records are L2-resident after
     # the first wave, so the compulsory traffic is the SoA records + dirs + origins + outputs.
     rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 32 + scene.obbs.size * 64  # hot records
@@ -200,7 +215,15 @@ def main():
         "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "raytrace_fast_kernel", "kernel_ms": rt_ms,
-                     "note": "FP32 VALU roof (no MFMA-shaped work); algorithmic ops per test per SURVEY.md 8(d)",
+                     "note": "FP32 VALU roof (no MFMA-shaped work). achieved = the reference algorithm's tests x ops per "
+                             "test (SURVEY.md 8(d)) per launch / kernel time: brute-force-equivalent, since the kernel's "
+                             "exact broad phase skips tests that cannot hit. 'executed' is the work the kernel did.",
+                     "executed": {"achieved": ex_tflops, "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS,
+                                  "ops_per_launch": ex_ops, "exact_lane_tests_per_launch": ex_tests,
+                                  "reference_tests_per_launch": tests_rank,
+                                  "counts": {k: v // ex_launches for k, v in executed.items() if k != "launches"},
+                                  "note": "lane-tests = wave-level tests x 64 (all lanes issue); broad-phase bound "
+                                          "tests at CULL_OPS ops each"},
                      "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
                              "algorithmic_bytes": alg_bytes}},
         "kernel_ms": {"raytrace": rt_ms, "permeate": ktimes["permeate_ms"] / n_rt, "reduce": ktimes["reduce_ms"] / n_rt},

@@ -63,6 +63,19 @@ ART_API int art_launch_device(art_ctx* ctx, const float* d_origins, int32_t fan_
 ART_API int art_count_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
                              uint32_t out_flags, void* stream, art_test_counts* out);
 
+/* Count the work the throughput raytrace kernel actually executes (ART_CTX_COUNT_EXECUTED):
+ * exact intersection tests in lane-tests (every wave-level test counts 64, whatever the exec
+ * mask), and broad-phase bound tests in lane-evaluations. The tests/s metric counts the tests the
+ * reference algorithm executes (art_count_device); this is what the hardware did instead. */
+#define ART_CTX_COUNT_EXECUTED 0x10u
+typedef struct {
+    uint64_t sphere, aabb, obb;      /* exact lane-tests executed */
+    uint64_t cull_box, cull_cone;    /* broad-phase lane-evaluations (segment box / shared-origin cone) */
+    uint64_t launches;               /* frames counted */
+} art_exec_counts;
+/* Executed-work counters since the last call (needs ART_CTX_COUNT_EXECUTED); synchronizes. */
+ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);
+
 /* Sum of kernel times since the last call (needs ART_CTX_TIME_KERNELS); synchronizes. */
 ART_API int art_kernel_timing(art_ctx* ctx, art_kernel_times* out);
 
