@@ -98,6 +98,7 @@ struct Device {
   DevBuf raw, soa, origins, block, acc, counts;
   DevBuf work;  // ticket counters of the persistent raytrace kernel (self-rearming, zeroed once)
   DevBuf exec;  // executed-work counters (ART_CTX_COUNT_EXECUTED)
+  DevBuf pairs; // global visibility pairs of the split raytrace path
   uint64_t exec_launches = 0;
   DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
   int wf_blocks = 0;
@@ -411,9 +412,12 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   fp.muf_curve = reinterpret_cast<const float*>(raw + f.off_muf);
   const int2* slot_batch = reinterpret_cast<const int2*>(raw + f.off_tab);
   const uint8_t* muffle_reset = raw + f.off_reset;
-  const size_t acc_bytes = (size_t)fan_count * f.TC * f.T * sizeof(uint32_t);
+  // muffle accumulators, then (16-B aligned) the visibility pair counter: one memset clears both
+  const size_t acc_words = ((size_t)fan_count * f.TC * f.T + 3) & ~(size_t)3;
+  const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16;
   if (!dv.acc.reserve(acc_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   uint32_t* acc = static_cast<uint32_t*>(dv.acc.p);
+  uint32_t* pair_count = acc + acc_words;
   DevCounts* counts = nullptr;
   unsigned long long* nhit = nullptr;
   if (count) {
@@ -455,7 +459,11 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         fpx.exec = static_cast<unsigned long long*>(dv.exec.p);
         dv.exec_launches++;
       }
-      launch_raytrace_fast(dv.sc, fpx, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), st);
+      FrameParams fps = fpx;
+      fps.S = fan_count;
+      if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
+      launch_raytrace_fast(dv.sc, fpx, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), dv.pairs.p,
+                           pair_count, st);
     } else if (f.T <= 31) {
       int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);
       if (rc) return rc;
@@ -552,7 +560,7 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
-    dv.work.release(); dv.exec.release();
+    dv.work.release(); dv.exec.release(); dv.pairs.release();
     dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);

@@ -104,8 +104,12 @@ void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, co
                  CullRec* cull, hipStream_t st);
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, uint32_t* muffle_acc, DevCounts* counts, hipStream_t st);
+// Bytes of the global visibility pair array the throughput kernel needs for this frame (0 when the
+// fused in-block visibility is built).
+size_t fast_pair_bytes(const FrameParams& fp);
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st);
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,
+                          uint32_t* pair_count, hipStream_t st);
 int fast_split(int S, int R);
 int fast_max_targets();
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,

@@ -290,6 +290,9 @@ __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, c
 // colliders, so the cyclic chunk order gives the reference's verdict, and a wave only keeps
 // sweeping for lanes that are still unblocked.
 // ------------------------------------------------------------------------------------------
+#ifndef ART_FAST_SPLIT
+#define ART_FAST_SPLIT 1  // visibility in its own kernel (vis_kernel) fed by a global pair array
+#endif
 #ifndef ART_FAST_CULL
 #define ART_FAST_CULL 1  // broad-phase visibility (exact; see visibility_culled)
 #endif
@@ -627,11 +630,95 @@ __device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet&
   return blocked;
 }
 
+// Broad-phase any-hit sweep of one lane's segment (s, maxd, owner) for a wave of up to 64
+// segments (`valid` lanes): the wave's segment box, then per chunk the bound ballot and the exact
+// tests of the candidates. Returns the lane's verdict (true = blocked).
+__device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid, int lane,
+                                           unsigned long long* ex, bool done_in = false, int c_lo = 0, int c_hi = 1 << 30) {
+  const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
+  const int nchunks = min(cm.total(), c_hi);
+  if (c_lo >= nchunks) return false;
+  WaveBox wb;
+  {
+    const vec3 e = s.o + s.d * maxd;
+    const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+    wb.lx = wave_min(valid ? fminf(s.o.x, e.x) : INFINITY);
+    wb.ly = wave_min(valid ? fminf(s.o.y, e.y) : INFINITY);
+    wb.lz = wave_min(valid ? fminf(s.o.z, e.z) : INFINITY);
+    wb.hx = wave_max(valid ? fmaxf(s.o.x, e.x) : -INFINITY);
+    wb.hy = wave_max(valid ? fmaxf(s.o.y, e.y) : -INFINITY);
+    wb.hz = wave_max(valid ? fmaxf(s.o.z, e.z) : -INFINITY);
+    wb.om = wave_max(valid ? om : 0.0f);
+  }
+  bool blocked = false;
+  const bool done = !valid || done_in;
+  if (__all(done)) return false;
+  unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
+  auto chunk_at = [&](int c, int& type, int& b, int& n) {
+    if (c < cm.cs) { type = 0; b = c * kChunk; n = min(kChunk, sc.ns - b); return b; }
+    if (c - cm.cs < cm.ca) { type = 1; b = (c - cm.cs) * kChunk; n = min(kChunk, sc.na - b); return sc.ns + b; }
+    type = 2; b = (c - cm.cs - cm.ca) * kChunk; n = min(kChunk, sc.no - b);
+    return sc.ns + sc.na + b;
+  };
+  // software pipeline: the bounds of chunk c + 1 are loaded while chunk c's candidates are tested
+  CullRec nxt;
+  {
+    int t0, b0, n0;
+    const int g0 = chunk_at(c_lo, t0, b0, n0);
+    nxt = sc.cull[g0 + min(lane, n0 - 1)];
+  }
+  for (int c = c_lo; c < nchunks; ++c) {
+    int type, b, n;
+    chunk_at(c, type, b, n);
+    const CullRec cr = nxt;
+    if (c + 1 < nchunks) {
+      int t1, b1, n1;
+      const int g1 = chunk_at(c + 1, t1, b1, n1);
+      nxt = sc.cull[g1 + min(lane, n1 - 1)];
+    }
+    const float m = cr.factor * (cr.scale + wb.om);
+    const bool cand = (lane < n) & (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) &
+                      (cr.hiy + m >= wb.ly) & (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
+    CandSet cs;
+    cs.m[0] = __ballot(cand);
+    cs.left = __popcll(cs.m[0]);
+    ++nchk;
+#ifdef ART_DIAG_CULL_STATS
+    if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
+#endif
+#ifdef ART_DIAG_CULL_ONLY  // diagnostic build only: broad phase without the exact tests
+    blocked |= (cs.left == -1);
+    continue;
+#endif
+    if (cs.left == 0) continue;
+    if (type == 0) {
+      blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
+        float d;
+        return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
+      }, nt[0]);
+    } else if (type == 1) {
+      blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
+        float d;
+        return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+      }, nt[1]);
+    } else {
+      blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
+        float d;
+        return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+      }, nt[2]);
+    }
+    if (__all(blocked || done)) break;
+  }
+  exec_add(ex, kExecSphere, 64ull * nt[0]);
+  exec_add(ex, kExecAabb, 64ull * nt[1]);
+  exec_add(ex, kExecObb, 64ull * nt[2]);
+  exec_add(ex, kExecCullBox, 64ull * nchk);
+  return blocked;
+}
+
 template <int U>
 __device__ __forceinline__ void visibility_culled(const DevScene& sc, const PairSeg* s_seg, uint8_t* s_res, int* s_head,
                                                   int np, int lane, unsigned long long* ex) {
-  const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
-  const int nchunks = cm.total();
   for (;;) {
     int base = 0;
     if (lane == 0) base = atomicAdd(s_head, 64);
@@ -639,95 +726,98 @@ __device__ __forceinline__ void visibility_culled(const DevScene& sc, const Pair
     if (base >= np) break;
     const int p = base + lane;
     const bool valid = p < np;
+    const PairSeg g = s_seg[valid ? p : base];
     Seg s;
-    float maxd = 0.0f;
-    int owner = kNoOwner;
-    WaveBox wb;
-    {
-      PairSeg g = s_seg[valid ? p : base];
-      s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
-      s.a2 = g.a2; s.a4 = 2.0f * g.a2;
-      maxd = g.maxd; owner = g.owner;
-      const vec3 e = s.o + s.d * maxd;
-      const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
-      wb.lx = wave_min(valid ? fminf(s.o.x, e.x) : INFINITY);
-      wb.ly = wave_min(valid ? fminf(s.o.y, e.y) : INFINITY);
-      wb.lz = wave_min(valid ? fminf(s.o.z, e.z) : INFINITY);
-      wb.hx = wave_max(valid ? fmaxf(s.o.x, e.x) : -INFINITY);
-      wb.hy = wave_max(valid ? fmaxf(s.o.y, e.y) : -INFINITY);
-      wb.hz = wave_max(valid ? fmaxf(s.o.z, e.z) : -INFINITY);
-      wb.om = wave_max(valid ? om : 0.0f);
-    }
-    bool blocked = false;
-    const bool done = !valid;
-    unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
+    s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
+    s.a2 = g.a2; s.a4 = 2.0f * g.a2;
 #ifdef ART_DIAG_CULL_STATS
     {
       const unsigned nv = (unsigned)__popcll(__ballot(valid));
       if (lane == 0) { atomicAdd(&g_diag[0], 1u); atomicAdd(&g_diag[3], nv); }
     }
 #endif
-    // chunk geometry: type, first index within the type, valid count, global index of the bounds
-    auto chunk_at = [&](int c, int& type, int& b, int& n) {
-      if (c < cm.cs) { type = 0; b = c * kChunk; n = min(kChunk, sc.ns - b); return b; }
-      if (c - cm.cs < cm.ca) { type = 1; b = (c - cm.cs) * kChunk; n = min(kChunk, sc.na - b); return sc.ns + b; }
-      type = 2; b = (c - cm.cs - cm.ca) * kChunk; n = min(kChunk, sc.no - b);
-      return sc.ns + sc.na + b;
-    };
-    // software pipeline: the bounds of chunk c + 1 are loaded while chunk c's candidates are tested
-    CullRec nxt;
-    {
-      int t0, b0, n0;
-      const int g0 = chunk_at(0, t0, b0, n0);
-      nxt = sc.cull[g0 + min(lane, n0 - 1)];
-    }
-    for (int c = 0; c < nchunks; ++c) {
-      int type, b, n;
-      chunk_at(c, type, b, n);
-      const CullRec cr = nxt;
-      if (c + 1 < nchunks) {
-        int t1, b1, n1;
-        const int g1 = chunk_at(c + 1, t1, b1, n1);
-        nxt = sc.cull[g1 + min(lane, n1 - 1)];
-      }
-      const float m = cr.factor * (cr.scale + wb.om);
-      const bool cand = (lane < n) & (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) &
-                        (cr.hiy + m >= wb.ly) & (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
-      CandSet cs;
-      cs.m[0] = __ballot(cand);
-      cs.left = __popcll(cs.m[0]);
-      ++nchk;
-#ifdef ART_DIAG_CULL_STATS
-      if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
-#endif
-#ifdef ART_DIAG_CULL_ONLY  // diagnostic build only: broad phase without the exact tests
-      blocked |= (cs.left == -1);
-      continue;
-#endif
-      if (cs.left == 0) continue;
-      if (type == 0) {
-        blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
-          float d;
-          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[0]);
-      } else if (type == 1) {
-        blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
-          float d;
-          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[1]);
-      } else {
-        blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
-          float d;
-          return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
-        }, nt[2]);
-      }
-      if (__all(blocked || done)) break;
-    }
+    const bool blocked = cull_sweep(sc, s, g.maxd, g.owner, valid, lane, ex);
     if (valid) s_res[p] = blocked ? 1 : 0;
-    exec_add(ex, kExecSphere, 64ull * nt[0]);
-    exec_add(ex, kExecAabb, 64ull * nt[1]);
-    exec_add(ex, kExecObb, 64ull * nt[2]);
-    exec_add(ex, kExecCullBox, 64ull * nchk);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Split visibility (ART_FAST_SPLIT): the path kernel emits every (hit, query) pair with its output
+// destination into a global array; vis_kernel sweeps them in batches of 64 with the broad phase
+// and writes the visible echoes and muffle counts. Visibility never feeds back into ray paths
+// (echo :124-145 and muffle :150-173 only write outputs), so the two kernels give the same
+// results as the fused sweep, and each runs with its own, much smaller, register state.
+// ------------------------------------------------------------------------------------------
+struct alignas(16) PairG {
+  float ox, oy, oz, dx;
+  float dy, dz, ix, iy;
+  float iz, a2, maxd;
+  int owner;
+  uint32_t dest;   // echo: u16 index into the fan blocks; muffle: index into muffle_acc
+  uint32_t val;    // bits 0-15: echo half (f32tof16(dist * echo)); bit 16: muffle pair
+  uint32_t pad0, pad1;
+};
+constexpr uint32_t kPairMuffle = 1u << 16;
+
+#ifndef ART_VIS_WPE
+#define ART_VIS_WPE 6
+#endif
+#ifndef ART_VIS_RANGES
+#define ART_VIS_RANGES 8
+#endif
+constexpr int kVisRanges = ART_VIS_RANGES;  // chunk ranges per 64-pair batch (work items)
+
+// Work item i of vis_kernel = (chunk range r, batch b), range-major: r = i / nb_max, b = i % nb_max.
+// A batch's later ranges usually start after its earlier ones finished and skip the pairs those
+// already blocked (a stale read only costs work). Verdicts meet in PairG::pad0 through relaxed
+// device-scope atomicOr (no fences: an agent-scope release writes back the XCD's L2);
+// vis_finalize writes the outputs after the kernel boundary.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
+void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restrict__ count, uint32_t nb_max,
+                uint8_t* __restrict__ block, uint32_t* __restrict__ muffle_acc, unsigned long long* ex) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t np = ldc(count, 0);
+  const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t r = item / nb_max, b = item - r * nb_max;
+  const uint32_t base = b * 64u;
+  if (r >= (uint32_t)kVisRanges || base >= np) return;
+  const uint32_t p = base + lane;
+  const bool valid = p < np;
+  PairG& gp = pairs[valid ? p : base];
+  const PairG g = gp;
+  const bool known = valid && __hip_atomic_load(&gp.pad0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  Seg s;
+  s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
+  s.a2 = g.a2; s.a4 = 2.0f * g.a2;
+  const int nch = (sc.ns + kChunk - 1) / kChunk + (sc.na + kChunk - 1) / kChunk + (sc.no + kChunk - 1) / kChunk;
+  const int c_lo = (int)(((long long)nch * r) / kVisRanges), c_hi = (int)(((long long)nch * (r + 1)) / kVisRanges);
+  const bool blocked = cull_sweep(sc, s, g.maxd, g.owner, valid, lane, ex, known, c_lo, c_hi);
+  if (valid && blocked && !known) __hip_atomic_fetch_or(&gp.pad0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
+// visible): visible echoes are stored, visible muffle rays counted.
+__global__ __launch_bounds__(256) void vis_finalize(const PairG* __restrict__ pairs, const uint32_t* __restrict__ count,
+                                                    uint8_t* __restrict__ block, uint32_t* __restrict__ muffle_acc) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t np = ldc(count, 0);
+  const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+  if (__builtin_amdgcn_readfirstlane(p - lane) >= np) return;
+  const bool valid = p < np;
+  uint32_t flag = 1u, dest = 0u, val = 0u;
+  if (valid) { flag = pairs[p].pad0; dest = pairs[p].dest; val = pairs[p].val; }
+  const bool vis = valid && flag == 0u;
+  const bool muf = (val & kPairMuffle) != 0;
+  if (vis && !muf) reinterpret_cast<uint16_t*>(block)[dest] = (uint16_t)(val & 0xffffu);  // :142-144
+  // muffle counts (:171): one atomic per wave when the wave shares its counter
+  const unsigned long long mv = __ballot(vis && muf);
+  if (mv) {
+    const uint32_t d0 = __builtin_amdgcn_readlane(dest, __builtin_ctzll(mv));
+    if (__all(!(vis && muf) || dest == d0)) {
+      if (lane == 0) atomicAdd(&muffle_acc[d0], (uint32_t)__popcll(mv));
+    } else if (vis && muf) {
+      atomicAdd(&muffle_acc[dest], 1u);
+    }
   }
 }
 
@@ -757,7 +847,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                uint8_t* __restrict__ block,
                                                                uint32_t* __restrict__ muffle_acc,
                                                                const int* __restrict__ ray_order,
-                                                               uint32_t* __restrict__ work) {
+                                                               uint32_t* __restrict__ work,
+                                                               PairG* __restrict__ pairs,
+                                                               uint32_t* __restrict__ pair_count) {
   __shared__ float s_dist[K][64];
   __shared__ int s_code[K][64];
   __shared__ short s_pairof[kMaxQueries][64];
@@ -766,7 +858,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   __shared__ uint32_t s_muf[kMaxTargets];
   __shared__ int s_ticket;
   __shared__ int s_go[3];  // staged visibility only
-  (void)s_go;
+  (void)s_go; (void)s_pairof; (void)s_res; (void)s_head; (void)s_np;
 #ifdef ART_TEST_NO_OBB
   sc.no = 0;
 #endif
@@ -878,6 +970,60 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // visibility pairs: q = 0 echo ray to the origin (:124-145), q = 1..T muffle rays (:150-173)
     const vec3 off = o - d * kEps;                 // :124, :158
     const float dist0 = distance(O, o);            // :130 (un-offset hit point)
+#if ART_FAST_SPLIT
+    // Emit the pairs with their output destinations for vis_kernel (wave 0 owns the group's rays).
+    if (w == 0) {
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      unsigned long long mq[kMaxQueries];
+      uint32_t actbits = 0;
+      uint32_t np = 0;
+#pragma unroll
+      for (int q = 0; q < kMaxQueries; ++q) {
+        bool act = false;
+        if (q <= T) {
+          if (q == 0) act = live_slot;  // the echo is written only into a live slot (:118)
+          else act = hit && distance(off, load3(sc.targets, q - 1)) < fp.max_muffle;  // :165-168
+        }
+        mq[q] = __ballot(act);
+        actbits |= act ? (1u << q) : 0u;
+        np += (uint32_t)__popcll(mq[q]);
+      }
+      if (np) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(pair_count, np);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+        uint32_t pos = base;
+#pragma unroll
+        for (int q = 0; q < kMaxQueries; ++q) {
+          if (q <= T && ((actbits >> q) & 1u)) {
+            vec3 qdir;
+            float maxd;
+            PairG r;
+            if (q == 0) {
+              qdir = normalize(O - off); maxd = dist0; r.owner = kNoOwner;
+              r.dest = (uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k);
+              r.val = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
+            } else {
+              const vec3 tp = load3(sc.targets, q - 1);
+              maxd = distance(off, tp);
+              qdir = normalize(tp - off);
+              r.owner = q - 1;                                    // :413, :426, :439
+              r.dest = (uint32_t)(((size_t)fan * fp.TC + my_slot) * T + (q - 1));
+              r.val = kPairMuffle;
+            }
+            const Seg g = make_seg(off, qdir);
+            r.ox = g.o.x; r.oy = g.o.y; r.oz = g.o.z; r.dx = g.d.x; r.dy = g.d.y; r.dz = g.d.z;
+            r.ix = g.inv.x; r.iy = g.inv.y; r.iz = g.inv.z; r.a2 = g.a2; r.maxd = maxd;
+            r.pad0 = r.pad1 = 0u;
+            pairs[pos + (uint32_t)__popcll(mq[q] & lt)] = r;
+          }
+          pos += (q <= T) ? (uint32_t)__popcll(mq[q]) : 0u;
+        }
+      }
+      // a blocked echo leaves the reset value (:76); vis_kernel overwrites the visible ones
+      if (live_slot && single_slot) echo[ray * H + k] = 0;
+    }
+#else
     if (w == 0) {
       const unsigned long long lt = (1ull << lane) - 1ull;
       int np = 0;
@@ -935,6 +1081,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
         }
       }
     }
+
+#endif
 
     // termination / reflection — :179-193, ReflectRay :456-532 (every wave, identical state)
     if (hit) {
@@ -1019,6 +1167,7 @@ int fast_split(int S, int R) {
 }
 
 static size_t fast_lds_bytes(const DevScene& sc, int T) {
+  if (ART_FAST_SPLIT) return 0;
   return sizeof(PairSeg) * 64 * (size_t)(T + 1) + (ART_FAST_STAGED ? 2 * (size_t)stage_stride(sc) : 0);
 }
 
@@ -1043,36 +1192,55 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
 
 template <int K, bool HITS, int U, int WPE>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
+                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
+                           uint32_t* pair_count, hipStream_t st) {
   const size_t lds = fast_lds_bytes(sc, fp.T);
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   const int resident = resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE>, 64 * K, lds);
   const int nblk = (int)std::min<long long>(groups, resident);
   hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
-                     muffle_acc, ray_order, work);
+                     muffle_acc, ray_order, work, pairs, pair_count);
 }
 
 template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
+                          uint32_t* pair_count, hipStream_t st) {
   if (sc.no > 0) {
-    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
-    else launch_fast_kh<K, false, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
+    else launch_fast_kh<K, false, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
   } else {
-    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
-    else launch_fast_kh<K, false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st);
+    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
+    else launch_fast_kh<K, false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
   }
 }
 
+size_t fast_pair_bytes(const FrameParams& fp) {
+  return ART_FAST_SPLIT ? (size_t)fp.S * fp.R * fp.H * (fp.T + 1) * sizeof(PairG) : 0;
+}
+
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, hipStream_t st) {
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,
+                          uint32_t* pair_count, hipStream_t st) {
   if (fp.S == 0) return;
+  PairG* pairs = static_cast<PairG*>(pair_buf);
   switch (fast_split(fp.S, fp.R)) {
-    case 1: launch_fast_k<1>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
-    case 2: launch_fast_k<2>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
-    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
-    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, st); break;
+    case 1: launch_fast_k<1>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
+    case 2: launch_fast_k<2>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
+    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
+    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
   }
+#if ART_FAST_SPLIT
+  const size_t max_pairs = (size_t)fp.S * fp.R * fp.H * (fp.T + 1);
+  const uint32_t nb_max = (uint32_t)((max_pairs + 63) / 64);
+  const size_t items = (size_t)nb_max * kVisRanges;
+  if (items) {
+    hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pairs, pair_count, nb_max, block,
+                       muffle_acc, fp.exec);
+    hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pairs, pair_count, block,
+                       muffle_acc);
+  }
+#endif
 }
 
 }  // namespace art
