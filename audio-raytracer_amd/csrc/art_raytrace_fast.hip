@@ -757,6 +757,7 @@ struct alignas(16) PairG {
   uint32_t val;    // bits 0-15: echo half (f32tof16(dist * echo)); bit 16: muffle pair
   uint32_t pad0, pad1;
 };
+static_assert(sizeof(PairG) == 64 && offsetof(PairG, dest) == 48, "PairG layout");
 constexpr uint32_t kPairMuffle = 1u << 16;
 
 #ifndef ART_VIS_WPE
@@ -782,17 +783,26 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
   const uint32_t base = b * 64u;
   if (r >= (uint32_t)kVisRanges || base >= np) return;
   const uint32_t p = base + lane;
-  const bool valid = p < np;
-  PairG& gp = pairs[valid ? p : base];
-  const PairG g = gp;
-  const bool known = valid && __hip_atomic_load(&gp.pad0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  PairG& gp = pairs[p < np ? p : base];
+  // pairs an earlier range already blocked are skipped (not loaded, and out of the wave's box)
+  const bool valid = p < np && __hip_atomic_load(&gp.pad0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  if (!__any(valid)) return;
   Seg s;
-  s.o = mk3(g.ox, g.oy, g.oz); s.d = mk3(g.dx, g.dy, g.dz); s.inv = mk3(g.ix, g.iy, g.iz);
-  s.a2 = g.a2; s.a4 = 2.0f * g.a2;
+  float maxd = 0.0f;
+  int owner = kNoOwner;
+  s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
+  s.a2 = s.a4 = 0.0f;
+  if (valid) {
+    const float4* q = reinterpret_cast<const float4*>(&gp);  // the 48-B segment only
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+    s.o = mk3(q0.x, q0.y, q0.z); s.d = mk3(q0.w, q1.x, q1.y); s.inv = mk3(q1.z, q1.w, q2.x);
+    s.a2 = q2.y; s.a4 = 2.0f * q2.y;
+    maxd = q2.z; owner = __float_as_int(q2.w);
+  }
   const int nch = (sc.ns + kChunk - 1) / kChunk + (sc.na + kChunk - 1) / kChunk + (sc.no + kChunk - 1) / kChunk;
   const int c_lo = (int)(((long long)nch * r) / kVisRanges), c_hi = (int)(((long long)nch * (r + 1)) / kVisRanges);
-  const bool blocked = cull_sweep(sc, s, g.maxd, g.owner, valid, lane, ex, known, c_lo, c_hi);
-  if (valid && blocked && !known) __hip_atomic_fetch_or(&gp.pad0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi);
+  if (valid && blocked) __hip_atomic_fetch_or(&gp.pad0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts

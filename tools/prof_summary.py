@@ -20,8 +20,10 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-HOT = ("raytrace_fast_kernel", "wf_nearest", "wf_visibility", "wf_finalize", "raytrace_kernel", "permeate_kernel",
-       "reduce_kernel")
+HOT = ("raytrace_fast_kernel", "vis_kernel", "vis_finalize", "wf_nearest", "wf_visibility", "wf_finalize",
+       "raytrace_kernel", "permeate_kernel", "reduce_kernel")
+# kernels of the timed raytrace stage (one launch of each per frame)
+STAGE = ("raytrace_fast_kernel", "vis_kernel", "vis_finalize")
 
 
 def short(name: str) -> str:
@@ -64,14 +66,16 @@ def main():
             w.writeheader()
             w.writerows(rows)
 
-    # HBM traffic of the dominant (timed) raytrace kernel, per launch
-    dom = [k for k in per if k.startswith("raytrace_fast_kernel")]
-    if dom:
-        k = dom[0]
-        fetch_kb = sum(per[k]["FETCH_SIZE"]) / max(1, len(per[k]["FETCH_SIZE"]))
-        write_kb = sum(per[k]["WRITE_SIZE"]) / max(1, len(per[k]["WRITE_SIZE"]))
+    # HBM traffic of the timed raytrace stage per frame (sum over its kernels of the mean per launch)
+    stage = [k for k in per if k.startswith(STAGE)]
+    if stage:
+        def mean(k, c):
+            v = per[k].get(c, [])
+            return sum(v) / len(v) if v else 0.0
+        fetch_kb = sum(mean(k, "FETCH_SIZE") for k in stage)
+        write_kb = sum(mean(k, "WRITE_SIZE") for k in stage)
         rec = {
-            "kernel": k,
+            "kernels": sorted(stage),
             "fetch_size_kb_raw": fetch_kb,
             "write_size_kb": write_kb,
             # MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE reports half the bytes of a
