@@ -89,6 +89,8 @@ struct Frame {
   size_t off_sph = 0, off_aabb = 0, off_obb = 0, off_tgt = 0, off_dirs = 0, off_vol = 0, off_muf = 0, off_tab = 0,
          off_reset = 0, off_order = 0, raw_bytes = 0;
   size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_cull = 0, soa_bytes = 0;
+  size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
+  size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0;
 };
 
 struct Device {
@@ -298,6 +300,22 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
   f.soa_aabbc = s; s = align_up(s + (size_t)f.na * sizeof(AabbCold), 256);
   f.soa_obbc = s; s = align_up(s + (size_t)f.no * sizeof(ObbCold), 256);
   f.soa_cull = s; s = align_up(s + (size_t)(f.ns + f.na + f.no) * sizeof(CullRec), 256);
+  {  // broad-phase structure (art_bvh.hip)
+    const size_t n = (size_t)(f.ns + f.na + f.no);
+    const size_t nch = (size_t)((f.ns + 63) / 64 + (f.na + 63) / 64 + (f.no + 63) / 64);
+    f.sort_temp = sort_scene_temp_bytes((int)n);
+    f.soa_box = s; s = align_up(s + 6 * sizeof(float), 256);
+    f.soa_keys = s; s = align_up(s + n * 4, 256);
+    f.soa_keys_s = s; s = align_up(s + n * 4, 256);
+    f.soa_vals = s; s = align_up(s + n * 4, 256);
+    f.soa_perm = s; s = align_up(s + n * 4, 256);
+    f.soa_temp = s; s = align_up(s + f.sort_temp, 256);
+    f.soa_sph_s = s; s = align_up(s + (size_t)f.ns * sizeof(SphereRec), 256);
+    f.soa_aabb_s = s; s = align_up(s + (size_t)f.na * sizeof(AabbRec), 256);
+    f.soa_obb_s = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
+    f.soa_cull_s = s; s = align_up(s + n * sizeof(CullRec), 256);
+    f.soa_chunks = s; s = align_up(s + nch * sizeof(CullRec), 256);
+  }
   f.soa_bytes = s;
 }
 
@@ -337,6 +355,18 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sc.cull = reinterpret_cast<const CullRec*>(soa + f.soa_cull);
   sc.targets = reinterpret_cast<const float*>(raw + f.off_tgt); sc.T = f.T;
   sc.dirs = reinterpret_cast<const uint16_t*>(raw + f.off_dirs); sc.R = f.R;
+  SortBufs sb;
+  sb.box = reinterpret_cast<float*>(soa + f.soa_box);
+  sb.keys = reinterpret_cast<uint32_t*>(soa + f.soa_keys); sb.keys_s = reinterpret_cast<uint32_t*>(soa + f.soa_keys_s);
+  sb.vals = reinterpret_cast<int*>(soa + f.soa_vals); sb.perm = reinterpret_cast<int*>(soa + f.soa_perm);
+  sb.temp = soa + f.soa_temp; sb.temp_bytes = f.sort_temp;
+  sb.sph_s = reinterpret_cast<SphereRec*>(soa + f.soa_sph_s); sb.aabb_s = reinterpret_cast<AabbRec*>(soa + f.soa_aabb_s);
+  sb.obb_s = reinterpret_cast<ObbRec*>(soa + f.soa_obb_s); sb.cull_s = reinterpret_cast<CullRec*>(soa + f.soa_cull_s);
+  sb.chunks = reinterpret_cast<CullRec*>(soa + f.soa_chunks);
+  sc.sph_s = nullptr; sc.aabb_s = nullptr; sc.obb_s = nullptr; sc.cull_s = nullptr; sc.chunks = nullptr; sc.nchunks = 0;
+  if (fast_uses_sorted_scene() && launch_sort_scene(sc, sb, dv.stream) != 0)
+    return fail(c, ART_E_DEVICE, "collider sort failed");
+  HIP_TRY(c, hipGetLastError());
   dv.bound = true;
   return ART_OK;
 }

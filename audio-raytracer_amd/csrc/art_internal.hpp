@@ -69,7 +69,23 @@ struct DevScene {
   const float* targets; int T;    // float3[T]
   const uint16_t* dirs; int R;    // half3[R] as 3 x u16
   const CullRec* cull;            // [ns + na + no]
+  // spatially sorted copies (art_bvh.hip): Morton order within each type; the records' pad field
+  // holds the original in-type index
+  const SphereRec* sph_s; const AabbRec* aabb_s; const ObbRec* obb_s;
+  const CullRec* cull_s;          // [ns + na + no], sorted order
+  const CullRec* chunks;          // [nchunks]: union bounds of 64 sorted colliders of one type
+  int nchunks;
 };
+
+struct SortBufs {
+  float* box;                     // 6 floats
+  uint32_t* keys; uint32_t* keys_s; int* vals; int* perm;
+  void* temp; size_t temp_bytes;
+  SphereRec* sph_s; AabbRec* aabb_s; ObbRec* obb_s; CullRec* cull_s; CullRec* chunks;
+};
+size_t sort_scene_temp_bytes(int n);
+bool fast_uses_sorted_scene();  // whether the throughput kernel reads the sorted copies
+int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
 
 // Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
 struct FanLayout {

@@ -218,6 +218,94 @@ __device__ __forceinline__ bool cone_candidate(const WaveCone& wc, const CullRec
   return vx * wc.ax + vy * wc.ay + vz * wc.az >= (cos_lim - 1e-4f) * L;
 }
 
+// Front-to-back nearest hit over the spatially sorted chunks for rays sharing their origin O (the
+// first segment). Wave w considers chunks c = w, w + K, ...; per pass of 64 of them, the chunks whose
+// bounds meet the wave's cone are visited in increasing order of a conservative lower bound of any
+// member's hit distance (distance from O to the chunk's widened bounds, shrunk for |d| != 1), and the
+// sweep stops once that bound exceeds every lane's current best (shared by the block's waves through
+// s_best, best only ever decreases, so a stale read only prunes less). Inside a chunk the members
+// meeting the cone get the exact test; (distance, rank<<28 | original index) decides ties as the
+// reference's first minimum over Sphere, AABB, OBB order does.
+template <int K>
+__device__ __forceinline__ void nearest_sorted(const DevScene& sc, const Seg& s, const WaveCone& wc, int w, int lane,
+                                               bool alive, float (*s_best)[64], float& best, int& code,
+                                               unsigned long long* ex) {
+  best = FLT_MAX;
+  code = kNoHit;
+  const int cs_n = (sc.ns + 63) / 64, ca_n = (sc.na + 63) / 64;
+  const int nch = sc.nchunks;
+  const int nmine = (nch - w + K - 1) / K;  // chunks of this wave
+  unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
+  s_best[w][lane] = FLT_MAX;
+  for (int pb = 0; pb < nmine; pb += 64) {
+    const int mine = pb + lane;
+    float key = INFINITY;
+    if (mine < nmine) {
+      const CullRec cr = sc.chunks[w + mine * K];
+      if (cone_candidate(wc, cr)) {
+        const float m = cr.factor * (cr.scale + wc.om);
+        const float dx = fmaxf(fmaxf(cr.lox - m - wc.ox, wc.ox - cr.hix - m), 0.0f);
+        const float dy = fmaxf(fmaxf(cr.loy - m - wc.oy, wc.oy - cr.hiy - m), 0.0f);
+        const float dz = fmaxf(fmaxf(cr.loz - m - wc.oz, wc.oz - cr.hiz - m), 0.0f);
+        key = sqrtf(dx * dx + dy * dy + dz * dz) * 0.99f;  // |d| of a half3 direction is 1 +- 1e-3
+        key = isfinite(key) ? key : 0.0f;
+      }
+    }
+    for (;;) {
+      const float kmin = wave_min(key);
+      if (!(kmin < INFINITY)) break;
+      // prune: no member of a chunk at distance >= kmin can beat a lane's best (all waves)
+      float bl = best;
+#pragma unroll
+      for (int k = 0; k < K; ++k) bl = fminf(bl, s_best[k][lane]);
+      const float bound = wave_max(alive ? bl : -INFINITY);
+      if (kmin > bound) break;
+      const int pick = (int)__builtin_ctzll(__ballot(key == kmin));
+      if (lane == pick) key = INFINITY;
+      const int c = w + (pb + pick) * K;
+      int type, b, n;
+      if (c < cs_n) { type = 0; b = c * 64; n = min(64, sc.ns - b); }
+      else if (c < cs_n + ca_n) { type = 1; b = (c - cs_n) * 64; n = min(64, sc.na - b); }
+      else { type = 2; b = (c - cs_n - ca_n) * 64; n = min(64, sc.no - b); }
+      const int g = type == 0 ? b : (type == 1 ? sc.ns + b : sc.ns + sc.na + b);
+      bool cand = false;
+      if (lane < n) cand = cone_candidate(wc, sc.cull_s[g + lane]);
+      CandSet cset;
+      cset.m[0] = __ballot(cand);
+      cset.left = __popcll(cset.m[0]);
+      ++nchk;
+      nt[type] += cset.left;
+      if (type == 0) {
+        while (cset.left > 0) {
+          const SphereRec r = ldc(sc.sph_s, wave_uniform(b + cset.pop()));
+          float d;
+          const int cc = r.pad0;
+          if (sphere_hit_dist(s, r, d) && (d < best || (d == best && cc < code))) { best = d; code = cc; }
+        }
+      } else if (type == 1) {
+        while (cset.left > 0) {
+          const AabbRec r = ldc(sc.aabb_s, wave_uniform(b + cset.pop()));
+          float d;
+          const int cc = (1 << 28) | __float_as_int(r.pad);
+          if (aabb_test<false>(s, r, d) && (d < best || (d == best && cc < code))) { best = d; code = cc; }
+        }
+      } else {
+        while (cset.left > 0) {
+          const ObbRec r = ldc(sc.obb_s, wave_uniform(b + cset.pop()));
+          float d;
+          const int cc = (2 << 28) | __float_as_int(r.pad0);
+          if (obb_test<false>(s, r, stored_q(r), d) && (d < best || (d == best && cc < code))) { best = d; code = cc; }
+        }
+      }
+      s_best[w][lane] = best;
+    }
+  }
+  exec_add(ex, kExecSphere, 64ull * nt[0]);
+  exec_add(ex, kExecAabb, 64ull * nt[1]);
+  exec_add(ex, kExecObb, 64ull * nt[2]);
+  exec_add(ex, kExecCullCone, 64ull * (nchk + (unsigned)nmine));
+}
+
 // brute-force nearest sweep of this wave's ranges (nearest_chunk): every collider of the range
 __device__ __forceinline__ void exec_brute(const DevScene& sc, int w, int K, unsigned long long* ex) {
   if (!ex) return;
@@ -290,6 +378,16 @@ __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, c
 // colliders, so the cyclic chunk order gives the reference's verdict, and a wave only keeps
 // sweeping for lanes that are still unblocked.
 // ------------------------------------------------------------------------------------------
+#ifndef ART_FAST_TWO_LEVEL
+// 1: visibility walks the spatially sorted chunks' union bounds first when the scene has more than
+// 64 chunks (config 4: +1 %; the larger kernel cost configs 2/5 1-4 %, so off by default)
+#define ART_FAST_TWO_LEVEL 0
+#endif
+#ifndef ART_FAST_SORTED_NEAREST
+#define ART_FAST_SORTED_NEAREST 0  // 1: first-segment nearest hit front to back over sorted chunks
+// (measured no faster on config 2: pruning needs every lane of a wide cone to have a hit; and the
+// cross-wave best sharing would need a barrier-protected reset before it is exact)
+#endif
 #ifndef ART_FAST_SPLIT
 #define ART_FAST_SPLIT 1  // visibility in its own kernel (vis_kernel) fed by a global pair array
 #endif
@@ -654,61 +752,124 @@ __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, flo
   const bool done = !valid || done_in;
   if (__all(done)) return false;
   unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
+  // chunk c: type, first sorted index within the type, member count; returns the global sorted index
   auto chunk_at = [&](int c, int& type, int& b, int& n) {
     if (c < cm.cs) { type = 0; b = c * kChunk; n = min(kChunk, sc.ns - b); return b; }
     if (c - cm.cs < cm.ca) { type = 1; b = (c - cm.cs) * kChunk; n = min(kChunk, sc.na - b); return sc.ns + b; }
     type = 2; b = (c - cm.cs - cm.ca) * kChunk; n = min(kChunk, sc.no - b);
     return sc.ns + sc.na + b;
   };
-  // software pipeline: the bounds of chunk c + 1 are loaded while chunk c's candidates are tested
-  CullRec nxt;
-  {
-    int t0, b0, n0;
-    const int g0 = chunk_at(c_lo, t0, b0, n0);
-    nxt = sc.cull[g0 + min(lane, n0 - 1)];
-  }
-  for (int c = c_lo; c < nchunks; ++c) {
-    int type, b, n;
-    chunk_at(c, type, b, n);
-    const CullRec cr = nxt;
-    if (c + 1 < nchunks) {
-      int t1, b1, n1;
-      const int g1 = chunk_at(c + 1, t1, b1, n1);
-      nxt = sc.cull[g1 + min(lane, n1 - 1)];
+  if (!ART_FAST_TWO_LEVEL || sc.nchunks <= 64) {
+    // Flat: every chunk's members against the wave box (original order; the bounds of chunk c + 1
+    // are loaded while chunk c's candidates are tested).
+    CullRec nxt;
+    {
+      int t0, b0, n0;
+      const int g0 = chunk_at(c_lo, t0, b0, n0);
+      nxt = sc.cull[g0 + min(lane, n0 - 1)];
     }
-    const float m = cr.factor * (cr.scale + wb.om);
-    const bool cand = (lane < n) & (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) &
-                      (cr.hiy + m >= wb.ly) & (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
-    CandSet cs;
-    cs.m[0] = __ballot(cand);
-    cs.left = __popcll(cs.m[0]);
-    ++nchk;
+    for (int c = c_lo; c < nchunks; ++c) {
+      int type, b, n;
+      chunk_at(c, type, b, n);
+      const CullRec cr = nxt;
+      if (c + 1 < nchunks) {
+        int t1, b1, n1;
+        const int g1 = chunk_at(c + 1, t1, b1, n1);
+        nxt = sc.cull[g1 + min(lane, n1 - 1)];
+      }
+      const float m = cr.factor * (cr.scale + wb.om);
+      const bool cand = (lane < n) & (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) &
+                        (cr.hiy + m >= wb.ly) & (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
+      CandSet cs;
+      cs.m[0] = __ballot(cand);
+      cs.left = __popcll(cs.m[0]);
+      ++nchk;
 #ifdef ART_DIAG_CULL_STATS
-    if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
+      if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
+#endif
+      if (cs.left == 0) continue;
+      if (type == 0) {
+        blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
+          float d;
+          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
+        }, nt[0]);
+      } else if (type == 1) {
+        blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
+          float d;
+          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+        }, nt[1]);
+      } else {
+        blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
+          float d;
+          return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+        }, nt[2]);
+      }
+      if (__all(blocked || done)) break;
+    }
+    exec_add(ex, kExecSphere, 64ull * nt[0]);
+    exec_add(ex, kExecAabb, 64ull * nt[1]);
+    exec_add(ex, kExecObb, 64ull * nt[2]);
+    exec_add(ex, kExecCullBox, 64ull * nchk);
+    return blocked;
+  }
+#if ART_FAST_TWO_LEVEL
+  // Two levels over the spatially sorted colliders (art_bvh.hip): the chunks' union bounds
+  // (lane = chunk, 64 per pass), then the members of the candidate chunks (lane = collider).
+  for (int pb = c_lo; pb < nchunks; pb += 64) {
+    const int pc = pb + lane;
+    bool ccand = false;
+    if (pc < nchunks) {
+      const CullRec cr = sc.chunks[pc];
+      const float m = cr.factor * (cr.scale + wb.om);
+      ccand = (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) & (cr.hiy + m >= wb.ly) &
+              (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
+    }
+    unsigned long long cm_mask = __ballot(ccand);
+    while (cm_mask) {
+      const int c = pb + (int)__builtin_ctzll(cm_mask);
+      cm_mask &= cm_mask - 1;
+      int type, b, n;
+      const int g = chunk_at(c, type, b, n);
+      bool cand = false;
+      if (lane < n) {
+        const CullRec cr = sc.cull_s[g + lane];
+        const float m = cr.factor * (cr.scale + wb.om);
+        cand = (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) & (cr.hiy + m >= wb.ly) &
+               (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
+      }
+      CandSet cs;
+      cs.m[0] = __ballot(cand);
+      cs.left = __popcll(cs.m[0]);
+      ++nchk;
+#ifdef ART_DIAG_CULL_STATS
+      if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
 #endif
 #ifdef ART_DIAG_CULL_ONLY  // diagnostic build only: broad phase without the exact tests
-    blocked |= (cs.left == -1);
-    continue;
+      blocked |= (cs.left == -1);
+      continue;
 #endif
-    if (cs.left == 0) continue;
-    if (type == 0) {
-      blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
-        float d;
-        return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
-      }, nt[0]);
-    } else if (type == 1) {
-      blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
-        float d;
-        return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
-      }, nt[1]);
-    } else {
-      blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
-        float d;
-        return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
-      }, nt[2]);
+      if (cs.left == 0) continue;
+      if (type == 0) {
+        blocked = test_candidates<kCullU>(sc.sph_s, b, cs, blocked, done, [&](const SphereRec& r) {
+          float d;
+          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
+        }, nt[0]);
+      } else if (type == 1) {
+        blocked = test_candidates<kCullU>(sc.aabb_s, b, cs, blocked, done, [&](const AabbRec& r) {
+          float d;
+          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+        }, nt[1]);
+      } else {
+        blocked = test_candidates<1>(sc.obb_s, b, cs, blocked, done, [&](const ObbRec& r) {
+          float d;
+          return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+        }, nt[2]);
+      }
+      if (__all(blocked || done)) break;
     }
     if (__all(blocked || done)) break;
   }
+#endif
   exec_add(ex, kExecSphere, 64ull * nt[0]);
   exec_add(ex, kExecAabb, 64ull * nt[1]);
   exec_add(ex, kExecObb, 64ull * nt[2]);
@@ -861,6 +1022,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                PairG* __restrict__ pairs,
                                                                uint32_t* __restrict__ pair_count) {
   __shared__ float s_dist[K][64];
+  __shared__ float s_best[K][64];  // running per-lane best of each wave (front-to-back pruning)
+  (void)s_best;
   __shared__ int s_code[K][64];
   __shared__ short s_pairof[kMaxQueries][64];
   __shared__ uint8_t s_res[kMaxQueries * 64];
@@ -934,7 +1097,11 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #if ART_FAST_CULL
     if (bounce == 0) {  // first segment: every ray of the fan starts at O
       const WaveCone wc = make_cone(O, d, alive);
+#if ART_FAST_SORTED_NEAREST
+      nearest_sorted<K>(sc, s, wc, w, lane, alive, s_best, best, code, fp.exec);
+#else
       nearest_cone<U>(sc, s, wc, w, K, lane, best, code, fp.exec);
+#endif
     } else {
       nearest_chunk<U>(sc, s, w, K, best, code);
       exec_brute(sc, w, K, fp.exec);
@@ -1224,6 +1391,8 @@ static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLa
     else launch_fast_kh<K, false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
   }
 }
+
+bool fast_uses_sorted_scene() { return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST; }
 
 size_t fast_pair_bytes(const FrameParams& fp) {
   return ART_FAST_SPLIT ? (size_t)fp.S * fp.R * fp.H * (fp.T + 1) * sizeof(PairG) : 0;
