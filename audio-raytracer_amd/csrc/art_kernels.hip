@@ -299,33 +299,82 @@ __device__ __forceinline__ float perm_term_slab(float ox, float oy, float oz, fl
   return umax(0.0f, tExit - enter) * density;
 }
 
+// Permeation first hit of one ray (ShootRayCast :101-141, OBB with the inverted stored rotation
+// :172-179) with the block's threads over the colliders: each thread keeps the first minimum of its
+// colliders (ascending global order, strict <), and a block reduction by (distance, global order)
+// gives the reference's first minimum over Sphere, AABB, OBB order. Block-uniform result.
+__device__ Hit nearest_block_perm(const DevScene& sc, const Seg& s, int tid, float* s_rd, int* s_ri) {
+  const int ctot = sc.ns + sc.na + sc.no;
+  float bd = __builtin_huge_valf();
+  int bi = 0x7fffffff;
+  for (int c = tid; c < ctot; c += kPermBlock) {
+    float d;
+    bool hit;
+    if (c < sc.ns) {
+      hit = sphere_test(s, sc.sph[c], d);
+    } else if (c < sc.ns + sc.na) {
+      hit = aabb_test<false>(s, sc.aabb[c - sc.ns], d);
+    } else {
+      const int i = c - sc.ns - sc.na;
+      hit = obb_test<false>(s, sc.obb[i], inverse_q(sc.obbc[i]), d);
+    }
+    if (hit && d < bd) { bd = d; bi = c; }
+  }
+  s_rd[tid] = bd;
+  s_ri[tid] = bi;
+  __syncthreads();
+  for (int st = kPermBlock / 2; st > 0; st >>= 1) {
+    if (tid < st) {
+      const float d2 = s_rd[tid + st];
+      const int i2 = s_ri[tid + st];
+      if (d2 < s_rd[tid] || (d2 == s_rd[tid] && i2 < s_ri[tid])) { s_rd[tid] = d2; s_ri[tid] = i2; }
+    }
+    __syncthreads();
+  }
+  Hit h;
+  h.type = kNone; h.idx = -1; h.dist = s_rd[0];
+  const int g = s_ri[0];
+  __syncthreads();  // s_rd / s_ri are reused by the next call
+  if (g == 0x7fffffff) return h;
+  if (g < sc.ns) {
+    h.type = kSphere; h.idx = g;
+  } else if (g < sc.ns + sc.na) {
+    h.type = kAabb; h.idx = g - sc.ns;
+    float d; aabb_test<true>(s, sc.aabb[h.idx], d); h.dist = d;  // exact re-evaluation (zero sign)
+  } else {
+    h.type = kObb; h.idx = g - sc.ns - sc.na;
+    float d; obb_test<true>(s, sc.obb[h.idx], inverse_q(sc.obbc[h.idx]), d); h.dist = d;
+  }
+  if (h.dist == __builtin_huge_valf()) h.type = kNone;  // :140 closestDist != INFINITY
+  return h;
+}
+
 __global__ __launch_bounds__(kPermBlock) void permeate_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                               const float* __restrict__ origins, uint8_t* __restrict__ block,
                                                               const int2* __restrict__ slot_batch) {
-  __shared__ int s_best;
   __shared__ Hit s_hit;
   __shared__ float s_terms[kPermBlock];
+  __shared__ float s_rd[kPermBlock];
+  __shared__ int s_ri[kPermBlock];
   const int fan = blockIdx.y, slot = blockIdx.x, tid = threadIdx.x;
   const int2 br = slot_batch[slot];
   if (br.y <= br.x) return;  // no batch maps to this slot: value stays (stale / uninitialized, Q7)
   const vec3 O = load3(origins, fan);
   LaneCounts lc = {0, 0, 0};
 
-  // Phase 1: highest-index ray in [br.x, br.y) whose first hit exists (ShootRayCast :58).
+  // Phase 1: highest-index ray in [br.x, br.y) whose first hit exists (ShootRayCast :58). Rays
+  // are taken from the end one at a time, each with the block's threads over the colliders
+  // (lane = collider); the first ray that hits ends the search, so usually one sweep is needed.
   int found = -1;
-  for (int end = br.y; end > br.x; end -= kPermBlock) {
-    const int ray = end - 1 - tid;
-    Hit h;
-    h.type = kNone;
-    if (ray >= br.x) h = nearest<true, false>(sc, make_seg(O, load_dir(sc.dirs, ray)), lc);
-    if (tid == 0) s_best = 0x7fffffff;
-    __syncthreads();
-    if (h.type != kNone) atomicMin(&s_best, tid);
-    __syncthreads();
-    const int b = s_best;
-    if (b != 0x7fffffff && tid == b) s_hit = h;
-    __syncthreads();
-    if (b != 0x7fffffff) { found = end - 1 - b; break; }
+  (void)lc;
+  for (int ray = br.y - 1; ray >= br.x; --ray) {
+    const Hit h = nearest_block_perm(sc, make_seg(O, load_dir(sc.dirs, ray)), tid, s_rd, s_ri);
+    if (h.type != kNone) {
+      if (tid == 0) s_hit = h;
+      __syncthreads();
+      found = ray;
+      break;
+    }
   }
 
   float* ppr = reinterpret_cast<float*>(block + (size_t)fan * L.stride + L.perm_off);
