@@ -1012,7 +1012,9 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 #define ART_FAST_U_OBB 4
 #endif
 
-template <int K, bool HITS, int U, int WPE>
+// MULTI = false: frames with one hit per ray (H == 1, configs 2-4) compile without the later-bounce
+// nearest sweep and the reflection, which removes their registers from the kernel.
+template <int K, bool HITS, int U, int WPE, bool MULTI>
 __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
@@ -1055,7 +1057,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   const int slot = (g - fan * nrb) * 64 + lane;
   const bool valid = slot < fp.R;
   const int ray = valid ? ray_order[slot] : 0;
-  const int T = fp.T, H = fp.H;
+  const int T = fp.T, H = MULTI ? fp.H : 1;
   for (int t = threadIdx.x; t < T; t += blockDim.x) s_muf[t] = 0;
 
   uint8_t* fb = block + (size_t)fan * L.stride;
@@ -1095,14 +1097,14 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     float best;
     int code;
 #if ART_FAST_CULL
-    if (bounce == 0) {  // first segment: every ray of the fan starts at O
+    if (!MULTI || bounce == 0) {  // first segment: every ray of the fan starts at O
       const WaveCone wc = make_cone(O, d, alive);
 #if ART_FAST_SORTED_NEAREST
       nearest_sorted<K>(sc, s, wc, w, lane, alive, s_best, best, code, fp.exec);
 #else
       nearest_cone<U>(sc, s, wc, w, K, lane, best, code, fp.exec);
 #endif
-    } else {
+    } else if (MULTI) {
       nearest_chunk<U>(sc, s, w, K, best, code);
       exec_brute(sc, w, K, fp.exec);
     }
@@ -1262,7 +1264,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #endif
 
     // termination / reflection — :179-193, ReflectRay :456-532 (every wave, identical state)
-    if (hit) {
+    if (!MULTI) {
+      alive = false;  // hits >= H == 1 after the first hit; a miss has already ended the ray
+    } else if (hit) {
       if (hits >= H || life <= 0.0f) {
         alive = false;
       } else {
@@ -1332,15 +1336,15 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 
 int fast_max_targets() { return kMaxQueries - 1; }
 
-// Waves per 64-ray group: enough waves to cover the chip (~24 per CU), at most 8.
+// Waves per 64-ray group. K = 8 measured best on every config once the visibility moved to its own
+// kernel (config 2: 0.79 ms vs 0.83 at K = 4 and 0.90 at K = 16; config 4: 16.4 ms vs 20.3 at
+// the K = 1 the old occupancy rule picked).
 int fast_split(int S, int R) {
+  (void)S; (void)R;
 #ifdef ART_FAST_FORCE_K
   return ART_FAST_FORCE_K;
 #endif
-  const long long groups = (long long)S * ((R + 63) / 64);
-  int K = 1;
-  while (K < 8 && groups * K < 256LL * 24) K *= 2;
-  return K;
+  return 8;
 }
 
 static size_t fast_lds_bytes(const DevScene& sc, int T) {
@@ -1367,15 +1371,15 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
   return blocks;
 }
 
-template <int K, bool HITS, int U, int WPE>
+template <int K, bool HITS, int U, int WPE, bool MULTI>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
                            uint32_t* pair_count, hipStream_t st) {
   const size_t lds = fast_lds_bytes(sc, fp.T);
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
-  const int resident = resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE>, 64 * K, lds);
+  const int resident = resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI>, 64 * K, lds);
   const int nblk = (int)std::min<long long>(groups, resident);
-  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
                      muffle_acc, ray_order, work, pairs, pair_count);
 }
 
@@ -1383,13 +1387,18 @@ template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
                           uint32_t* pair_count, hipStream_t st) {
+  // instantiation by scene kind (OBBs or not), hit outputs, and one or several hits per ray
+#define ART_LAUNCH(H_, U_, W_, M_) \
+  launch_fast_kh<K, H_, U_, W_, M_>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st)
+  const bool multi = fp.H > 1;
   if (sc.no > 0) {
-    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
-    else launch_fast_kh<K, false, ART_FAST_U_OBB, ART_FAST_WPE_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
+    if (L.has_hits) { if (multi) ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, true); else ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, false); }
+    else { if (multi) ART_LAUNCH(false, ART_FAST_U_OBB, ART_FAST_WPE_OBB, true); else ART_LAUNCH(false, ART_FAST_U_OBB, ART_FAST_WPE_OBB, false); }
   } else {
-    if (L.has_hits) launch_fast_kh<K, true, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
-    else launch_fast_kh<K, false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st);
+    if (L.has_hits) { if (multi) ART_LAUNCH(true, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB, true); else ART_LAUNCH(true, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB, false); }
+    else { if (multi) ART_LAUNCH(false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB, true); else ART_LAUNCH(false, ART_FAST_U_NO_OBB, ART_FAST_WPE_NO_OBB, false); }
   }
+#undef ART_LAUNCH
 }
 
 bool fast_uses_sorted_scene() { return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST; }
@@ -1404,8 +1413,6 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   if (fp.S == 0) return;
   PairG* pairs = static_cast<PairG*>(pair_buf);
   switch (fast_split(fp.S, fp.R)) {
-    case 1: launch_fast_k<1>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
-    case 2: launch_fast_k<2>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
     case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
     default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
   }
