@@ -315,18 +315,85 @@ __device__ __forceinline__ void exec_brute(const DevScene& sc, int w, int K, uns
   chunk_of(sc.no, w, K, b, e); exec_add(ex, kExecObb, 64ull * (e - b));
 }
 
+#ifndef ART_CONE_MODE
+#define ART_CONE_MODE 0
+#endif
+#ifndef ART_CONE_DYNAMIC
+#define ART_CONE_DYNAMIC 1  // waves of a block take nearest-hit chunks dynamically (balance)
+#endif
+// Nearest-hit tests of a chunk's candidates in increasing index order with a strict `<`.
+template <int U, typename Rec, typename Test>
+__device__ __forceinline__ void nearest_group(const Rec* recs, int b, CandSet& cs, int rank, float& best, int& code,
+                                              Test test) {
+  while (cs.left >= U) {
+    int idx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) idx[u] = b + cs.pop();
+    Rec r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = ldc(recs, wave_uniform(idx[u]));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float d;
+      if (test(r[u], d) && d < best) { best = d; code = rank | idx[u]; }
+    }
+  }
+  while (cs.left > 0) {
+    const int i = b + cs.pop();
+    const Rec r = ldc(recs, wave_uniform(i));
+    float d;
+    if (test(r, d) && d < best) { best = d; code = rank | i; }
+  }
+}
+template <typename Rec, typename Test>
+__device__ __forceinline__ void nearest_pipe(const Rec* recs, int b, CandSet& cs, int rank, float& best, int& code,
+                                             Test test) {
+  if (cs.left <= 0) return;
+  int i = b + cs.pop();
+  Rec cur = ldc(recs, wave_uniform(i));
+  for (;;) {
+    const bool more = cs.left > 0;
+    const int inx = more ? b + cs.pop() : i;
+    const Rec nxt = ldc(recs, wave_uniform(inx));
+    float d;
+    if (test(cur, d) && d < best) { best = d; code = rank | i; }
+    if (!more) break;
+    cur = nxt;
+    i = inx;
+  }
+}
+
 template <int U>
 __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, const WaveCone& wc, int w, int K,
-                                             int lane, float& best, int& code, unsigned long long* ex) {
+                                             int lane, float& best, int& code, unsigned long long* ex, int* s_chead) {
   best = FLT_MAX;
   code = kNoHit;
   unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
+#if ART_CONE_DYNAMIC
+  // Waves take 64-collider chunks (global order: spheres, AABBs, OBBs) from the block's counter;
+  // each wave's chunks come in increasing order, so its partial is the first minimum over them.
+  (void)K;
+  const int cs_n = (sc.ns + 63) / 64, ca_n = (sc.na + 63) / 64, co_n = (sc.no + 63) / 64;
+  const int nch = cs_n + ca_n + co_n;
+  for (;;) {
+    int gc = 0;
+    if (lane == 0) gc = atomicAdd(s_chead, 1);
+    gc = __builtin_amdgcn_readfirstlane(__shfl(gc, 0, 64));
+    if (gc >= nch) break;
+    int type, cb, e, gofs;
+    if (gc < cs_n) { type = 0; cb = gc * 64; e = min(cb + 64, sc.ns); gofs = 0; }
+    else if (gc < cs_n + ca_n) { type = 1; cb = (gc - cs_n) * 64; e = min(cb + 64, sc.na); gofs = sc.ns; }
+    else { type = 2; cb = (gc - cs_n - ca_n) * 64; e = min(cb + 64, sc.no); gofs = sc.ns + sc.na; }
+    {
+#else
+  (void)s_chead;
   for (int type = 0; type < 3; ++type) {
     const int n = type == 0 ? sc.ns : (type == 1 ? sc.na : sc.no);
     const int gofs = type == 0 ? 0 : (type == 1 ? sc.ns : sc.ns + sc.na);
     int b, e;
     chunk_of(n, w, K, b, e);
     for (int cb = b; cb < e; cb += 64) {
+#endif
       const int k = cb + lane;
       bool cand = false;
       if (k < e) cand = cone_candidate(wc, sc.cull[gofs + k]);
@@ -338,6 +405,25 @@ __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, c
 #ifdef ART_DIAG_CULL_STATS
       if (lane == 0) { atomicAdd(&g_diag[4], (unsigned)min(64, e - cb)); atomicAdd(&g_diag[5], (unsigned)cs.left); }
 #endif
+#if ART_CONE_MODE == 1
+      // groups of kCullU records per scalar-load wait, then singles
+      if (type == 0) {
+        nearest_group<kCullU>(sc.sph, cb, cs, 0, best, code, [&](const SphereRec& r, float& d) { return sphere_hit_dist(s, r, d); });
+      } else if (type == 1) {
+        nearest_group<kCullU>(sc.aabb, cb, cs, 1 << 28, best, code, [&](const AabbRec& r, float& d) { return aabb_test<false>(s, r, d); });
+      } else {
+        nearest_group<1>(sc.obb, cb, cs, 2 << 28, best, code, [&](const ObbRec& r, float& d) { return obb_test<false>(s, r, stored_q(r), d); });
+      }
+#elif ART_CONE_MODE == 2
+      // one-deep pipeline: the next candidate's record load is issued before this one's test
+      if (type == 0) {
+        nearest_pipe(sc.sph, cb, cs, 0, best, code, [&](const SphereRec& r, float& d) { return sphere_hit_dist(s, r, d); });
+      } else if (type == 1) {
+        nearest_pipe(sc.aabb, cb, cs, 1 << 28, best, code, [&](const AabbRec& r, float& d) { return aabb_test<false>(s, r, d); });
+      } else {
+        nearest_pipe(sc.obb, cb, cs, 2 << 28, best, code, [&](const ObbRec& r, float& d) { return obb_test<false>(s, r, stored_q(r), d); });
+      }
+#else
       if (type == 0) {
         while (cs.left > 0) {
           const int i = cb + cs.pop();
@@ -360,6 +446,7 @@ __device__ __forceinline__ void nearest_cone(const DevScene& sc, const Seg& s, c
           if (obb_test<false>(s, r, stored_q(r), d) && d < best) { best = d; code = (2 << 28) | i; }
         }
       }
+#endif
     }
   }
   exec_add(ex, kExecSphere, 64ull * nt[0]);
@@ -924,6 +1011,9 @@ constexpr uint32_t kPairMuffle = 1u << 16;
 #ifndef ART_VIS_WPE
 #define ART_VIS_WPE 6
 #endif
+#ifndef ART_VIS_PLAIN_FLAG
+#define ART_VIS_PLAIN_FLAG 0
+#endif
 #ifndef ART_VIS_RANGES
 #define ART_VIS_RANGES 8
 #endif
@@ -946,7 +1036,12 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
   const uint32_t p = base + lane;
   PairG& gp = pairs[p < np ? p : base];
   // pairs an earlier range already blocked are skipped (not loaded, and out of the wave's box)
+#if ART_VIS_PLAIN_FLAG
+  // plain load: a stale 0 (another XCD's verdict not yet visible) only repeats work
+  const bool valid = p < np && gp.pad0 == 0u;
+#else
   const bool valid = p < np && __hip_atomic_load(&gp.pad0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+#endif
   if (!__any(valid)) return;
   Seg s;
   float maxd = 0.0f;
@@ -1026,6 +1121,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   __shared__ float s_dist[K][64];
   __shared__ float s_best[K][64];  // running per-lane best of each wave (front-to-back pruning)
   (void)s_best;
+  __shared__ int s_chead;  // next nearest-hit chunk of the block (dynamic cone sweep)
   __shared__ int s_code[K][64];
   __shared__ short s_pairof[kMaxQueries][64];
   __shared__ uint8_t s_res[kMaxQueries * 64];
@@ -1082,6 +1178,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
       }
     }
   }
+  if (threadIdx.x == 0) s_chead = 0;
   __syncthreads();
 
   const vec3 O = load3(origins, fan);
@@ -1102,7 +1199,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #if ART_FAST_SORTED_NEAREST
       nearest_sorted<K>(sc, s, wc, w, lane, alive, s_best, best, code, fp.exec);
 #else
-      nearest_cone<U>(sc, s, wc, w, K, lane, best, code, fp.exec);
+      nearest_cone<U>(sc, s, wc, w, K, lane, best, code, fp.exec, &s_chead);
 #endif
     } else if (MULTI) {
       nearest_chunk<U>(sc, s, w, K, best, code);
