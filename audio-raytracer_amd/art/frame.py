@@ -56,9 +56,9 @@ class Scene:
 @dataclass
 class DspSettings:
     """AudioSpatializerSettings fields used by the DSP-parameter stage (baked curves are inputs)."""
-    reverb_dry_level: tuple = (0.0, -2000.0)          # AudioSpatializerSettings.cs:337
-    reverb_dry_boost: tuple = (1.0, 3.0)              # :339
-    muffle_cutoff: tuple = (75.0, 8000.0)             # :335
+    reverb_dry_level: tuple = (0.0, -2000.0)          # AudioSpatializerSettings.cs:69
+    reverb_dry_boost: tuple = (1.0, 3.0)              # :71
+    muffle_cutoff: tuple = (75.0, 8000.0)             # :67
     reverb_volume_curve: np.ndarray = None            # float32 [n]
     reverb_volume_length: float = 1.0
     muffle_curve: np.ndarray = None

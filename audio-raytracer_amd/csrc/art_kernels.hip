@@ -4,8 +4,8 @@
 //   raytrace_kernel  AudioRaytracerJobBatched.Execute   (Jobs/AudioRaytracerJobBatched.cs:61-215)
 //   permeate_kernel  AudioPermeationJobBatched.Execute  (Jobs/AudioPermeationJobBatched.cs:34-91)
 //   reduce_kernel    ProcessAudioDataJob.Execute        (Jobs/ProcessAudioDataJob.cs:32-76)
-//                    + DSP parameters                   (AudioSpatializer.cs:58, ReverbDSP.cs:105,
-//                                                        MuffleDSP.cs:140-160)
+//                    + DSP parameters                   (AudioSpatializer.cs:58, ReverbDSP.cs:12-13,
+//                                                        MuffleDSP.cs:22-26, :38-42)
 //
 // Mapping: one lane per (fan, ray). All lanes of a wave sweep the collider arrays in the same
 // order, so every collider record is wave-uniform and is fetched with scalar loads into SGPRs.

@@ -84,10 +84,10 @@ typedef struct {
 
 /* Per-target DSP parameters derived from the settings (config 5's "reverb DSP" pass):
  *   dry_level     = lerp(DryLevel.min, DryLevel.max, ReverbStrength)      AudioSpatializer.cs:58
- *   dry_boost     = lerp(DryBoost.min, DryBoost.max, VolCurve(ReverbVolume))  ReverbDSP.cs:105-106
- *   muffle_cutoff = lerp(Cutoff.max, Cutoff.min, MuffleCurve(MuffleStrength))  MuffleDSP.cs:142-144
- *   muffle_alpha  = dt / (rc + dt), rc = 1/(cutoff*2pi), dt = 1/sampleRate  MuffleDSP.cs:158-160
- *   muffle_active = MuffleStrength > 0  (MuffleDSP.cs:140); cutoff/alpha are 0 when inactive. */
+ *   dry_boost     = lerp(DryBoost.min, DryBoost.max, VolCurve(ReverbVolume))  ReverbDSP.cs:12-13
+ *   muffle_cutoff = lerp(Cutoff.max, Cutoff.min, MuffleCurve(MuffleStrength))  MuffleDSP.cs:24-26
+ *   muffle_alpha  = dt / (rc + dt), rc = 1/(cutoff*2pi), dt = 1/sampleRate  MuffleDSP.cs:40-42
+ *   muffle_active = MuffleStrength > 0  (MuffleDSP.cs:22); cutoff/alpha are 0 when inactive. */
 typedef struct {
     float dry_level;
     float dry_boost;
@@ -97,7 +97,7 @@ typedef struct {
     int32_t reserved;
 } art_dsp_params; /* 24 B */
 
-/* A baked NativeSampledAnimationCurve (DataTypes/NativeSampledAnimationCurve.cs:187-192). */
+/* A baked NativeSampledAnimationCurve (DataTypes/NativeSampledAnimationCurve.cs:22-29; evaluated as :64-89). */
 typedef struct {
     const float* baked;   /* float[sample_count] */
     int32_t sample_count; /* >= 2 */

@@ -614,8 +614,8 @@ static void process_audio_data(const art_frame_desc* d, const art_fan* fan, int 
 }
 
 /* ========================================================================================
- * 6. DSP parameters (config 5): AudioSpatializer.cs:58, ReverbDSP.cs:105-106, MuffleDSP.cs:140-160,
- *    NativeSampledAnimationCurve.cs:227-252
+ * 6. DSP parameters (config 5): AudioSpatializer.cs:58, ReverbDSP.cs:12-13, MuffleDSP.cs:22-26 and :38-42,
+ *    NativeSampledAnimationCurve.cs:64-89
  * ====================================================================================== */
 static float curve_evaluate(const art_curve* c, float time)
 {
@@ -629,7 +629,7 @@ static float curve_evaluate(const art_curve* c, float time)
 
 static void dsp_params(const art_dsp_desc* dsp, const art_target_settings* s, art_dsp_params* out)
 {
-    const float DOUBLE_PI = 2.0f * 3.14159265f; /* MuffleDSP.cs:153, math.PI (float) */
+    const float DOUBLE_PI = 2.0f * 3.14159265f; /* MuffleDSP.cs:35, math.PI (float) */
     out->dry_level = ulerp(dsp->reverb_dry_level_min, dsp->reverb_dry_level_max, s->reverb_strength);
     float t = curve_evaluate(&dsp->reverb_volume_curve, s->reverb_volume);
     out->dry_boost = ulerp(dsp->reverb_dry_boost_min, dsp->reverb_dry_boost_max, t);
