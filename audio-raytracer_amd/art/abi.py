@@ -109,6 +109,48 @@ class art_exec_counts(C.Structure):
                 ("cull_cone", C.c_uint64), ("launches", C.c_uint64)]
 
 
+# include/art_dsp.h
+class art_stereo(C.Structure):
+    _fields_ = [("left", C.c_float), ("right", C.c_float)]
+
+
+class art_dsp_state(C.Structure):
+    _fields_ = [("previous_muffle", art_stereo), ("previous_lp", art_stereo), ("previous_hp", art_stereo),
+                ("previous_input", art_stereo)]
+
+
+class art_spatializer_settings(C.Structure):
+    _fields_ = [("pan_strength", C.c_float), ("rear_attenuation_strength", C.c_float),
+                ("distance_based_panning", C.c_int32), ("max_pan_distance", C.c_float),
+                ("distance_based_rear_attenuation", C.c_int32), ("max_rear_attenuation_distance", C.c_float),
+                ("max_elevation_effect_distance", C.c_float),
+                ("low_pass_cutoff_min", C.c_float), ("low_pass_cutoff_max", C.c_float), ("low_pass_volume", C.c_float),
+                ("high_pass_cutoff_min", C.c_float), ("high_pass_cutoff_max", C.c_float), ("high_pass_volume", C.c_float),
+                ("muffle_curve", art_curve), ("muffle_cutoff_min", C.c_float), ("muffle_cutoff_max", C.c_float),
+                ("reverb_volume_curve", art_curve), ("reverb_dry_boost_min", C.c_float),
+                ("reverb_dry_boost_max", C.c_float)]
+
+
+class art_audio_source(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_float)), ("frames", C.c_int32), ("channels", C.c_int32),
+                ("muffle_strength", C.c_float), ("reverb_volume", C.c_float), ("local_dir", C.c_float * 3),
+                ("listener_distance", C.c_float), ("volume_multiplier", C.c_float),
+                ("state", C.POINTER(art_dsp_state))]
+
+
+class art_dsp_source_params(C.Structure):
+    _fields_ = [("muffle_alpha", C.c_float), ("dry_boost", C.c_float), ("gain_left", C.c_float),
+                ("gain_right", C.c_float), ("filter_alpha", C.c_float), ("volume", C.c_float),
+                ("flags", C.c_int32), ("reserved", C.c_int32)]
+
+
+DSP_STATE = np.dtype([("previous_muffle", np.float32, 2), ("previous_lp", np.float32, 2),
+                      ("previous_hp", np.float32, 2), ("previous_input", np.float32, 2)])
+DSP_SOURCE_PARAMS = np.dtype([("muffle_alpha", np.float32), ("dry_boost", np.float32), ("gain_left", np.float32),
+                       ("gain_right", np.float32), ("filter_alpha", np.float32), ("volume", np.float32),
+                       ("flags", np.int32), ("reserved", np.int32)])
+
+
 class art_synth_config(C.Structure):
     _fields_ = [("sphere_count", C.c_int32), ("aabb_count", C.c_int32), ("obb_count", C.c_int32),
                 ("target_count", C.c_int32), ("fan_count", C.c_int32), ("ray_count", C.c_int32),
@@ -135,6 +177,11 @@ SIGNATURES = {
     "art_count_device": (I32, [VP, VP, I32, VP, U32, VP, C.POINTER(art_test_counts)]),
     "art_kernel_timing": (I32, [VP, C.POINTER(art_kernel_times)]),
     "art_executed_counts": (I32, [VP, C.POINTER(art_exec_counts)]),
+    # art_dsp.h
+    "art_dsp_process": (I32, [VP, C.POINTER(art_spatializer_settings), C.POINTER(art_audio_source), I32, I32]),
+    "art_dsp_source_params_get": (I32, [C.POINTER(art_spatializer_settings), C.POINTER(art_audio_source), I32,
+                                        C.POINTER(art_dsp_source_params)]),
+    "art_dsp_process_device": (I32, [VP, VP, VP, VP, I32, I32, VP]),
     "art_device_count": (I32, []),
     # art_synth.h
     "art_synth_scene": (I32, [C.POINTER(art_synth_config), VP, VP, VP, VP, VP, VP]),

@@ -21,6 +21,7 @@
 
 #include "../../include/art.h"
 #include "../../include/art_device.h"
+#include "../../include/art_dsp.h"
 #include "art_internal.hpp"
 #include "art_wavefront.hpp"
 #include "unity_math.hpp"
@@ -101,6 +102,7 @@ struct Device {
   DevBuf work;  // ticket counters of the persistent raytrace kernel (self-rearming, zeroed once)
   DevBuf exec;  // executed-work counters (ART_CTX_COUNT_EXECUTED)
   DevBuf pairs; // global visibility pairs of the split raytrace path
+  DevBuf dsp;   // per-sample DSP batch (art_dsp_process): samples, offsets, frames, params, states
   uint64_t exec_launches = 0;
   DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
   int wf_blocks = 0;
@@ -118,6 +120,7 @@ struct art_ctx {
   std::string err;
   uint32_t flags = 0;
   HostBuf h_in, h_block;
+  HostBuf h_dsp;                 // staging of art_dsp_process
   Frame fr;                      // frame of the bound scene / last schedule
   // in-flight frame
   bool inflight = false;
@@ -590,7 +593,7 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
-    dv.work.release(); dv.exec.release(); dv.pairs.release();
+    dv.work.release(); dv.exec.release(); dv.pairs.release(); dv.dsp.release();
     dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
@@ -598,6 +601,7 @@ ART_API void art_destroy(art_ctx* c) {
   }
   c->h_in.release();
   c->h_block.release();
+  c->h_dsp.release();
   delete c;
 }
 
@@ -850,6 +854,83 @@ ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {
     dv.ev_used.clear();
     out->launches += frames;
   }
+  return ART_OK;
+}
+
+// ---- per-sample spatializer DSP (include/art_dsp.h) -------------------------------------
+ART_API int art_dsp_source_params_get(const art_spatializer_settings* settings, const art_audio_source* source,
+                                      int32_t sample_rate, art_dsp_source_params* out) {
+  if (!settings || !source || !out || sample_rate <= 0) return ART_E_INVALID;
+  return dsp_source_params(*settings, *source, sample_rate, *out);
+}
+
+ART_API int art_dsp_process(art_ctx* c, const art_spatializer_settings* settings, art_audio_source* sources,
+                            int32_t count, int32_t sample_rate) {
+  if (!c) return ART_E_INVALID;
+  if (!settings || count < 0 || (count > 0 && !sources) || sample_rate <= 0) return fail(c, ART_E_INVALID, "invalid argument");
+  if (c->inflight) return fail(c, ART_E_STATE, "a frame is in flight");
+  // host: per-buffer scalars; stereo sources with samples go to the device
+  std::vector<int> idx;
+  std::vector<art_dsp_source_params> params;
+  std::vector<long long> offs;
+  std::vector<int> frames;
+  long long total = 0;  // floats, each source 16-B aligned
+  for (int32_t k = 0; k < count; ++k) {
+    const art_audio_source& a = sources[k];
+    if (a.frames < 0 || (a.frames > 0 && !a.data) || !a.state) return fail(c, ART_E_INVALID, "invalid source %d", k);
+    if (a.channels != 2 || a.frames == 0) continue;  // left as is (AudioSpatializer.cs:72)
+    art_dsp_source_params p;
+    if (dsp_source_params(*settings, a, sample_rate, p) != ART_OK) return fail(c, ART_E_INVALID, "invalid curve");
+    idx.push_back(k);
+    params.push_back(p);
+    offs.push_back(total);
+    frames.push_back(a.frames);
+    total += ((long long)a.frames * 2 + 3) & ~3LL;
+  }
+  const size_t n = idx.size();
+  if (n == 0) return ART_OK;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_data = 0, o_offs = al(o_data + (size_t)total * 4), o_frames = al(o_offs + n * 8),
+               o_params = al(o_frames + n * 4), o_state = al(o_params + n * sizeof(art_dsp_source_params)),
+               bytes = al(o_state + n * sizeof(art_dsp_state));
+  Device& dv = c->devs[0];
+  HIP_TRY(c, hipSetDevice(dv.id));
+  if (!c->h_dsp.reserve(bytes) || !dv.dsp.reserve(bytes)) return fail(c, ART_E_NOMEM, "allocation failed");
+  uint8_t* h = static_cast<uint8_t*>(c->h_dsp.p);
+  for (size_t j = 0; j < n; ++j) {
+    const art_audio_source& a = sources[idx[j]];
+    std::memcpy(h + o_data + offs[j] * 4, a.data, (size_t)a.frames * 8);
+    std::memcpy(h + o_state + j * sizeof(art_dsp_state), a.state, sizeof(art_dsp_state));
+  }
+  std::memcpy(h + o_offs, offs.data(), n * 8);
+  std::memcpy(h + o_frames, frames.data(), n * 4);
+  std::memcpy(h + o_params, params.data(), n * sizeof(art_dsp_source_params));
+  uint8_t* d = static_cast<uint8_t*>(dv.dsp.p);
+  HIP_TRY(c, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, dv.stream));
+  launch_dsp(reinterpret_cast<float*>(d + o_data), reinterpret_cast<const long long*>(d + o_offs),
+             reinterpret_cast<const int*>(d + o_frames), 0, reinterpret_cast<const art_dsp_source_params*>(d + o_params),
+             reinterpret_cast<art_dsp_state*>(d + o_state), (int)n, dv.stream);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpyAsync(h + o_data, d + o_data, (size_t)total * 4, hipMemcpyDeviceToHost, dv.stream));
+  HIP_TRY(c, hipMemcpyAsync(h + o_state, d + o_state, n * sizeof(art_dsp_state), hipMemcpyDeviceToHost, dv.stream));
+  HIP_TRY(c, hipStreamSynchronize(dv.stream));
+  for (size_t j = 0; j < n; ++j) {
+    art_audio_source& a = sources[idx[j]];
+    std::memcpy(a.data, h + o_data + offs[j] * 4, (size_t)a.frames * 8);
+    std::memcpy(a.state, h + o_state + j * sizeof(art_dsp_state), sizeof(art_dsp_state));
+  }
+  return ART_OK;
+}
+
+ART_API int art_dsp_process_device(art_ctx* c, float* d_data, const art_dsp_source_params* d_params,
+                                   art_dsp_state* d_state, int32_t count, int32_t frames, void* stream) {
+  if (!c) return ART_E_INVALID;
+  if (count < 0 || frames < 0 || (count > 0 && (!d_data || !d_params || !d_state))) return fail(c, ART_E_INVALID, "invalid argument");
+  if (count == 0 || frames == 0) return ART_OK;
+  Device& dv = c->devs[0];
+  HIP_TRY(c, hipSetDevice(dv.id));
+  launch_dsp(d_data, nullptr, nullptr, frames, d_params, d_state, count, static_cast<hipStream_t>(stream));
+  HIP_TRY(c, hipGetLastError());
   return ART_OK;
 }
 

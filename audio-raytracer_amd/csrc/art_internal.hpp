@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/art.h"
+#include "../../include/art_dsp.h"
 
 namespace art {
 
@@ -83,6 +84,12 @@ struct SortBufs {
   void* temp; size_t temp_bytes;
   SphereRec* sph_s; AabbRec* aabb_s; ObbRec* obb_s; CullRec* cull_s; CullRec* chunks;
 };
+// per-sample spatializer DSP (art_dsp.hip)
+int dsp_source_params(const art_spatializer_settings& st, const art_audio_source& src, int sample_rate,
+                      art_dsp_source_params& p);
+void launch_dsp(float* data, const long long* offsets, const int* frames_of, int frames_all,
+                const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st);
+
 size_t sort_scene_temp_bytes(int n);
 bool fast_uses_sorted_scene();  // whether the throughput kernel reads the sorted copies
 int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);

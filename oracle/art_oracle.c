@@ -619,12 +619,12 @@ static void process_audio_data(const art_frame_desc* d, const art_fan* fan, int 
  * ====================================================================================== */
 static float curve_evaluate(const art_curve* c, float time)
 {
-    float percent = time / c->length;                                            /* :237 */
+    float percent = time / c->length;                                            /* :74 */
     int n = c->sample_count;
-    float curvePercentage = umax(0.0f, umin((float)(n - 1), percent * (float)(n - 1))); /* :246 clamp */
-    int floorIndex = (int)floorf(curvePercentage);
+    float curvePercentage = umax(0.0f, umin((float)(n - 1), percent * (float)(n - 1))); /* :83 clamp */
+    int floorIndex = (int)floorf(curvePercentage);                               /* :85-86 */
     int ceilIndex = (int)ceilf(curvePercentage);
-    return ulerp(c->baked[floorIndex], c->baked[ceilIndex], curvePercentage - (float)floorIndex); /* :251 */
+    return ulerp(c->baked[floorIndex], c->baked[ceilIndex], curvePercentage - (float)floorIndex); /* :88 */
 }
 
 static void dsp_params(const art_dsp_desc* dsp, const art_target_settings* s, art_dsp_params* out)
@@ -793,4 +793,125 @@ void or_quat_mul_vec(const float q[4], const float v[3], float out[3])
     f4 qq = { q[0], q[1], q[2], q[3] };
     f3 r = qmul(qq, v3(v[0], v[1], v[2]));
     out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+
+/* ========================================================================================
+ * 8. Per-sample spatializer DSP (SURVEY.md §8 f rank 1): AudioSpatializer.OnAudioFilterRead
+ *    (Audio/AudioTarget/AudioSpatializer.cs:70-87) = MuffleDSP.Process (MuffleDSP.cs:13-32),
+ *    ReverbDSP.Process (ReverbDSP.cs:10-24), BinauralDSP.Process (BinauralDSP.cs:15-82), volume.
+ *    Literal: per-sample quantities are recomputed inside the loops as the C# does.
+ *    math.sin/cos/atan2 are the host libm (Burst's are not reproducible here: parity for those
+ *    per-buffer scalars is unpinned by the reference).
+ * ====================================================================================== */
+#define OR_TODEGREES 57.29578f      /* Unity.Mathematics math.degrees factor */
+#define OR_TORADIANS 0.0174532924f  /* math.radians factor */
+
+static float or_lowpass(float input, float* prev, float cutoff, float sampleRate) /* MuffleDSP.cs:38-45, BinauralDSP.cs:87-94 */
+{
+    const float DOUBLE_PI = 2.0f * 3.14159265f;
+    float rc = 1.0f / (cutoff * DOUBLE_PI);
+    float dt = 1.0f / sampleRate;
+    float alpha = dt / (rc + dt);
+    *prev += alpha * (input - *prev);
+    return *prev;
+}
+
+static float or_highpass(float input, float* prevIn, float* prevOut, float cutoff, float sampleRate) /* BinauralDSP.cs:97-106 */
+{
+    const float DOUBLE_PI = 2.0f * 3.14159265f;
+    float rc = 1.0f / (cutoff * DOUBLE_PI);
+    float dt = 1.0f / sampleRate;
+    float alpha = rc / (rc + dt);
+    float output = alpha * (*prevOut + input - *prevIn);
+    *prevIn = input;
+    *prevOut = output;
+    return output;
+}
+
+static float uclamp(float x, float a, float b) { return umax(a, umin(b, x)); }
+
+static void or_dsp_source(const art_spatializer_settings* st, art_audio_source* src, int sampleRate)
+{
+    if (src->channels != 2) return;                                  /* AudioSpatializer.cs:72 */
+    float* data = src->data;
+    const int len = src->frames * 2;
+    art_dsp_state* S = src->state;
+    const float sr = (float)sampleRate;
+    /* MuffleDSP.Process :13-32 */
+    for (int i = 0; i < len; i += 2) {
+        float l = data[i], r = data[i + 1];
+        if (src->muffle_strength > 0.0f) {                           /* :22 */
+            float muffle = curve_evaluate(&st->muffle_curve, src->muffle_strength);       /* :24 */
+            float cutoff = ulerp(st->muffle_cutoff_max, st->muffle_cutoff_min, muffle);   /* :26 */
+            data[i] = or_lowpass(l, &S->previous_muffle.left, cutoff, sr);                /* :28 */
+            data[i + 1] = or_lowpass(r, &S->previous_muffle.right, cutoff, sr);           /* :29 */
+        }
+    }
+    /* ReverbDSP.Process :10-24 */
+    {
+        float t = curve_evaluate(&st->reverb_volume_curve, src->reverb_volume);           /* :12 */
+        float dryBoost = ulerp(st->reverb_dry_boost_min, st->reverb_dry_boost_max, t);    /* :13 */
+        for (int i = 0; i < len; i += 2) {
+            float l = data[i], r = data[i + 1];
+            data[i] = l * dryBoost;
+            data[i + 1] = r * dryBoost;
+        }
+    }
+    /* BinauralDSP.Process :15-82 */
+    {
+        const float* ld = src->local_dir;
+        float dist = src->listener_distance;
+        float azimuth = atan2f(ld[0], ld[2]) * OR_TODEGREES;                              /* :17 */
+        float effectivePanStrength = st->pan_strength;                                    /* :19 */
+        if (st->distance_based_panning) {                                                 /* :20-24 */
+            float distanceFactor = usaturate(dist / st->max_pan_distance);
+            effectivePanStrength *= distanceFactor;
+        }
+        float pan = sinf(azimuth * OR_TORADIANS) * effectivePanStrength;                  /* :27 */
+        float leftGain = sqrtf(0.5f * (1.0f - pan));                                      /* :28 */
+        float rightGain = sqrtf(0.5f * (1.0f + pan));                                     /* :29 */
+        float frontFactor = umax(0.0f, cosf(azimuth * OR_TORADIANS));                     /* :32 */
+        float rearAtten = ulerp(1.0f - st->rear_attenuation_strength, 1.0f, frontFactor); /* :33 */
+        if (st->distance_based_rear_attenuation) {                                        /* :35-40 */
+            float distanceFactor = usaturate(1.0f - (dist / st->max_rear_attenuation_distance));
+            rearAtten = uclamp(rearAtten * distanceFactor, 1.0f - st->rear_attenuation_strength, 1.0f);
+        }
+        float elev = ld[1] <= 0.0f ? ulerp(1.0f, st->low_pass_volume, usaturate(-ld[1]))  /* :43-45 */
+                                   : ulerp(1.0f, st->high_pass_volume, usaturate(ld[1]));
+        float modL = leftGain * rearAtten * elev;                                         /* :48-50 */
+        float modR = rightGain * rearAtten * elev;
+        for (int i = 0; i < len; i += 2) {                                                /* :54-81 */
+            float pl = data[i] * modL;
+            float pr = data[i + 1] * modR;
+            if (ld[1] <= 0.0f) {
+                float lowPassCutoff = ulerp(st->low_pass_cutoff_min, st->low_pass_cutoff_max, usaturate(-ld[1])) *
+                                      (1.0f - 0.5f * usaturate(dist / st->max_elevation_effect_distance)); /* :65 */
+                pl = or_lowpass(pl, &S->previous_lp.left, lowPassCutoff, sr);
+                pr = or_lowpass(pr, &S->previous_lp.right, lowPassCutoff, sr);
+            } else {
+                float highPassCutoff = ulerp(st->high_pass_cutoff_min, st->high_pass_cutoff_max, usaturate(ld[1])) *
+                                       (1.0f + 0.5f * usaturate(dist / st->max_elevation_effect_distance)); /* :73 */
+                pl = or_highpass(pl, &S->previous_input.left, &S->previous_hp.left, highPassCutoff, sr);
+                pr = or_highpass(pr, &S->previous_input.right, &S->previous_hp.right, highPassCutoff, sr);
+            }
+            data[i] = pl;
+            data[i + 1] = pr;
+        }
+    }
+    /* volume multiplier, AudioSpatializer.cs:79-86 */
+    for (int i = 0; i < len; i += 2) {
+        float l = data[i], r = data[i + 1];
+        data[i] = l * src->volume_multiplier;
+        data[i + 1] = r * src->volume_multiplier;
+    }
+}
+
+int or_dsp_process(const art_spatializer_settings* settings, art_audio_source* sources, int32_t count, int32_t sample_rate)
+{
+    if (!settings || (count > 0 && !sources) || count < 0) return ART_E_INVALID;
+    for (int32_t k = 0; k < count; ++k) {
+        if (sources[k].frames < 0 || (sources[k].frames > 0 && !sources[k].data) || !sources[k].state) return ART_E_INVALID;
+        or_dsp_source(settings, &sources[k], sample_rate);
+    }
+    return ART_OK;
 }

@@ -17,6 +17,7 @@
 
 #include <stdint.h>
 #include "../include/art.h"
+#include "../include/art_dsp.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -36,6 +37,10 @@ void or_fibonacci_directions(int32_t count, art_half3* out);
  * Returns 0 or a negative ART_E_* code. */
 int or_run_frame(const art_frame_desc* desc, const art_fan* fans, int32_t fan_count,
                  int32_t threads, art_test_counts* counts);
+
+/* Per-sample spatializer DSP (AudioSpatializer.OnAudioFilterRead, SURVEY.md §8 f rank 1). */
+int or_dsp_process(const art_spatializer_settings* settings, art_audio_source* sources, int32_t count,
+                   int32_t sample_rate);
 
 /* Individual primitives, exposed for known-answer tests. */
 int or_ray_intersects_aabb(const float o[3], const float d[3], const float c[3], const float h[3], float* dist);

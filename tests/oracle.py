@@ -48,6 +48,9 @@ def load():
     lib.or_ray_intersects_sphere.argtypes = [f3, f3, f3, C.c_float, C.POINTER(C.c_float)]
     lib.or_ray_intersects_obb.restype = C.c_int
     lib.or_ray_intersects_obb.argtypes = [f3, f3, f3, f3, f4, C.POINTER(C.c_float)]
+    lib.or_dsp_process.restype = C.c_int
+    lib.or_dsp_process.argtypes = [C.POINTER(abi.art_spatializer_settings), C.POINTER(abi.art_audio_source), C.c_int32,
+                                   C.c_int32]
     lib.or_half_quaternion_value.argtypes = [C.c_uint16, C.c_uint16, C.c_uint16, f4]
     lib.or_quat_inverse.argtypes = [f4, f4]
     lib.or_quat_mul_vec.argtypes = [f4, f3, f3]
@@ -77,3 +80,13 @@ def f32tof16(x: float) -> int:
 
 def f16tof32(h: int) -> float:
     return float(load().or_f16tof32(h))
+
+
+def dsp_process(settings, sources, sample_rate: int = 48000):
+    """Oracle AudioSpatializer.OnAudioFilterRead (art_oracle.c §8) over art.dsp.AudioSource objects."""
+    from art import dsp
+    lib = load()
+    st = settings.to_c()
+    arr = dsp.sources_to_c(sources)
+    rc = lib.or_dsp_process(C.byref(st), arr, len(sources), sample_rate)
+    assert rc == 0, rc
