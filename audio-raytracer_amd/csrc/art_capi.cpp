@@ -889,6 +889,25 @@ ART_API int art_dsp_process(art_ctx* c, const art_spatializer_settings* settings
   }
   const size_t n = idx.size();
   if (n == 0) return ART_OK;
+  {  // group sources by filter class (muffle x low/high pass) so a wave's chains run one code path
+    std::vector<size_t> ord(n);
+    for (size_t j = 0; j < n; ++j) ord[j] = j;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return (params[a].flags & 3) < (params[b].flags & 3); });
+    std::vector<int> idx2(n);
+    std::vector<art_dsp_source_params> params2(n);
+    std::vector<int> frames2(n);
+    total = 0;
+    for (size_t j = 0; j < n; ++j) {
+      idx2[j] = idx[ord[j]];
+      params2[j] = params[ord[j]];
+      frames2[j] = frames[ord[j]];
+      offs[j] = total;
+      total += ((long long)frames2[j] * 2 + 3) & ~3LL;
+    }
+    idx.swap(idx2);
+    params.swap(params2);
+    frames.swap(frames2);
+  }
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t o_data = 0, o_offs = al(o_data + (size_t)total * 4), o_frames = al(o_offs + n * 8),
                o_params = al(o_frames + n * 4), o_state = al(o_params + n * sizeof(art_dsp_source_params)),
@@ -907,7 +926,7 @@ ART_API int art_dsp_process(art_ctx* c, const art_spatializer_settings* settings
   std::memcpy(h + o_params, params.data(), n * sizeof(art_dsp_source_params));
   uint8_t* d = static_cast<uint8_t*>(dv.dsp.p);
   HIP_TRY(c, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, dv.stream));
-  launch_dsp(reinterpret_cast<float*>(d + o_data), reinterpret_cast<const long long*>(d + o_offs),
+  launch_dsp(reinterpret_cast<float*>(d + o_data), (unsigned long long)total * 4, reinterpret_cast<const long long*>(d + o_offs),
              reinterpret_cast<const int*>(d + o_frames), 0, reinterpret_cast<const art_dsp_source_params*>(d + o_params),
              reinterpret_cast<art_dsp_state*>(d + o_state), (int)n, dv.stream);
   HIP_TRY(c, hipGetLastError());
@@ -929,7 +948,8 @@ ART_API int art_dsp_process_device(art_ctx* c, float* d_data, const art_dsp_sour
   if (count == 0 || frames == 0) return ART_OK;
   Device& dv = c->devs[0];
   HIP_TRY(c, hipSetDevice(dv.id));
-  launch_dsp(d_data, nullptr, nullptr, frames, d_params, d_state, count, static_cast<hipStream_t>(stream));
+  launch_dsp(d_data, (unsigned long long)count * (unsigned long long)frames * 8ull, nullptr, nullptr, frames, d_params,
+             d_state, count, static_cast<hipStream_t>(stream));
   HIP_TRY(c, hipGetLastError());
   return ART_OK;
 }

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -119,6 +121,177 @@ __global__ __launch_bounds__(kDspBlock) void dsp_kernel(float* __restrict__ data
   state[s] = st;
 }
 
+// ---- tiled kernel: one lane per (source, channel), tiles transposed through LDS -------------
+//
+// The recurrences are serial over frames, so a lane owns one channel chain. The buffers are
+// [source][frame][L,R]: a wave reads a tile of kTF frames of its kTS sources with coalesced 8-B
+// loads (one instruction covers 256 contiguous bytes of two sources), transposes it through LDS,
+// runs the chains out of LDS, and writes the tile back the same way. The next tile's loads are in
+// flight while the current one is processed.
+#ifndef ART_DSP_TF
+#define ART_DSP_TF 64
+#endif
+constexpr int kTS = 32;              // sources per wave (lane = 2 * source + channel)
+constexpr int kTF = ART_DSP_TF;      // frames per tile (64; 32 measured slower on large batches)
+constexpr int kSPI = 64 / kTF;       // sources covered by one load instruction
+static_assert(kTF == 32 || kTF == 64, "tile width");
+constexpr int kRow = 2 * kTF + 2;    // floats per LDS row: bank (2 s + c + 2 n) mod 32 is distinct per half-wave
+constexpr int kLoads = kTS * kTF / 64;  // float2 loads per lane per tile
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+struct Chain {
+  float pm, pl, ph, pi;  // previousMuffle, previousLP, previousHP, previousInput of this channel
+};
+
+// M: bit 0 muffle, bit 1 low pass (fixed for the wave); M == 4: per-lane selects (exact: every
+// selected value is computed with the same operations as in the fixed variants).
+template <int M>
+__device__ __forceinline__ float step(float x, const art_dsp_source_params& p, float gain, bool mf, bool lp,
+                                      Chain& c) {
+  if constexpr (M == 4) {
+    const float m = c.pm + p.muffle_alpha * (x - c.pm);
+    x = mf ? m : x;
+    c.pm = mf ? m : c.pm;
+  } else if constexpr (M & 1) {
+    c.pm = c.pm + p.muffle_alpha * (x - c.pm);  // MuffleDSP.LowPass :43-44
+    x = c.pm;
+  }
+  x = x * p.dry_boost;  // ReverbDSP :21-22
+  x = x * gain;         // BinauralDSP :59-60
+  if constexpr (M == 4) {
+    const float l = c.pl + p.filter_alpha * (x - c.pl);
+    const float h = p.filter_alpha * (c.ph + x - c.pi);
+    c.pl = lp ? l : c.pl;
+    c.ph = lp ? c.ph : h;
+    c.pi = lp ? c.pi : x;
+    x = lp ? l : h;
+  } else if constexpr (M & 2) {
+    c.pl = c.pl + p.filter_alpha * (x - c.pl);  // LowPass :92-93
+    x = c.pl;
+  } else {
+    const float h = p.filter_alpha * (c.ph + x - c.pi);  // HighPass :102-105
+    c.pi = x;
+    c.ph = h;
+    x = h;
+  }
+  return x * p.volume;  // AudioSpatializer.cs:84-85
+}
+
+template <int M>
+__device__ __forceinline__ void run_tile(float* row, int n, const art_dsp_source_params& p, float gain, bool mf,
+                                         bool lp, Chain& c) {
+  if (n == kTF) {
+    float x[kTF];
+#pragma unroll
+    for (int k = 0; k < kTF; ++k) x[k] = row[2 * k];
+#pragma unroll
+    for (int k = 0; k < kTF; ++k) x[k] = step<M>(x[k], p, gain, mf, lp, c);
+#pragma unroll
+    for (int k = 0; k < kTF; ++k) row[2 * k] = x[k];
+  } else {
+    for (int k = 0; k < n; ++k) row[2 * k] = step<M>(row[2 * k], p, gain, mf, lp, c);
+  }
+}
+
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(64) void dsp_tiled_kernel(float* __restrict__ data, const long long* __restrict__ offsets,
+                                                       const int* __restrict__ frames_of, int frames_all,
+                                                       const art_dsp_source_params* __restrict__ params,
+                                                       art_dsp_state* __restrict__ state, int count,
+                                                       uint32_t nbytes) {
+  __shared__ float tile[kTS * kRow];
+  const int lane = threadIdx.x;
+  const int s0 = blockIdx.x * kTS;
+  const int sl = lane >> 1, ch = lane & 1;
+  const int s = s0 + sl;
+  art_dsp_source_params p{};
+  int my_frames = 0;
+  Chain c{};
+  if (s < count) {
+    p = params[s];
+    if (!(p.flags & 4)) {
+      my_frames = frames_of ? frames_of[s] : frames_all;
+      const float* sv = reinterpret_cast<const float*>(state + s);
+      c.pm = sv[0 + ch]; c.pl = sv[2 + ch]; c.ph = sv[4 + ch]; c.pi = sv[6 + ch];
+    }
+  }
+  const bool mf = (p.flags & 1) != 0, lp = (p.flags & 2) != 0;
+  const float gain = ch ? p.gain_right : p.gain_left;
+  const int cls = my_frames > 0 ? (p.flags & 3) : -1;
+  const int fmax = wave_max_i(my_frames);
+  if (fmax == 0) return;
+  const uint64_t b0 = __ballot(cls == 0), b1 = __ballot(cls == 1), b2 = __ballot(cls == 2), b3 = __ballot(cls == 3);
+  const bool generic = (b0 != 0) + (b1 != 0) + (b2 != 0) + (b3 != 0) >= 3;
+
+  // loader view: item i of this lane is frame lane % kTF of local source kSPI * i + lane / kTF.
+  // Buffer loads/stores with the hardware range check: an item past its source's frames gets the
+  // offset nbytes (loads 0, store dropped), so the transfers are branch-free and the wait for the
+  // next tile's loads does not also wait for this tile's stores.
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(data, 0, (int)nbytes, 0x00020000);
+  const int lf = lane & (kTF - 1);
+  // per-source frames and byte offset come from the source's channel-0 lane (no dependent loads)
+  const long long my_off = my_frames > 0 ? (offsets ? offsets[s] : (long long)s * frames_all * 2) : 0;
+  const int my_ob = (int)(uint32_t)(my_off * 4);
+  uint32_t obase[kLoads];
+  int lfr[kLoads];
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) {
+    const int src_lane = 2 * (kSPI * i + lane / kTF);
+    lfr[i] = __shfl(my_frames, src_lane, 64);
+    obase[i] = (uint32_t)__shfl(my_ob, src_lane, 64);
+  }
+  u32x2 pre[kLoads];
+  auto voff = [&](int i, int t) -> uint32_t {
+    const int f = t * kTF + lf;
+    return f < lfr[i] ? obase[i] + (uint32_t)f * 8u : nbytes;
+  };
+  auto load = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) pre[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff(i, t), 0, 0);
+  };
+  const int ntiles = (fmax + kTF - 1) / kTF;
+  float* row = tile + sl * kRow + ch;
+  load(0);
+  // 16 out-of-range stores (dropped by the range check): the loop is then entered with the same
+  // memory-op order as its back edge (loads, then stores), so the wait for the prefetched tile at
+  // the loop head leaves the previous tile's stores in flight (vmcnt(16), not vmcnt(0))
+#pragma unroll
+  for (int i = 0; i < kLoads; ++i) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, rs, nbytes + 16u * i, 0, 0);
+  for (int t = 0; t < ntiles; ++t) {
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i)
+      *reinterpret_cast<u32x2*>(tile + (kSPI * i + lane / kTF) * kRow + 2 * lf) = pre[i];
+    __syncthreads();
+    load(t + 1);  // past the last tile every offset is out of range: loads 0, no branch
+    const int n = min(max(my_frames - t * kTF, 0), kTF);
+    if (generic) {
+      run_tile<4>(row, n, p, gain, mf, lp, c);
+    } else {
+      if (b0 && cls == 0) run_tile<0>(row, n, p, gain, mf, lp, c);
+      if (b1 && cls == 1) run_tile<1>(row, n, p, gain, mf, lp, c);
+      if (b2 && cls == 2) run_tile<2>(row, n, p, gain, mf, lp, c);
+      if (b3 && cls == 3) run_tile<3>(row, n, p, gain, mf, lp, c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) {
+      const u32x2 v = *reinterpret_cast<const u32x2*>(tile + (kSPI * i + lane / kTF) * kRow + 2 * lf);
+      __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff(i, t), 0, 0);
+    }
+    __syncthreads();
+  }
+  if (my_frames > 0) {
+    float* sv = reinterpret_cast<float*>(state + s);
+    sv[0 + ch] = c.pm; sv[2 + ch] = c.pl; sv[4 + ch] = c.ph; sv[6 + ch] = c.pi;
+  }
+}
+
 }  // namespace
 
 // Per-buffer scalars (everything the C# recomputes per sample is constant over the buffer).
@@ -173,11 +346,23 @@ int dsp_source_params(const art_spatializer_settings& st, const art_audio_source
   return ART_OK;
 }
 
-void launch_dsp(float* data, const long long* offsets, const int* frames_of, int frames_all,
-                const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st) {
+void launch_dsp(float* data, unsigned long long data_bytes, const long long* offsets, const int* frames_of,
+                int frames_all, const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st) {
   if (count <= 0) return;
-  hipLaunchKernelGGL(dsp_kernel, dim3((count + kDspBlock - 1) / kDspBlock), dim3(kDspBlock), 0, st, data, offsets,
-                     frames_of, frames_all, params, state, count);
+  static const int mode = [] {  // ART_DSP_KERNEL=lane: one lane per source, direct loads (A/B only)
+    const char* e = std::getenv("ART_DSP_KERNEL");
+    return e && !std::strcmp(e, "lane") ? 1 : 0;
+  }();
+  // the tiled kernel's 8-B buffer ops need an 8-B aligned base (every source offset is an even
+  // float count) and 32-bit byte offsets
+  const bool aligned = (reinterpret_cast<uintptr_t>(data) & 7) == 0;
+  if (mode == 0 && aligned && data_bytes < 0x7fffffffULL) {
+    hipLaunchKernelGGL(dsp_tiled_kernel, dim3((count + kTS - 1) / kTS), dim3(64), 0, st, data, offsets, frames_of,
+                       frames_all, params, state, count, (uint32_t)data_bytes);
+  } else {
+    hipLaunchKernelGGL(dsp_kernel, dim3((count + kDspBlock - 1) / kDspBlock), dim3(kDspBlock), 0, st, data, offsets,
+                       frames_of, frames_all, params, state, count);
+  }
 }
 
 }  // namespace art

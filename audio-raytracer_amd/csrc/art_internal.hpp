@@ -87,8 +87,8 @@ struct SortBufs {
 // per-sample spatializer DSP (art_dsp.hip)
 int dsp_source_params(const art_spatializer_settings& st, const art_audio_source& src, int sample_rate,
                       art_dsp_source_params& p);
-void launch_dsp(float* data, const long long* offsets, const int* frames_of, int frames_all,
-                const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st);
+void launch_dsp(float* data, unsigned long long data_bytes, const long long* offsets, const int* frames_of,
+                int frames_all, const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st);
 
 size_t sort_scene_temp_bytes(int n);
 bool fast_uses_sorted_scene();  // whether the throughput kernel reads the sorted copies

@@ -54,6 +54,12 @@ def parse():
     p.add_argument("--collider-scale", type=float, default=None,
                    help="scale the config's collider count (experiments only; the metric is quoted at 1)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU-baseline sample")
+    p.add_argument("--path", choices=("raytrace", "dsp"), default="raytrace",
+                   help="raytrace: the headline metric; dsp: the per-sample spatializer DSP (SURVEY.md 8 f rank 1)")
+    p.add_argument("--dsp-frames", type=int, default=1024, help="frames per OnAudioFilterRead buffer (dsp path)")
+    p.add_argument("--dsp-batch", type=int, default=65536, help="sources of the large-batch roofline run (dsp path)")
+    p.add_argument("--dsp-sort", action="store_true",
+                   help="group the device batch by filter class, as art_dsp_process does (dsp path)")
     return p.parse_args()
 
 
@@ -78,8 +84,181 @@ def cpu_baseline(cfg, scene, params, org, fans, threads, min_seconds):
     return tests / dt, dt, tests, frames
 
 
+DSP_BYTES_PER_FRAME = 16     # one stereo frame read + written (8 B each way)
+DSP_BYTES_PER_SOURCE = 32 + 64  # art_dsp_source_params read + art_dsp_state read and written
+
+
+def dsp_sources(rng, n, frames):
+    from art.dsp import AudioSource, SpatializerSettings
+    st = SpatializerSettings(muffle_curve=rng.random(50).astype(np.float32),
+                             reverb_volume_curve=rng.random(50).astype(np.float32))
+    srcs = []
+    for i in range(n):
+        d = rng.standard_normal(3)
+        d /= np.linalg.norm(d)
+        srcs.append(AudioSource(data=(rng.standard_normal(frames * 2) * 0.3).astype(np.float32),
+                                muffle_strength=float(rng.random()) if i % 3 else 0.0, reverb_volume=float(rng.random()),
+                                local_dir=tuple(float(v) for v in d), listener_distance=float(rng.uniform(0, 30))))
+    return st, srcs
+
+
+def dsp_device_run(ctx, d_data, d_params, d_state, count, frames, steps, warmup):
+    """Time `steps` launches of art_dsp_process_device on torch's current stream (HIP events on
+    that stream); returns ms per launch."""
+    sp = torch.cuda.current_stream().cuda_stream
+    for _ in range(warmup):
+        assert ctx.lib.art_dsp_process_device(ctx.ptr, d_data.data_ptr(), d_params.data_ptr(), d_state.data_ptr(),
+                                              count, frames, sp) == 0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        ctx.lib.art_dsp_process_device(ctx.ptr, d_data.data_ptr(), d_params.data_ptr(), d_state.data_ptr(), count,
+                                       frames, sp)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def main_dsp(a):
+    """Per-sample spatializer DSP (include/art_dsp.h): one step = one audio tick, every source's
+    OnAudioFilterRead buffer (AudioSpatializer.cs:70-87) processed on the device. Sources are
+    independent: N ranks run N shards of sources (weak scaling, no collective)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg = art.CONFIGS[a.config]
+    S, F, sr = cfg.S, a.dsp_frames, 48000
+    rng = np.random.default_rng(1234 + rank)
+    st, srcs = dsp_sources(rng, S, F)
+    params = np.concatenate([art.dsp.source_params(st, x, sr) for x in srcs])
+    if a.dsp_sort:
+        order = np.argsort(params["flags"] & 3, kind="stable")
+        srcs = [srcs[i] for i in order]
+        params = params[order]
+    ctx = art.Context(1 << torch.cuda.current_device())
+    d_data = torch.from_numpy(np.stack([x.data for x in srcs])).to(dev)
+    d_params = torch.from_numpy(params.view(np.uint8).copy()).to(dev)
+    d_state = torch.zeros(S * abi.DSP_STATE.itemsize, dtype=torch.uint8, device=dev)
+
+    sp = torch.cuda.current_stream().cuda_stream
+    for _ in range(a.warmup):
+        ctx.lib.art_dsp_process_device(ctx.ptr, d_data.data_ptr(), d_params.data_ptr(), d_state.data_ptr(), S, F, sp)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(a.steps):
+        ctx.lib.art_dsp_process_device(ctx.ptr, d_data.data_ptr(), d_params.data_ptr(), d_state.data_ptr(), S, F, sp)
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / a.steps
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    frames_all = S * F * world * a.steps
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # host API (art_dsp_process): host buffers, H2D + kernel + D2H, per tick
+    import ctypes as C
+    c_st = st.to_c()
+    c_srcs = art.dsp.sources_to_c(srcs)  # the C# caller's struct array: built once, reused per tick
+    host_ms = []
+    for i in range(25):
+        t1 = time.perf_counter()
+        rc = ctx.lib.art_dsp_process(ctx.ptr, C.byref(c_st), c_srcs, S, sr)
+        if i >= 5:
+            host_ms.append((time.perf_counter() - t1) * 1e3)
+        assert rc == 0, rc
+    # large batch: the same sources repeated; HBM roofline of the kernel
+    B = a.dsp_batch
+    reps = (B + S - 1) // S
+    b_data = d_data.repeat(reps, 1)[:B].contiguous()
+    b_params = d_params.view(S, -1).repeat(reps, 1)[:B].contiguous()
+    b_state = torch.zeros(B * abi.DSP_STATE.itemsize, dtype=torch.uint8, device=dev)
+    big_ms = dsp_device_run(ctx, b_data, b_params, b_state, B, F, max(3, a.steps // 10), 2)
+    big_bytes = B * F * DSP_BYTES_PER_FRAME + B * DSP_BYTES_PER_SOURCE
+    big_gbs = big_bytes / (big_ms * 1e-3) / 1e9
+    tick_bytes = S * F * DSP_BYTES_PER_FRAME + S * DSP_BYTES_PER_SOURCE
+    tick_gbs = tick_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "traffic_dsp.json")
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get("dsp_bytes_per_launch_batch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle  # CPU baseline leg only
+        oracle.load()
+        n, t1 = 0, time.perf_counter()
+        while True:
+            oracle.dsp_process(st, srcs, sr)
+            n += 1
+            cdt = time.perf_counter() - t1
+            if cdt >= a.cpu_seconds or n >= 20000:
+                break
+        cpu = {"value": n * S * F / cdt, "unit": "stereo frames/s", "cores": 1, "kind": "port",
+               "sample": f"{n} ticks x {S} sources x {F} frames ({cdt:.1f} s) through or_dsp_process "
+                         f"(oracle/art_oracle.c, gcc -O3 -ffp-contract=off), one thread"}
+    value = frames_all / dt
+    res = {
+        "metric": "spatializer DSP stereo frames/s (per-sample OnAudioFilterRead chain)",
+        "value": value,
+        "unit": "stereo frames/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "realtime_sources_at_48k": value / sr,
+        "p50_host_tick_ms": statistics.median(host_ms),
+        "p50_host_tick_ms_note": "art_dsp_process on host buffers: pack, H2D, kernel, D2H, unpack (PCIe-inclusive)",
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"dsp tick: {S} spatializers (config{cfg.index} sources) x {F} stereo frames @ 48 kHz",
+                   "sources_per_gpu": S, "frames": F, "grouped_by_filter_class": bool(a.dsp_sort), "parallelism": f"source-sharded x{world} (replicas, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": big_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": big_gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel": "dsp_tiled_kernel",
+                     "kernel_ms": big_ms, "batch_sources": B, "algorithmic_bytes": big_bytes,
+                     "note": f"large batch ({B} sources x {F} frames, {DSP_BYTES_PER_FRAME} B/frame + "
+                             f"{DSP_BYTES_PER_SOURCE} B/source); the {S}-source tick is bound by the serial "
+                             "per-channel recurrence (one lane per chain), not HBM",
+                     "tick": {"kernel_ms": kern_ms, "achieved": tick_gbs, "frac": tick_gbs / HBM_PEAK_GBS,
+                              "algorithmic_bytes": tick_bytes}},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.path == "dsp":
+        return main_dsp(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -195,12 +195,13 @@ def test_gpu_matches_oracle(ctx, seed):
 
 
 @pytest.mark.gpu
-def test_gpu_device_batch_matches_oracle(ctx):
-    import ctypes as C
+@pytest.mark.parametrize("count,frames", [(300, 512), (33, 37), (1, 1), (64, 1000)])
+def test_gpu_device_batch_matches_oracle(ctx, count, frames):
+    """Device-resident batch: the tiled kernel's full and partial tiles, partial waves, mixed
+    filter classes (the per-lane select variant) and carried state."""
     import torch
-    rng = np.random.default_rng(7)
+    rng = np.random.default_rng(7 + count)
     st = random_settings(rng)
-    count, frames = 300, 512
     srcs = random_sources(rng, count, frames_choices=(frames,))
     for s in srcs:
         s.channels = 2
