@@ -50,6 +50,8 @@ ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_WAVEFRONT = 0x8
 ART_CTX_COUNT_EXECUTED = 0x10
+ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
+ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 
 ART_OWN_SPHERE, ART_OWN_AABB, ART_OWN_OBB = 0, 1, 2
@@ -102,6 +104,11 @@ class art_fan_layout(C.Structure):
 class art_kernel_times(C.Structure):
     _fields_ = [("raytrace_ms", C.c_double), ("permeate_ms", C.c_double), ("reduce_ms", C.c_double),
                 ("launches", C.c_int32)]
+
+
+class art_collider_sync_stats(C.Structure):
+    _fields_ = [("dirty_records", C.c_int32), ("full_prep", C.c_int32), ("reallocated", C.c_int32),
+                ("reserved", C.c_int32), ("bytes_uploaded", C.c_uint64)]
 
 
 class art_exec_counts(C.Structure):
@@ -182,6 +189,16 @@ SIGNATURES = {
     "art_dsp_source_params_get": (I32, [C.POINTER(art_spatializer_settings), C.POINTER(art_audio_source), I32,
                                         C.POINTER(art_dsp_source_params)]),
     "art_dsp_process_device": (I32, [VP, VP, VP, VP, I32, I32, VP]),
+    # art_colliders.h
+    "art_collider_add": (I32, [VP, I32, VP, C.POINTER(I32)]),
+    "art_collider_set": (I32, [VP, I32, I32, VP]),
+    "art_collider_set_many": (I32, [VP, I32, VP, VP, I32]),
+    "art_collider_remove_swapback": (I32, [VP, I32, I32]),
+    "art_collider_get": (I32, [VP, I32, I32, VP]),
+    "art_collider_count": (I32, [VP, I32]),
+    "art_colliders_clear": (I32, [VP]),
+    "art_colliders_sync": (I32, [VP]),
+    "art_colliders_last_sync": (I32, [VP, C.POINTER(art_collider_sync_stats)]),
     "art_device_count": (I32, []),
     # art_synth.h
     "art_synth_scene": (I32, [C.POINTER(art_synth_config), VP, VP, VP, VP, VP, VP]),

@@ -22,6 +22,7 @@
 #include "../../include/art.h"
 #include "../../include/art_device.h"
 #include "../../include/art_dsp.h"
+#include "../../include/art_colliders.h"
 #include "art_internal.hpp"
 #include "art_wavefront.hpp"
 #include "unity_math.hpp"
@@ -81,6 +82,7 @@ struct Frame {
   int R = 0, H = 0, T = 0, TC = 0, bs = 0, nb = 0;
   int ns = 0, na = 0, no = 0;
   uint32_t stages = 0;
+  bool resident = false;               // colliders come from the resident store (art_colliders.h)
   FrameParams fp{};
   FanLayout L{};
   std::vector<int2> slot_batch;        // permeation: [TC] ray range of the last batch writing slot s
@@ -103,6 +105,13 @@ struct Device {
   DevBuf exec;  // executed-work counters (ART_CTX_COUNT_EXECUTED)
   DevBuf pairs; // global visibility pairs of the split raytrace path
   DevBuf dsp;   // per-sample DSP batch (art_dsp_process): samples, offsets, frames, params, states
+  // resident collider store (art_colliders.h): AoS lists, decoded records + bounds, sync upload
+  DevBuf st_raw, st_soa, st_upd;
+  int st_cap[3] = {0, 0, 0};
+  DevScene st_sc{};             // collider pointers of the store (counts = last sync)
+  bool st_fresh = true;         // capacity (re)allocated: every record must be uploaded
+  hipEvent_t st_done = nullptr; // recorded after the last sync's upload + decode (dv.stream)
+  bool st_pending = false;      // st_done recorded and the host staging may still be read
   uint64_t exec_launches = 0;
   DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
   int wf_blocks = 0;
@@ -131,6 +140,21 @@ struct art_ctx {
   art_test_counts last_counts{};
   bool has_counts = false;
   std::vector<uint64_t> nonowned;  // per type (s, a, o): sum over targets of non-owned colliders
+  // resident collider store: the NextBatch mirror per kind, dirty marks, the last sync's counts
+  struct Kind {
+    std::vector<uint8_t> recs;      // count * size bytes
+    int count = 0;
+    std::vector<uint8_t> dirty;     // per record
+    std::vector<int> dirty_list;
+  } kinds[3];
+  int synced[3] = {0, 0, 0};
+  bool store_synced = false;
+  // audio_target_id of every synced record and their histogram (index = id + 32768), kept
+  // incrementally from the dirty records (permeation loss test counts of counting frames)
+  std::vector<int16_t> synced_tid[3];
+  std::vector<int> tid_hist[3];
+  art_collider_sync_stats last_sync{};
+  HostBuf h_upd;
 };
 
 namespace {
@@ -242,11 +266,17 @@ void coherent_order(const art_half3* dirs, int R, std::vector<int>& order) {
 }
 
 // Frame scalars + batch tables (Audio/AudioRayTracer.cs:161, Jobs/*:63-64, :36-37).
-void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
+void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int* resident_counts = nullptr) {
   f = Frame();
   f.R = d->ray_count; f.H = d->max_hits_per_ray; f.T = d->audio_target_count;
   f.TC = d->batch_slots; f.bs = d->batch_size; f.nb = (f.R + f.bs - 1) / f.bs;
   f.ns = d->sphere_count; f.na = d->aabb_count; f.no = d->obb_count;
+  if (resident_counts) {
+    f.resident = true;
+    f.ns = resident_counts[0]; f.na = resident_counts[1]; f.no = resident_counts[2];
+  }
+  // collider sections of the staging and record buffers (empty when the store holds them)
+  const size_t sn = f.resident ? 0 : (size_t)f.ns, an = f.resident ? 0 : (size_t)f.na, on = f.resident ? 0 : (size_t)f.no;
   f.stages = d->stages;
   f.L = make_layout(d, out_flags);
   f.slot_batch.assign(f.TC, make_int2(0, 0));
@@ -284,9 +314,9 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
   }
   // input staging layout (16-B aligned sections)
   size_t o = 0;
-  f.off_sph = o; o = align_up(o + (size_t)f.ns * sizeof(art_sphere), 16);
-  f.off_aabb = o; o = align_up(o + (size_t)f.na * sizeof(art_aabb), 16);
-  f.off_obb = o; o = align_up(o + (size_t)f.no * sizeof(art_obb), 16);
+  f.off_sph = o; o = align_up(o + sn * sizeof(art_sphere), 16);
+  f.off_aabb = o; o = align_up(o + an * sizeof(art_aabb), 16);
+  f.off_obb = o; o = align_up(o + on * sizeof(art_obb), 16);
   f.off_tgt = o; o = align_up(o + (size_t)f.T * 12, 16);
   f.off_dirs = o; o = align_up(o + (size_t)f.R * sizeof(art_half3), 16);
   f.off_vol = o; o = align_up(o + (size_t)p.vol_n * 4, 16);
@@ -296,13 +326,13 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
   f.off_order = o; o = align_up(o + (size_t)f.R * 4, 16);
   f.raw_bytes = o;
   size_t s = 0;
-  f.soa_sph = s; s = align_up(s + (size_t)f.ns * sizeof(SphereRec), 256);
-  f.soa_aabb = s; s = align_up(s + (size_t)f.na * sizeof(AabbRec), 256);
-  f.soa_obb = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
-  f.soa_sphc = s; s = align_up(s + (size_t)f.ns * sizeof(SphereCold), 256);
-  f.soa_aabbc = s; s = align_up(s + (size_t)f.na * sizeof(AabbCold), 256);
-  f.soa_obbc = s; s = align_up(s + (size_t)f.no * sizeof(ObbCold), 256);
-  f.soa_cull = s; s = align_up(s + (size_t)(f.ns + f.na + f.no) * sizeof(CullRec), 256);
+  f.soa_sph = s; s = align_up(s + sn * sizeof(SphereRec), 256);
+  f.soa_aabb = s; s = align_up(s + an * sizeof(AabbRec), 256);
+  f.soa_obb = s; s = align_up(s + on * sizeof(ObbRec), 256);
+  f.soa_sphc = s; s = align_up(s + sn * sizeof(SphereCold), 256);
+  f.soa_aabbc = s; s = align_up(s + an * sizeof(AabbCold), 256);
+  f.soa_obbc = s; s = align_up(s + on * sizeof(ObbCold), 256);
+  f.soa_cull = s; s = align_up(s + (sn + an + on) * sizeof(CullRec), 256);
   {  // broad-phase structure (art_bvh.hip)
     const size_t n = (size_t)(f.ns + f.na + f.no);
     const size_t nch = (size_t)((f.ns + 63) / 64 + (f.na + 63) / 64 + (f.no + 63) / 64);
@@ -323,9 +353,11 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f) {
 }
 
 void pack_inputs(const art_frame_desc* d, const Frame& f, uint8_t* h) {
-  if (f.ns) memcpy(h + f.off_sph, d->sphere_colliders, (size_t)f.ns * sizeof(art_sphere));
-  if (f.na) memcpy(h + f.off_aabb, d->aabb_colliders, (size_t)f.na * sizeof(art_aabb));
-  if (f.no) memcpy(h + f.off_obb, d->obb_colliders, (size_t)f.no * sizeof(art_obb));
+  if (!f.resident) {
+    if (f.ns) memcpy(h + f.off_sph, d->sphere_colliders, (size_t)f.ns * sizeof(art_sphere));
+    if (f.na) memcpy(h + f.off_aabb, d->aabb_colliders, (size_t)f.na * sizeof(art_aabb));
+    if (f.no) memcpy(h + f.off_obb, d->obb_colliders, (size_t)f.no * sizeof(art_obb));
+  }
   memcpy(h + f.off_tgt, d->audio_target_positions, (size_t)f.T * 12);
   memcpy(h + f.off_dirs, d->ray_directions, (size_t)f.R * sizeof(art_half3));
   if (f.fp.vol_n) memcpy(h + f.off_vol, d->dsp->reverb_volume_curve.baked, (size_t)f.fp.vol_n * 4);
@@ -342,20 +374,27 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   HIP_TRY(c, hipMemcpyAsync(dv.raw.p, h_in, f.raw_bytes, hipMemcpyHostToDevice, dv.stream));
   uint8_t* raw = static_cast<uint8_t*>(dv.raw.p);
   uint8_t* soa = static_cast<uint8_t*>(dv.soa.p);
-  launch_prep(reinterpret_cast<const art_sphere*>(raw + f.off_sph), f.ns, reinterpret_cast<const art_aabb*>(raw + f.off_aabb),
-              f.na, reinterpret_cast<const art_obb*>(raw + f.off_obb), f.no, reinterpret_cast<SphereRec*>(soa + f.soa_sph),
-              reinterpret_cast<SphereCold*>(soa + f.soa_sphc), reinterpret_cast<AabbRec*>(soa + f.soa_aabb),
-              reinterpret_cast<AabbCold*>(soa + f.soa_aabbc), reinterpret_cast<ObbRec*>(soa + f.soa_obb),
-              reinterpret_cast<ObbCold*>(soa + f.soa_obbc), reinterpret_cast<CullRec*>(soa + f.soa_cull), dv.stream);
-  HIP_TRY(c, hipGetLastError());
   DevScene& sc = dv.sc;
-  sc.sph = reinterpret_cast<const SphereRec*>(soa + f.soa_sph); sc.ns = f.ns;
-  sc.aabb = reinterpret_cast<const AabbRec*>(soa + f.soa_aabb); sc.na = f.na;
-  sc.obb = reinterpret_cast<const ObbRec*>(soa + f.soa_obb); sc.no = f.no;
-  sc.sphc = reinterpret_cast<const SphereCold*>(soa + f.soa_sphc);
-  sc.aabbc = reinterpret_cast<const AabbCold*>(soa + f.soa_aabbc);
-  sc.obbc = reinterpret_cast<const ObbCold*>(soa + f.soa_obbc);
-  sc.cull = reinterpret_cast<const CullRec*>(soa + f.soa_cull);
+  if (f.resident) {  // records and bounds of the last art_colliders_sync
+    sc.sph = dv.st_sc.sph; sc.sphc = dv.st_sc.sphc; sc.ns = dv.st_sc.ns;
+    sc.aabb = dv.st_sc.aabb; sc.aabbc = dv.st_sc.aabbc; sc.na = dv.st_sc.na;
+    sc.obb = dv.st_sc.obb; sc.obbc = dv.st_sc.obbc; sc.no = dv.st_sc.no;
+    sc.cull = dv.st_sc.cull;
+  } else {
+    launch_prep(reinterpret_cast<const art_sphere*>(raw + f.off_sph), f.ns, reinterpret_cast<const art_aabb*>(raw + f.off_aabb),
+                f.na, reinterpret_cast<const art_obb*>(raw + f.off_obb), f.no, reinterpret_cast<SphereRec*>(soa + f.soa_sph),
+                reinterpret_cast<SphereCold*>(soa + f.soa_sphc), reinterpret_cast<AabbRec*>(soa + f.soa_aabb),
+                reinterpret_cast<AabbCold*>(soa + f.soa_aabbc), reinterpret_cast<ObbRec*>(soa + f.soa_obb),
+                reinterpret_cast<ObbCold*>(soa + f.soa_obbc), reinterpret_cast<CullRec*>(soa + f.soa_cull), dv.stream);
+    HIP_TRY(c, hipGetLastError());
+    sc.sph = reinterpret_cast<const SphereRec*>(soa + f.soa_sph); sc.ns = f.ns;
+    sc.aabb = reinterpret_cast<const AabbRec*>(soa + f.soa_aabb); sc.na = f.na;
+    sc.obb = reinterpret_cast<const ObbRec*>(soa + f.soa_obb); sc.no = f.no;
+    sc.sphc = reinterpret_cast<const SphereCold*>(soa + f.soa_sphc);
+    sc.aabbc = reinterpret_cast<const AabbCold*>(soa + f.soa_aabbc);
+    sc.obbc = reinterpret_cast<const ObbCold*>(soa + f.soa_obbc);
+    sc.cull = reinterpret_cast<const CullRec*>(soa + f.soa_cull);
+  }
   sc.targets = reinterpret_cast<const float*>(raw + f.off_tgt); sc.T = f.T;
   sc.dirs = reinterpret_cast<const uint16_t*>(raw + f.off_dirs); sc.R = f.R;
   SortBufs sb;
@@ -377,6 +416,15 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
 // Per-type sum over targets of colliders NOT owned by the target (permeation loss test counts).
 void count_nonowned(art_ctx* c, const art_frame_desc* d) {
   c->nonowned.assign(3, 0);
+  if (c->flags & ART_CTX_RESIDENT_COLLIDERS) {  // from the last sync's audio_target_id histograms
+    for (int k = 0; k < 3; ++k) {
+      uint64_t owned = 0;
+      if (!c->tid_hist[k].empty())
+        for (int t = 0; t < d->audio_target_count && t < 32768; ++t) owned += (uint64_t)c->tid_hist[k][(size_t)t + 32768];
+      c->nonowned[k] = (uint64_t)d->audio_target_count * (uint64_t)c->synced[k] - owned;
+    }
+    return;
+  }
   for (int t = 0; t < d->audio_target_count; ++t) {
     uint64_t os = 0, oa = 0, oo = 0;
     for (int i = 0; i < d->sphere_count; ++i) os += d->sphere_colliders[i].audio_target_id == t;
@@ -386,6 +434,15 @@ void count_nonowned(art_ctx* c, const art_frame_desc* d) {
     c->nonowned[1] += d->aabb_count - oa;
     c->nonowned[2] += d->obb_count - oo;
   }
+}
+
+// ART_CTX_RESIDENT_COLLIDERS: the desc carries no colliders and the store has been synced.
+int check_resident(art_ctx* c, const art_frame_desc* d) {
+  if (!(c->flags & ART_CTX_RESIDENT_COLLIDERS)) return ART_OK;
+  if (d->sphere_count || d->aabb_count || d->obb_count || d->sphere_colliders || d->aabb_colliders || d->obb_colliders)
+    return fail(c, ART_E_INVALID, "ART_CTX_RESIDENT_COLLIDERS: the desc's collider arrays must be NULL / 0");
+  if (!c->store_synced) return fail(c, ART_E_STATE, "ART_CTX_RESIDENT_COLLIDERS: no art_colliders_sync yet");
+  return ART_OK;
 }
 
 // Throughput raytrace implementation: the single-launch K-way block kernel (default, targets up
@@ -594,6 +651,8 @@ ART_API void art_destroy(art_ctx* c) {
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.work.release(); dv.exec.release(); dv.pairs.release(); dv.dsp.release();
+    dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
+    if (dv.st_done) (void)hipEventDestroy(dv.st_done);
     dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
@@ -602,6 +661,7 @@ ART_API void art_destroy(art_ctx* c) {
   c->h_in.release();
   c->h_block.release();
   c->h_dsp.release();
+  c->h_upd.release();
   delete c;
 }
 
@@ -631,6 +691,8 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
   int rc = validate_desc(c, d);
   if (rc) return rc;
   if (fan_count < 0 || (fan_count > 0 && !fans)) return fail(c, ART_E_INVALID, "bad fans array");
+  rc = check_resident(c, d);
+  if (rc) return rc;
   const bool hits = fan_wants_hits(fans, fan_count);
   for (int i = 0; i < fan_count; ++i) {
     const art_fan& f = fans[i];
@@ -638,7 +700,7 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
       return fail(c, ART_E_INVALID, "fan %d: echo/muffle/permeation/settings arrays are required", i);
   }
   Frame& f = c->fr;
-  make_frame(d, hits ? ART_OUT_HIT_RESULTS : 0u, f);
+  make_frame(d, hits ? ART_OUT_HIT_RESULTS : 0u, f, (c->flags & ART_CTX_RESIDENT_COLLIDERS) ? c->synced : nullptr);
   const FanLayout& L = f.L;
   if (!c->h_in.reserve(f.raw_bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
   const size_t origins_off = align_up(f.raw_bytes, 16);
@@ -772,8 +834,10 @@ ART_API int art_scene_bind(art_ctx* c, const art_frame_desc* d) {
   if (!c) return ART_E_INVALID;
   int rc = validate_desc(c, d);
   if (rc) return rc;
+  rc = check_resident(c, d);
+  if (rc) return rc;
   Frame& f = c->fr;
-  make_frame(d, 0u, f);
+  make_frame(d, 0u, f, (c->flags & ART_CTX_RESIDENT_COLLIDERS) ? c->synced : nullptr);
   if (!c->h_in.reserve(f.raw_bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
   pack_inputs(d, f, static_cast<uint8_t*>(c->h_in.p));
   count_nonowned(c, d);
@@ -802,6 +866,7 @@ static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, 
     f.L = make_layout(&tmp, out_flags);
   }
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL is the HIP default stream (torch's default)
+  if (f.resident && dv.st_done) HIP_TRY(c, hipStreamWaitEvent(st, dv.st_done, 0));
   int rc = enqueue_kernels(c, dv, f, d_origins, fan_count, static_cast<uint8_t*>(d_block), st, count);
   if (rc) return rc;
   if (count) return read_counts(c, dv, st, out, false);
@@ -854,6 +919,253 @@ ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {
     dv.ev_used.clear();
     out->launches += frames;
   }
+  return ART_OK;
+}
+
+// ---- resident collider store (include/art_colliders.h) ----------------------------------
+static const size_t kRecSize[3] = {sizeof(art_sphere), sizeof(art_aabb), sizeof(art_obb)};
+
+ART_API int art_collider_add(art_ctx* c, int32_t kind, const void* rec, int32_t* out_id) {
+  if (!c) return ART_E_INVALID;
+  if (kind < 0 || kind > 2 || !rec) return fail(c, ART_E_INVALID, "art_collider_add: bad kind or record");
+  auto& K = c->kinds[kind];
+  if (K.count >= (1 << 24)) return fail(c, ART_E_UNSUPPORTED, "more than 2^24 colliders of one kind");
+  const size_t rs = kRecSize[kind];
+  K.recs.resize((size_t)(K.count + 1) * rs);
+  memcpy(K.recs.data() + (size_t)K.count * rs, rec, rs);
+  K.dirty.push_back(1);
+  K.dirty_list.push_back(K.count);
+  if (out_id) *out_id = K.count;  // AudioColliderId = NextBatch.Length before the add
+  K.count++;
+  return ART_OK;
+}
+
+ART_API int art_collider_set(art_ctx* c, int32_t kind, int32_t id, const void* rec) {
+  if (!c) return ART_E_INVALID;
+  if (kind < 0 || kind > 2 || !rec) return fail(c, ART_E_INVALID, "art_collider_set: bad kind or record");
+  auto& K = c->kinds[kind];
+  if (id < 0 || id >= K.count) return fail(c, ART_E_INVALID, "art_collider_set: id %d out of range [0, %d)", id, K.count);
+  const size_t rs = kRecSize[kind];
+  memcpy(K.recs.data() + (size_t)id * rs, rec, rs);
+  if (!K.dirty[(size_t)id]) { K.dirty[(size_t)id] = 1; K.dirty_list.push_back(id); }
+  return ART_OK;
+}
+
+ART_API int art_collider_set_many(art_ctx* c, int32_t kind, const int32_t* ids, const void* recs, int32_t n) {
+  if (!c) return ART_E_INVALID;
+  if (kind < 0 || kind > 2 || n < 0 || (n > 0 && (!ids || !recs)))
+    return fail(c, ART_E_INVALID, "art_collider_set_many: bad arguments");
+  auto& K = c->kinds[kind];
+  for (int32_t j = 0; j < n; ++j)  // validate first: all or nothing
+    if (ids[j] < 0 || ids[j] >= K.count)
+      return fail(c, ART_E_INVALID, "art_collider_set_many: id %d out of range [0, %d)", ids[j], K.count);
+  const size_t rs = kRecSize[kind];
+  const uint8_t* r = static_cast<const uint8_t*>(recs);
+  for (int32_t j = 0; j < n; ++j) {
+    const int id = ids[j];
+    memcpy(K.recs.data() + (size_t)id * rs, r + (size_t)j * rs, rs);
+    if (!K.dirty[(size_t)id]) { K.dirty[(size_t)id] = 1; K.dirty_list.push_back(id); }
+  }
+  return ART_OK;
+}
+
+ART_API int art_collider_remove_swapback(art_ctx* c, int32_t kind, int32_t id) {
+  if (!c) return ART_E_INVALID;
+  if (kind < 0 || kind > 2) return fail(c, ART_E_INVALID, "art_collider_remove_swapback: bad kind");
+  auto& K = c->kinds[kind];
+  if (id < 0 || id >= K.count) return ART_OK;  // skipped, as AudioColliderManager.SwapRemove (:92-93)
+  const size_t rs = kRecSize[kind];
+  const int last = K.count - 1;
+  if (id != last) {
+    memcpy(K.recs.data() + (size_t)id * rs, K.recs.data() + (size_t)last * rs, rs);
+    if (!K.dirty[(size_t)id]) { K.dirty[(size_t)id] = 1; K.dirty_list.push_back(id); }
+  }
+  K.count = last;
+  K.recs.resize((size_t)last * rs);
+  K.dirty.resize((size_t)last);
+  return ART_OK;
+}
+
+ART_API int art_collider_get(art_ctx* c, int32_t kind, int32_t id, void* rec) {
+  if (!c) return ART_E_INVALID;
+  if (kind < 0 || kind > 2 || !rec) return fail(c, ART_E_INVALID, "art_collider_get: bad kind or record");
+  const auto& K = c->kinds[kind];
+  if (id < 0 || id >= K.count) return fail(c, ART_E_INVALID, "art_collider_get: id %d out of range [0, %d)", id, K.count);
+  memcpy(rec, K.recs.data() + (size_t)id * kRecSize[kind], kRecSize[kind]);
+  return ART_OK;
+}
+
+ART_API int art_collider_count(art_ctx* c, int32_t kind) {
+  if (!c) return ART_E_INVALID;
+  if (kind < 0 || kind > 2) return fail(c, ART_E_INVALID, "art_collider_count: bad kind");
+  return c->kinds[kind].count;
+}
+
+ART_API int art_colliders_clear(art_ctx* c) {
+  if (!c) return ART_E_INVALID;
+  for (auto& K : c->kinds) {
+    K.recs.clear(); K.dirty.clear(); K.dirty_list.clear(); K.count = 0;
+  }
+  return ART_OK;
+}
+
+ART_API int art_colliders_last_sync(art_ctx* c, art_collider_sync_stats* out) {
+  if (!c || !out) return ART_E_INVALID;
+  *out = c->last_sync;
+  return ART_OK;
+}
+
+ART_API int art_colliders_sync(art_ctx* c) {
+  if (!c) return ART_E_INVALID;
+  if (c->inflight) return fail(c, ART_E_STATE, "art_colliders_sync: a frame is in flight (sync after art_complete)");
+  const int n[3] = {c->kinds[0].count, c->kinds[1].count, c->kinds[2].count};
+  bool counts_changed = !c->store_synced;
+  for (int k = 0; k < 3; ++k) counts_changed |= n[k] != c->synced[k];
+  // device capacity: grow (x2) and re-upload everything when a list outgrows it
+  bool fresh = false;
+  for (Device& dv : c->devs) {
+    if (n[0] > dv.st_cap[0] || n[1] > dv.st_cap[1] || n[2] > dv.st_cap[2] || !dv.st_raw.p) {
+      for (int k = 0; k < 3; ++k) dv.st_cap[k] = std::max({n[k], 2 * dv.st_cap[k], 64});
+      dv.st_raw.release();
+      dv.st_soa.release();
+      dv.st_fresh = true;
+    }
+    fresh |= dv.st_fresh;
+  }
+  // dirty records of each kind (all of them after a reallocation), ascending
+  std::vector<int> lists[3];
+  for (int k = 0; k < 3; ++k) {
+    auto& K = c->kinds[k];
+    if (fresh) {
+      lists[k].resize((size_t)n[k]);
+      for (int i = 0; i < n[k]; ++i) lists[k][(size_t)i] = i;
+    } else {
+      for (int i : K.dirty_list)
+        if (i < n[k] && K.dirty[(size_t)i]) lists[k].push_back(i);
+      std::sort(lists[k].begin(), lists[k].end());
+      lists[k].erase(std::unique(lists[k].begin(), lists[k].end()), lists[k].end());
+    }
+  }
+  // upload image: [idx_s][rec_s][idx_a][rec_a][idx_o][rec_o], 16-B aligned sections
+  size_t off_idx[3], off_rec[3], bytes = 0;
+  for (int k = 0; k < 3; ++k) {
+    off_idx[k] = bytes; bytes = align_up(bytes + lists[k].size() * 4, 16);
+    off_rec[k] = bytes; bytes = align_up(bytes + lists[k].size() * kRecSize[k], 16);
+  }
+  const int nd = (int)(lists[0].size() + lists[1].size() + lists[2].size());
+  for (Device& dv : c->devs) {  // the previous sync's copy may still read the pinned staging
+    if (dv.st_pending) {
+      HIP_TRY(c, hipSetDevice(dv.id));
+      HIP_TRY(c, hipEventSynchronize(dv.st_done));
+      dv.st_pending = false;
+    }
+  }
+  if (bytes && !c->h_upd.reserve(bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  uint8_t* h = static_cast<uint8_t*>(c->h_upd.p);
+  for (int k = 0; k < 3; ++k) {
+    const auto& K = c->kinds[k];
+    const size_t rs = kRecSize[k];
+    for (size_t j = 0; j < lists[k].size(); ++j) {
+      const int i = lists[k][j];
+      memcpy(h + off_idx[k] + j * 4, &i, 4);
+      memcpy(h + off_rec[k] + j * rs, K.recs.data() + (size_t)i * rs, rs);
+    }
+  }
+  for (Device& dv : c->devs) {
+    HIP_TRY(c, hipSetDevice(dv.id));
+    const int* cap = dv.st_cap;
+    const size_t r_s = 0, r_a = align_up((size_t)cap[0] * sizeof(art_sphere), 256),
+                 r_o = r_a + align_up((size_t)cap[1] * sizeof(art_aabb), 256),
+                 r_end = r_o + align_up((size_t)cap[2] * sizeof(art_obb), 256);
+    size_t o = 0;
+    const size_t s_sph = o; o = align_up(o + (size_t)cap[0] * sizeof(SphereRec), 256);
+    const size_t s_sphc = o; o = align_up(o + (size_t)cap[0] * sizeof(SphereCold), 256);
+    const size_t s_aabb = o; o = align_up(o + (size_t)cap[1] * sizeof(AabbRec), 256);
+    const size_t s_aabbc = o; o = align_up(o + (size_t)cap[1] * sizeof(AabbCold), 256);
+    const size_t s_obb = o; o = align_up(o + (size_t)cap[2] * sizeof(ObbRec), 256);
+    const size_t s_obbc = o; o = align_up(o + (size_t)cap[2] * sizeof(ObbCold), 256);
+    const size_t s_cull = o; o = align_up(o + (size_t)(cap[0] + cap[1] + cap[2]) * sizeof(CullRec), 256);
+    if (!dv.st_raw.reserve(r_end) || !dv.st_soa.reserve(o) || (bytes && !dv.st_upd.reserve(bytes)))
+      return fail(c, ART_E_NOMEM, "device allocation failed");
+    uint8_t* raw = static_cast<uint8_t*>(dv.st_raw.p);
+    uint8_t* soa = static_cast<uint8_t*>(dv.st_soa.p);
+    uint8_t* up = static_cast<uint8_t*>(dv.st_upd.p);
+    auto* sph = reinterpret_cast<art_sphere*>(raw + r_s);
+    auto* aabb = reinterpret_cast<art_aabb*>(raw + r_a);
+    auto* obb = reinterpret_cast<art_obb*>(raw + r_o);
+    auto* osph = reinterpret_cast<SphereRec*>(soa + s_sph);
+    auto* osphc = reinterpret_cast<SphereCold*>(soa + s_sphc);
+    auto* oaabb = reinterpret_cast<AabbRec*>(soa + s_aabb);
+    auto* oaabbc = reinterpret_cast<AabbCold*>(soa + s_aabbc);
+    auto* oobb = reinterpret_cast<ObbRec*>(soa + s_obb);
+    auto* oobbc = reinterpret_cast<ObbCold*>(soa + s_obbc);
+    auto* cull = reinterpret_cast<CullRec*>(soa + s_cull);
+    if (nd) {
+      HIP_TRY(c, hipMemcpyAsync(up, h, bytes, hipMemcpyHostToDevice, dv.stream));
+      launch_scatter_prep(reinterpret_cast<const int*>(up + off_idx[0]), reinterpret_cast<const art_sphere*>(up + off_rec[0]),
+                          (int)lists[0].size(), reinterpret_cast<const int*>(up + off_idx[1]),
+                          reinterpret_cast<const art_aabb*>(up + off_rec[1]), (int)lists[1].size(),
+                          reinterpret_cast<const int*>(up + off_idx[2]), reinterpret_cast<const art_obb*>(up + off_rec[2]),
+                          (int)lists[2].size(), sph, aabb, obb, n[0], n[1], osph, osphc, oaabb, oaabbc, oobb, oobbc, cull,
+                          dv.stream);
+      HIP_TRY(c, hipGetLastError());
+    }
+    // a count change moves the bounds of the later kinds (global order spheres, AABBs, OBBs)
+    if (counts_changed && !fresh && n[0] + n[1] + n[2] > 0) {
+      launch_prep(sph, n[0], aabb, n[1], obb, n[2], osph, osphc, oaabb, oaabbc, oobb, oobbc, cull, dv.stream);
+      HIP_TRY(c, hipGetLastError());
+    }
+    // stream-ordered: frames on dv.stream follow; device-path launches on other streams wait on st_done
+    if (!dv.st_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.st_done, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));
+    dv.st_pending = true;
+    DevScene& t = dv.st_sc;
+    t.sph = osph; t.sphc = osphc; t.ns = n[0];
+    t.aabb = oaabb; t.aabbc = oaabbc; t.na = n[1];
+    t.obb = oobb; t.obbc = oobbc; t.no = n[2];
+    t.cull = cull;
+    dv.st_fresh = false;
+    if (dv.bound && c->fr.resident) {  // a bound device-resident scene sees the new snapshot
+      if (fast_uses_sorted_scene() && counts_changed) {
+        dv.bound = false;  // the sorted copies are sized by count: bind again
+      } else {
+        dv.sc.sph = t.sph; dv.sc.sphc = t.sphc; dv.sc.ns = t.ns;
+        dv.sc.aabb = t.aabb; dv.sc.aabbc = t.aabbc; dv.sc.na = t.na;
+        dv.sc.obb = t.obb; dv.sc.obbc = t.obbc; dv.sc.no = t.no;
+        dv.sc.cull = t.cull;
+      }
+    }
+  }
+  if (c->fr.resident) { c->fr.ns = n[0]; c->fr.na = n[1]; c->fr.no = n[2]; }
+  for (int k = 0; k < 3; ++k) {
+    auto& K = c->kinds[k];
+    for (int i : K.dirty_list)  // O(changes), not O(colliders)
+      if ((size_t)i < K.dirty.size()) K.dirty[(size_t)i] = 0;
+    K.dirty_list.clear();
+    c->synced[k] = n[k];
+    // audio_target_id histogram of the synced records: removed tail, then the dirty records
+    auto& tids = c->synced_tid[k];
+    auto& hist = c->tid_hist[k];
+    if (hist.empty()) hist.assign(65536, 0);
+    for (size_t i = (size_t)n[k]; i < tids.size(); ++i) hist[(size_t)(tids[i] + 32768)]--;
+    const size_t old_n = tids.size();
+    tids.resize((size_t)n[k], 0);
+    const size_t rs = kRecSize[k];
+    const size_t tid_off = k == 0 ? offsetof(art_sphere, audio_target_id)
+                                  : (k == 1 ? offsetof(art_aabb, audio_target_id) : offsetof(art_obb, audio_target_id));
+    for (int i : lists[k]) {
+      int16_t v;
+      memcpy(&v, K.recs.data() + (size_t)i * rs + tid_off, 2);
+      if ((size_t)i < old_n) hist[(size_t)(tids[(size_t)i] + 32768)]--;
+      tids[(size_t)i] = v;
+      hist[(size_t)(v + 32768)]++;
+    }
+  }
+  c->store_synced = true;
+  c->last_sync.dirty_records = nd;
+  c->last_sync.full_prep = (counts_changed || fresh) ? 1 : 0;
+  c->last_sync.reallocated = fresh ? 1 : 0;
+  c->last_sync.bytes_uploaded = nd ? bytes : 0;
   return ART_OK;
 }
 

@@ -52,80 +52,120 @@ __device__ __forceinline__ CullRec make_cull(float lx, float ly, float lz, float
   return c;
 }
 
+// Per-collider decode (shared by the full prep and the resident store's scatter): the hot/cold
+// records at in-kind index i and the broad-phase bounds at global index gi.
+__device__ __forceinline__ void prep_sphere(const art_sphere& s, int i, int gi, SphereRec* __restrict__ osph,
+                                            SphereCold* __restrict__ osphc, CullRec* __restrict__ cull) {
+  SphereRec r;
+  r.cx = f16tof32(s.center.x); r.cy = f16tof32(s.center.y); r.cz = f16tof32(s.center.z);
+  float rad = f16tof32(s.radius);
+  r.r2 = rad * rad;
+  r.tid = s.audio_target_id;
+  r.pad0 = r.pad1 = r.pad2 = 0;
+  SphereCold c;
+  c.density = f16tof32(s.material.density);
+  c.absorption = f16tof32(s.material.absorption);
+  c.echo = f16tof32(s.material.echo);
+  c.pad = 0.0f;
+  osph[i] = r;
+  osphc[i] = c;
+  const float ra = fabsf(rad);
+  cull[gi] = make_cull(r.cx - ra, r.cy - ra, r.cz - ra, r.cx + ra, r.cy + ra, r.cz + ra,
+                       fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + ra, kCullSphere);
+}
+
+__device__ __forceinline__ void prep_aabb(const art_aabb& a, int i, int gi, AabbRec* __restrict__ oaabb,
+                                          AabbCold* __restrict__ oaabbc, CullRec* __restrict__ cull) {
+  AabbCold c;
+  c.cx = f16tof32(a.center.x); c.cy = f16tof32(a.center.y); c.cz = f16tof32(a.center.z);
+  c.hx = f16tof32(a.size.x); c.hy = f16tof32(a.size.y); c.hz = f16tof32(a.size.z);
+  c.density = f16tof32(a.material.density);
+  c.absorption = f16tof32(a.material.absorption);
+  c.echo = f16tof32(a.material.echo);
+  c.pad0 = c.pad1 = c.pad2 = 0.0f;
+  AabbRec r;
+  r.mnx = c.cx - c.hx; r.mny = c.cy - c.hy; r.mnz = c.cz - c.hz;
+  r.mxx = c.cx + c.hx; r.mxy = c.cy + c.hy; r.mxz = c.cz + c.hz;
+  r.tid = a.audio_target_id;
+  r.pad = 0.0f;
+  oaabb[i] = r;
+  oaabbc[i] = c;
+  cull[gi] = make_cull(fminf(r.mnx, r.mxx), fminf(r.mny, r.mxy), fminf(r.mnz, r.mxz), fmaxf(r.mnx, r.mxx),
+                       fmaxf(r.mny, r.mxy), fmaxf(r.mnz, r.mxz),
+                       fabsf(c.cx) + fabsf(c.cy) + fabsf(c.cz) + fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz), kCullBox);
+}
+
+__device__ __forceinline__ void prep_obb(const art_obb& b, int i, int gi, ObbRec* __restrict__ oobb,
+                                         ObbCold* __restrict__ oobbc, CullRec* __restrict__ cull) {
+  ObbRec r;
+  ObbCold c;
+  r.cx = f16tof32(b.center.x); r.cy = f16tof32(b.center.y); r.cz = f16tof32(b.center.z);
+  c.hx = f16tof32(b.size.x); c.hy = f16tof32(b.size.y); c.hz = f16tof32(b.size.z);
+  r.lmnx = 0.0f - c.hx; r.lmny = 0.0f - c.hy; r.lmnz = 0.0f - c.hz;
+  r.lmxx = 0.0f + c.hx; r.lmxy = 0.0f + c.hy; r.lmxz = 0.0f + c.hz;
+  r.pad0 = r.pad1 = 0.0f;
+  quat q = half_quaternion_value(b.rot_x, b.rot_y, b.rot_z);
+  quat qi = qinverse(q);
+  r.qx = q.x; r.qy = q.y; r.qz = q.z; r.qw = q.w;
+  c.iqx = qi.x; c.iqy = qi.y; c.iqz = qi.z; c.iqw = qi.w;
+  r.tid = b.audio_target_id;
+  c.density = f16tof32(b.material.density);
+  c.absorption = f16tof32(b.material.absorption);
+  c.echo = f16tof32(b.material.echo);
+  c.pad0 = c.pad1 = 0.0f;
+  oobb[i] = r;
+  oobbc[i] = c;
+  // bounding sphere of the box (|h|_1 >= |h|_2), whatever the rotation
+  const float rho = (fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz)) * 1.001f;
+  const bool qok = isfinite(q.x) && isfinite(q.y) && isfinite(q.z) && isfinite(q.w);
+  cull[gi] = make_cull(r.cx - rho, r.cy - rho, r.cz - rho, r.cx + rho, r.cy + rho, r.cz + rho,
+                       qok ? fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + rho : INFINITY, kCullObb);
+}
+
 __global__ void prep_kernel(const art_sphere* __restrict__ sph, int ns, const art_aabb* __restrict__ aabb, int na,
                             const art_obb* __restrict__ obb, int no, SphereRec* __restrict__ osph,
                             SphereCold* __restrict__ osphc, AabbRec* __restrict__ oaabb, AabbCold* __restrict__ oaabbc,
                             ObbRec* __restrict__ oobb, ObbCold* __restrict__ oobbc, CullRec* __restrict__ cull) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int gi = i;  // global collider order (spheres, AABBs, OBBs) of the broad-phase bounds
-  if (i < ns) {
-    art_sphere s = sph[i];
-    SphereRec r;
-    r.cx = f16tof32(s.center.x); r.cy = f16tof32(s.center.y); r.cz = f16tof32(s.center.z);
-    float rad = f16tof32(s.radius);
-    r.r2 = rad * rad;
-    r.tid = s.audio_target_id;
-    r.pad0 = r.pad1 = r.pad2 = 0;
-    SphereCold c;
-    c.density = f16tof32(s.material.density);
-    c.absorption = f16tof32(s.material.absorption);
-    c.echo = f16tof32(s.material.echo);
-    c.pad = 0.0f;
-    osph[i] = r;
-    osphc[i] = c;
-    const float ra = fabsf(rad);
-    cull[gi] = make_cull(r.cx - ra, r.cy - ra, r.cz - ra, r.cx + ra, r.cy + ra, r.cz + ra,
-                         fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + ra, kCullSphere);
-    return;
-  }
+  const int gi = blockIdx.x * blockDim.x + threadIdx.x;  // global collider order (spheres, AABBs, OBBs)
+  int i = gi;
+  if (i < ns) { prep_sphere(sph[i], i, gi, osph, osphc, cull); return; }
   i -= ns;
-  if (i < na) {
-    art_aabb a = aabb[i];
-    AabbCold c;
-    c.cx = f16tof32(a.center.x); c.cy = f16tof32(a.center.y); c.cz = f16tof32(a.center.z);
-    c.hx = f16tof32(a.size.x); c.hy = f16tof32(a.size.y); c.hz = f16tof32(a.size.z);
-    c.density = f16tof32(a.material.density);
-    c.absorption = f16tof32(a.material.absorption);
-    c.echo = f16tof32(a.material.echo);
-    c.pad0 = c.pad1 = c.pad2 = 0.0f;
-    AabbRec r;
-    r.mnx = c.cx - c.hx; r.mny = c.cy - c.hy; r.mnz = c.cz - c.hz;
-    r.mxx = c.cx + c.hx; r.mxy = c.cy + c.hy; r.mxz = c.cz + c.hz;
-    r.tid = a.audio_target_id;
-    r.pad = 0.0f;
-    oaabb[i] = r;
-    oaabbc[i] = c;
-    cull[gi] = make_cull(fminf(r.mnx, r.mxx), fminf(r.mny, r.mxy), fminf(r.mnz, r.mxz), fmaxf(r.mnx, r.mxx),
-                         fmaxf(r.mny, r.mxy), fmaxf(r.mnz, r.mxz),
-                         fabsf(c.cx) + fabsf(c.cy) + fabsf(c.cz) + fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz), kCullBox);
+  if (i < na) { prep_aabb(aabb[i], i, gi, oaabb, oaabbc, cull); return; }
+  i -= na;
+  if (i < no) prep_obb(obb[i], i, gi, oobb, oobbc, cull);
+}
+
+// Resident collider store (include/art_colliders.h): each dirty record is written to the
+// resident AoS list at its index and decoded in place; the bounds use the synced counts.
+__global__ void scatter_prep_kernel(const int* __restrict__ idx_s, const art_sphere* __restrict__ rec_s, int ds,
+                                    const int* __restrict__ idx_a, const art_aabb* __restrict__ rec_a, int da,
+                                    const int* __restrict__ idx_o, const art_obb* __restrict__ rec_o, int dob,
+                                    art_sphere* __restrict__ sph, art_aabb* __restrict__ aabb, art_obb* __restrict__ obb,
+                                    int ns, int na, SphereRec* __restrict__ osph, SphereCold* __restrict__ osphc,
+                                    AabbRec* __restrict__ oaabb, AabbCold* __restrict__ oaabbc, ObbRec* __restrict__ oobb,
+                                    ObbCold* __restrict__ oobbc, CullRec* __restrict__ cull) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < ds) {
+    const int i = idx_s[j];
+    const art_sphere r = rec_s[j];
+    sph[i] = r;
+    prep_sphere(r, i, i, osph, osphc, cull);
     return;
   }
-  i -= na;
-  if (i < no) {
-    art_obb b = obb[i];
-    ObbRec r;
-    ObbCold c;
-    r.cx = f16tof32(b.center.x); r.cy = f16tof32(b.center.y); r.cz = f16tof32(b.center.z);
-    c.hx = f16tof32(b.size.x); c.hy = f16tof32(b.size.y); c.hz = f16tof32(b.size.z);
-    r.lmnx = 0.0f - c.hx; r.lmny = 0.0f - c.hy; r.lmnz = 0.0f - c.hz;
-    r.lmxx = 0.0f + c.hx; r.lmxy = 0.0f + c.hy; r.lmxz = 0.0f + c.hz;
-    r.pad0 = r.pad1 = 0.0f;
-    quat q = half_quaternion_value(b.rot_x, b.rot_y, b.rot_z);
-    quat qi = qinverse(q);
-    r.qx = q.x; r.qy = q.y; r.qz = q.z; r.qw = q.w;
-    c.iqx = qi.x; c.iqy = qi.y; c.iqz = qi.z; c.iqw = qi.w;
-    r.tid = b.audio_target_id;
-    c.density = f16tof32(b.material.density);
-    c.absorption = f16tof32(b.material.absorption);
-    c.echo = f16tof32(b.material.echo);
-    c.pad0 = c.pad1 = 0.0f;
-    oobb[i] = r;
-    oobbc[i] = c;
-    // bounding sphere of the box (|h|_1 >= |h|_2), whatever the rotation
-    const float rho = (fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz)) * 1.001f;
-    const bool qok = isfinite(q.x) && isfinite(q.y) && isfinite(q.z) && isfinite(q.w);
-    cull[gi] = make_cull(r.cx - rho, r.cy - rho, r.cz - rho, r.cx + rho, r.cy + rho, r.cz + rho,
-                         qok ? fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + rho : INFINITY, kCullObb);
+  j -= ds;
+  if (j < da) {
+    const int i = idx_a[j];
+    const art_aabb r = rec_a[j];
+    aabb[i] = r;
+    prep_aabb(r, i, ns + i, oaabb, oaabbc, cull);
+    return;
+  }
+  j -= da;
+  if (j < dob) {
+    const int i = idx_o[j];
+    const art_obb r = rec_o[j];
+    obb[i] = r;
+    prep_obb(r, i, ns + na + i, oobb, oobbc, cull);
   }
 }
 
@@ -550,6 +590,16 @@ void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, co
   if (n == 0) return;
   hipLaunchKernelGGL(prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sph, ns, aabb, na, obb, no, osph, osphc, oaabb,
                      oaabbc, oobb, oobbc, cull);
+}
+
+void launch_scatter_prep(const int* idx_s, const art_sphere* rec_s, int ds, const int* idx_a, const art_aabb* rec_a,
+                         int da, const int* idx_o, const art_obb* rec_o, int dob, art_sphere* sph, art_aabb* aabb,
+                         art_obb* obb, int ns, int na, SphereRec* osph, SphereCold* osphc, AabbRec* oaabb,
+                         AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc, CullRec* cull, hipStream_t st) {
+  const int n = ds + da + dob;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scatter_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, idx_s, rec_s, ds, idx_a, rec_a, da,
+                     idx_o, rec_o, dob, sph, aabb, obb, ns, na, osph, osphc, oaabb, oaabbc, oobb, oobbc, cull);
 }
 
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,

@@ -11,7 +11,8 @@ import art
 from art import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("art.h", "art_device.h", "art_synth.h", "art_dsp.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("art.h", "art_device.h", "art_synth.h", "art_dsp.h",
+                                                                 "art_colliders.h")]
 
 
 def declared_symbols():
