@@ -189,6 +189,7 @@ SIGNATURES = {
     "art_dsp_source_params_get": (I32, [C.POINTER(art_spatializer_settings), C.POINTER(art_audio_source), I32,
                                         C.POINTER(art_dsp_source_params)]),
     "art_dsp_process_device": (I32, [VP, VP, VP, VP, I32, I32, VP]),
+    "art_fibonacci_directions_device": (I32, [VP, I32, VP, VP]),
     # art_colliders.h
     "art_collider_add": (I32, [VP, I32, VP, C.POINTER(I32)]),
     "art_collider_set": (I32, [VP, I32, I32, VP]),

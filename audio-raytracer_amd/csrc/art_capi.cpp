@@ -884,6 +884,16 @@ ART_API int art_count_device(art_ctx* c, const float* d_origins, int32_t fan_cou
   return launch_common(c, d_origins, fan_count, d_block, out_flags, stream, true, out);
 }
 
+ART_API int art_fibonacci_directions_device(art_ctx* c, int32_t count, art_half3* d_out, void* stream) {
+  if (!c) return ART_E_INVALID;
+  if (count < 0 || (count > 0 && !d_out)) return fail(c, ART_E_INVALID, "art_fibonacci_directions_device: bad arguments");
+  if (count == 0) return ART_OK;
+  HIP_TRY(c, hipSetDevice(c->devs[0].id));
+  launch_fibonacci(count, d_out, static_cast<hipStream_t>(stream));
+  HIP_TRY(c, hipGetLastError());
+  return ART_OK;
+}
+
 ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
   if (!c || !out) return ART_E_INVALID;
   memset(out, 0, sizeof *out);

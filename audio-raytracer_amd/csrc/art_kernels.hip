@@ -592,6 +592,32 @@ void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, co
                      oaabbc, oobb, oobbc, cull);
 }
 
+// FibonacciDirectionsJobParallel.Execute (Jobs/FibonacciDirectionsJobParallel.cs:15-35), one lane
+// per ray. The float operations are the reference's (and art_fibonacci_directions' on the host);
+// cos/sin are evaluated in double and rounded to float, which gives the correctly rounded float
+// values that the host libm's cosf/sinf return on these arguments (tests/test_dirs_gpu.py).
+__global__ void fibonacci_kernel(int count, art_half3* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const float phi = 3.14159265f * (3.0f - sqrtf(5.0f));
+  const float y = 1.0f - ((float)i / (float)(count - 1)) * 2.0f;
+  const float radius = sqrtf(1.0f - y * y);
+  const float theta = phi * (float)i;
+  const float x = (float)cos((double)theta) * radius;
+  const float z = (float)sin((double)theta) * radius;
+  // count == 1 divides 0 by 0. The reference runs on x86, whose default NaN has the sign bit set
+  // (half 0xFE00, as the host generator produces); the GPU's is positive, so NaNs are canonicalized.
+  auto h16 = [](float v) -> uint16_t { return v != v ? (uint16_t)0xFE00u : f32tof16(v); };
+  art_half3 h;
+  h.x = h16(x); h.y = h16(y); h.z = h16(z);
+  out[i] = h;
+}
+
+void launch_fibonacci(int count, art_half3* out, hipStream_t st) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(fibonacci_kernel, dim3((count + 255) / 256), dim3(256), 0, st, count, out);
+}
+
 void launch_scatter_prep(const int* idx_s, const art_sphere* rec_s, int ds, const int* idx_a, const art_aabb* rec_a,
                          int da, const int* idx_o, const art_obb* rec_o, int dob, art_sphere* sph, art_aabb* aabb,
                          art_obb* obb, int ns, int na, SphereRec* osph, SphereCold* osphc, AabbRec* oaabb,

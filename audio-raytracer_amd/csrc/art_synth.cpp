@@ -64,14 +64,18 @@ extern "C" {
 ART_API uint16_t art_f32tof16(float x) { return f32tof16(x); }
 ART_API float art_f16tof32(uint16_t h) { return f16tof32(h); }
 
+// FibonacciDirectionsJobParallel.Execute (Jobs/FibonacciDirectionsJobParallel.cs:15-35). cos/sin are
+// evaluated in double and rounded to float (the correctly rounded float values), exactly as
+// fibonacci_kernel does on the device, so host and device directions are identical; glibc's
+// cosf/sinf (the oracle's) differ from them in a few arguments per million.
 ART_API void art_fibonacci_directions(int32_t count, art_half3* out) {
   for (int32_t i = 0; i < count; ++i) {
     float phi = 3.14159265f * (3.0f - std::sqrt(5.0f));
     float y = 1.0f - ((float)i / (float)(count - 1)) * 2.0f;
     float radius = std::sqrt(1.0f - y * y);
     float theta = phi * (float)i;
-    float x = std::cos(theta) * radius;
-    float z = std::sin(theta) * radius;
+    float x = (float)std::cos((double)theta) * radius;
+    float z = (float)std::sin((double)theta) * radius;
     out[i] = h3(x, y, z);
   }
 }

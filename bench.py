@@ -54,8 +54,10 @@ def parse():
     p.add_argument("--collider-scale", type=float, default=None,
                    help="scale the config's collider count (experiments only; the metric is quoted at 1)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU-baseline sample")
-    p.add_argument("--path", choices=("raytrace", "dsp"), default="raytrace",
-                   help="raytrace: the headline metric; dsp: the per-sample spatializer DSP (SURVEY.md 8 f rank 1)")
+    p.add_argument("--path", choices=("raytrace", "dsp", "dirs"), default="raytrace",
+                   help="raytrace: the headline metric; dsp: the per-sample spatializer DSP (SURVEY.md 8 f rank 1); "
+                        "dirs: Fibonacci ray directions on the device (rank 3)")
+    p.add_argument("--dirs-count", type=int, default=1 << 24, help="directions per launch (dirs path)")
     p.add_argument("--dsp-frames", type=int, default=1024, help="frames per OnAudioFilterRead buffer (dsp path)")
     p.add_argument("--dsp-batch", type=int, default=65536, help="sources of the large-batch roofline run (dsp path)")
     p.add_argument("--dsp-sort", action="store_true",
@@ -255,10 +257,57 @@ def main_dsp(a):
         dist.destroy_process_group()
 
 
+def main_dirs(a):
+    """FibonacciDirectionsJobParallel on the device (art_fibonacci_directions_device): one step =
+    one launch generating --dirs-count half3 directions in HBM. Single GPU (an init-time step)."""
+    torch.cuda.set_device(0)
+    n = a.dirs_count
+    ctx = art.Context(1)
+    d = torch.empty(n * 3, dtype=torch.int16, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    for _ in range(a.warmup):
+        assert ctx.lib.art_fibonacci_directions_device(ctx.ptr, n, d.data_ptr(), sp) == 0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(a.steps):
+        ctx.lib.art_fibonacci_directions_device(ctx.ptr, n, d.data_ptr(), sp)
+    e1.record()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    k_ms = e0.elapsed_time(e1) / a.steps
+    gbs = n * 6 / (k_ms * 1e-3) / 1e9  # 6 B (half3) written per direction, nothing read
+    cpu = None
+    if not a.no_cpu_baseline:
+        m = min(n, 1 << 20)
+        host = np.zeros((m, 3), np.uint16)
+        reps, t1 = 0, time.perf_counter()
+        while True:
+            art.load_library().art_fibonacci_directions(m, host.ctypes.data)
+            reps += 1
+            cdt = time.perf_counter() - t1
+            if cdt >= min(a.cpu_seconds, 5.0):
+                break
+        cpu = {"value": reps * m / cdt, "unit": "directions/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} x {m} directions ({cdt:.1f} s) through art_fibonacci_directions (host C++, one thread)"}
+    print(json.dumps({
+        "metric": "Fibonacci ray directions/s (FibonacciDirectionsJobParallel)", "value": n * a.steps / dt,
+        "unit": "directions/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{n} directions per launch", "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                     "traffic": None, "kernel": "fibonacci_kernel", "kernel_ms": k_ms,
+                     "note": "6 B written per direction; double-precision cos/sin make it FP64-VALU-heavy"},
+        "cpu_baseline": cpu}))
+
+
 def main():
     a = parse()
     if a.path == "dsp":
         return main_dsp(a)
+    if a.path == "dirs":
+        return main_dirs(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -59,6 +59,11 @@ ART_API int art_scene_bind(art_ctx* ctx, const art_frame_desc* desc);
 ART_API int art_launch_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
                               uint32_t out_flags, void* stream);
 
+/* FibonacciDirectionsJobParallel (Jobs/FibonacciDirectionsJobParallel.cs:15-35) on the device:
+ * d_out = half3[count] in HBM, enqueued on `stream`. Equals art_fibonacci_directions (host) bit
+ * for bit; directions stay an input of art_frame_desc (the half3 bits are the contract). */
+ART_API int art_fibonacci_directions_device(art_ctx* ctx, int32_t count, art_half3* d_out, void* stream);
+
 /* Same frame with the test-counting kernels (for the tests/s metric); synchronizes. */
 ART_API int art_count_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
                              uint32_t out_flags, void* stream, art_test_counts* out);
