@@ -117,6 +117,7 @@ struct Device {
   int wf_blocks = 0;
   int fan_begin = 0, fan_count = 0;
   DevScene sc{};
+  SortBufs sb{};  // buffers of the spatially sorted scene copy (art_bvh.hip), set by upload_scene
   bool bound = false;
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
   std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
@@ -406,6 +407,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sb.obb_s = reinterpret_cast<ObbRec*>(soa + f.soa_obb_s); sb.cull_s = reinterpret_cast<CullRec*>(soa + f.soa_cull_s);
   sb.chunks = reinterpret_cast<CullRec*>(soa + f.soa_chunks);
   sc.sph_s = nullptr; sc.aabb_s = nullptr; sc.obb_s = nullptr; sc.cull_s = nullptr; sc.chunks = nullptr; sc.nchunks = 0;
+  dv.sb = sb;
   if (fast_uses_sorted_scene() && launch_sort_scene(sc, sb, dv.stream) != 0)
     return fail(c, ART_E_DEVICE, "collider sort failed");
   HIP_TRY(c, hipGetLastError());
@@ -1143,6 +1145,11 @@ ART_API int art_colliders_sync(art_ctx* c) {
         dv.sc.aabb = t.aabb; dv.sc.aabbc = t.aabbc; dv.sc.na = t.na;
         dv.sc.obb = t.obb; dv.sc.obbc = t.obbc; dv.sc.no = t.no;
         dv.sc.cull = t.cull;
+        // moved colliders move in the sorted copy too: sort again (device only, no H2D)
+        if (fast_uses_sorted_scene() && nd) {
+          if (launch_sort_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider sort failed");
+          HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));  // device-path launches wait for the sort too
+        }
       }
     }
   }

@@ -15,6 +15,8 @@
 // point into a small solid angle and their visibility sweeps end together; every output is
 // written at the ray's own index, so the order changes no result.
 // This kernel does not count tests; the test-count metric comes from raytrace_kernel<COUNT>.
+#include <hipcub/hipcub.hpp>
+
 #include "art_device_fns.hpp"
 
 namespace art {
@@ -216,6 +218,74 @@ __device__ __forceinline__ bool cone_candidate(const WaveCone& wc, const CullRec
   const float cos_lim = wc.cos_t * cb - wc.sin_t * sb;  // cos(theta + beta), theta + beta < pi
   // slack (1e-4 L) only ever admits more colliders: cos_lim <= 1 and the threshold is lowered
   return vx * wc.ax + vy * wc.ay + vz * wc.az >= (cos_lim - 1e-4f) * L;
+}
+
+// Visibility cone of a wave of segments [o, o + maxd d] that (nearly) share their END point: the
+// muffle rays of one target end at the target (:165), the echo rays of one fan at its origin
+// (:130). Apex A = the first valid lane's computed end point; every lane's end point lies within
+// `extra` of A (its computed distance, widened for the rounding of o + maxd d), so each segment
+// lies in the hull of its start o and the ball (A, extra), and that hull lies in cone(A, axis,
+// theta) (+) ball(extra) once o is inside the cone. Starts inside the ball need no cone. A wave
+// with a non-finite segment, whose starts all lie in the ball, or whose cone is wider than a
+// half-space, is not cone-culled (on = false). theta carries the 2e-3 rad slack of make_cone.
+struct VisCone {
+  float ax, ay, az;       // apex
+  float nx, ny, nz;       // unit axis
+  float cos2, sin_t;      // cos^2 and sin of the half-angle
+  float extra;            // apex ball radius
+  bool on;
+};
+
+__device__ __forceinline__ VisCone make_vis_cone(const Seg& s, float maxd, bool valid, float om) {
+  VisCone vc;
+  const vec3 e = s.o + s.d * maxd;
+  const unsigned long long vm = __ballot(valid);
+  const int first = vm ? (int)__builtin_ctzll(vm) : 0;
+  vc.ax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.x), first));
+  vc.ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.y), first));
+  vc.az = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.z), first));
+  const float ex = e.x - vc.ax, ey = e.y - vc.ay, ez = e.z - vc.az;
+  const float re = sqrtf(ex * ex + ey * ey + ez * ez);
+  vc.extra = wave_max(valid ? re : 0.0f) * 1.001f + 1e-6f * om + 1e-6f;
+  const float vx = s.o.x - vc.ax, vy = s.o.y - vc.ay, vz = s.o.z - vc.az;
+  const float l2 = vx * vx + vy * vy + vz * vz;
+  const float l = sqrtf(l2);
+  const bool fin = isfinite(l2) && isfinite(re) && isfinite(maxd) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z);
+  const bool use = valid && fin && l > vc.extra;
+  const float inv = use ? 1.0f / l : 0.0f;
+  const float ux = vx * inv, uy = vy * inv, uz = vz * inv;
+  const float sx = wave_sum(ux), sy = wave_sum(uy), sz = wave_sum(uz);
+  const float sn = sqrtf(sx * sx + sy * sy + sz * sz);
+  vc.nx = 1.0f; vc.ny = 0.0f; vc.nz = 0.0f; vc.cos2 = 0.0f; vc.sin_t = 1.0f; vc.on = false;
+  if (!(sn > 0.0f) || __any(valid && !fin) || !isfinite(vc.extra)) return vc;
+  vc.nx = sx / sn; vc.ny = sy / sn; vc.nz = sz / sn;
+  float c = wave_min(use ? ux * vc.nx + uy * vc.ny + uz * vc.nz : INFINITY);
+  c = fminf(c, 1.0f);
+  const float s0 = sqrtf(fmaxf(0.0f, 1.0f - c * c));
+  constexpr float ce = 0.999998f, se = 0.002f;  // cos / sin of the slack angle
+  const float cos_t = c * ce - s0 * se;
+  vc.sin_t = s0 * ce + c * se;
+  vc.cos2 = cos_t * cos_t;
+  vc.on = cos_t > 0.0f;
+  return vc;
+}
+
+// Does the collider's widened bounding sphere (centre c, radius rho) meet cone (+) ball(extra)?
+// Distance from c to the cone's lateral surface is perp cos(theta) - proj sin(theta) (negative
+// inside; for c behind the apex it is at most |c - A|, so the test only over-admits there):
+// candidate iff perp cos <= rho' + proj sin =: rhs, evaluated squared (no sqrt or division) with
+// an absolute slack of 1e-6 |c - A|^2 for the cancellation in perp^2 = |v|^2 - proj^2. Non-finite
+// bounds give NaN/inf terms, which every comparison below admits.
+__device__ __forceinline__ bool vis_cone_cand(const VisCone& vc, const CullRec& cr, float om) {
+  const float cx = 0.5f * (cr.lox + cr.hix), cy = 0.5f * (cr.loy + cr.hiy), cz = 0.5f * (cr.loz + cr.hiz);
+  const float rho = 0.5f * ((cr.hix - cr.lox) + (cr.hiy - cr.loy) + (cr.hiz - cr.loz)) * 1.001f +
+                    cr.factor * (cr.scale + om) + vc.extra;
+  const float vx = cx - vc.ax, vy = cy - vc.ay, vz = cz - vc.az;
+  const float l2 = vx * vx + vy * vy + vz * vz;
+  const float pj = vx * vc.nx + vy * vc.ny + vz * vc.nz;
+  const float rhs = rho + pj * vc.sin_t;
+  const float perp2 = l2 - pj * pj;
+  return !(rhs < 0.0f) && !(perp2 * vc.cos2 > rhs * rhs + 1e-6f * l2);
 }
 
 // Front-to-back nearest hit over the spatially sorted chunks for rays sharing their origin O (the
@@ -816,10 +886,15 @@ __device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet&
 }
 
 // Broad-phase any-hit sweep of one lane's segment (s, maxd, owner) for a wave of up to 64
-// segments (`valid` lanes): the wave's segment box, then per chunk the bound ballot and the exact
-// tests of the candidates. Returns the lane's verdict (true = blocked).
+// segments (`valid` lanes): the wave's segment box (and, for vis_kernel, the visibility cone of
+// make_vis_cone), then per chunk the bound ballot and the exact tests of the candidates. Flat:
+// every chunk of [c_lo, c_hi) in reference order. Two-level (`two`, needs the spatially sorted
+// scene of art_bvh.hip): chunks [c_lo, c_hi) of the sorted order are tested as a whole first
+// (lane = chunk, union bounds), then the members of the candidate chunks. Any-hit is an OR over
+// the colliders, so the order is free. Returns the lane's verdict (true = blocked).
 __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid, int lane,
-                                           unsigned long long* ex, bool done_in = false, int c_lo = 0, int c_hi = 1 << 30) {
+                                           unsigned long long* ex, bool done_in = false, int c_lo = 0, int c_hi = 1 << 30,
+                                           const VisCone* vc = nullptr, bool two = false) {
   const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
   const int nchunks = min(cm.total(), c_hi);
   if (c_lo >= nchunks) return false;
@@ -839,16 +914,43 @@ __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, flo
   const bool done = !valid || done_in;
   if (__all(done)) return false;
   unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
-  // chunk c: type, first sorted index within the type, member count; returns the global sorted index
+  // broad-phase candidate: widened bounds meet the wave box (and the cone)
+  auto candidate = [&](const CullRec& cr) {
+    const float m = cr.factor * (cr.scale + wb.om);
+    bool c = (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) & (cr.hiy + m >= wb.ly) &
+             (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
+    if (vc && vc->on && __any(c)) c = c && vis_cone_cand(*vc, cr, wb.om);
+    return c;
+  };
+  // chunk c: type, first (sorted) index within the type, member count; returns the global index
   auto chunk_at = [&](int c, int& type, int& b, int& n) {
     if (c < cm.cs) { type = 0; b = c * kChunk; n = min(kChunk, sc.ns - b); return b; }
     if (c - cm.cs < cm.ca) { type = 1; b = (c - cm.cs) * kChunk; n = min(kChunk, sc.na - b); return sc.ns + b; }
     type = 2; b = (c - cm.cs - cm.ca) * kChunk; n = min(kChunk, sc.no - b);
     return sc.ns + sc.na + b;
   };
-  if (!ART_FAST_TWO_LEVEL || sc.nchunks <= 64) {
-    // Flat: every chunk's members against the wave box (original order; the bounds of chunk c + 1
-    // are loaded while chunk c's candidates are tested).
+  // exact tests of one chunk's candidates (records `sph`/`aabb`/`obb`: reference or sorted order)
+  auto test_chunk = [&](int type, int b, CandSet& cs, const SphereRec* sph, const AabbRec* aabb, const ObbRec* obb) {
+    if (type == 0) {
+      blocked = test_candidates<kCullU>(sph, b, cs, blocked, done, [&](const SphereRec& r) {
+        float d;
+        return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
+      }, nt[0]);
+    } else if (type == 1) {
+      blocked = test_candidates<kCullU>(aabb, b, cs, blocked, done, [&](const AabbRec& r) {
+        float d;
+        return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
+      }, nt[1]);
+    } else {
+      blocked = test_candidates<1>(obb, b, cs, blocked, done, [&](const ObbRec& r) {
+        float d;
+        return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+      }, nt[2]);
+    }
+  };
+  if (!two) {
+    // Flat: every chunk's members (the bounds of chunk c + 1 are loaded while chunk c's candidates
+    // are tested).
     CullRec nxt;
     {
       int t0, b0, n0;
@@ -864,99 +966,45 @@ __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, flo
         const int g1 = chunk_at(c + 1, t1, b1, n1);
         nxt = sc.cull[g1 + min(lane, n1 - 1)];
       }
-      const float m = cr.factor * (cr.scale + wb.om);
-      const bool cand = (lane < n) & (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) &
-                        (cr.hiy + m >= wb.ly) & (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
       CandSet cs;
-      cs.m[0] = __ballot(cand);
+      cs.m[0] = __ballot((lane < n) && candidate(cr));
       cs.left = __popcll(cs.m[0]);
       ++nchk;
 #ifdef ART_DIAG_CULL_STATS
       if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
 #endif
       if (cs.left == 0) continue;
-      if (type == 0) {
-        blocked = test_candidates<kCullU>(sc.sph, b, cs, blocked, done, [&](const SphereRec& r) {
-          float d;
-          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[0]);
-      } else if (type == 1) {
-        blocked = test_candidates<kCullU>(sc.aabb, b, cs, blocked, done, [&](const AabbRec& r) {
-          float d;
-          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[1]);
-      } else {
-        blocked = test_candidates<1>(sc.obb, b, cs, blocked, done, [&](const ObbRec& r) {
-          float d;
-          return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
-        }, nt[2]);
-      }
+      test_chunk(type, b, cs, sc.sph, sc.aabb, sc.obb);
       if (__all(blocked || done)) break;
     }
-    exec_add(ex, kExecSphere, 64ull * nt[0]);
-    exec_add(ex, kExecAabb, 64ull * nt[1]);
-    exec_add(ex, kExecObb, 64ull * nt[2]);
-    exec_add(ex, kExecCullBox, 64ull * nchk);
-    return blocked;
-  }
-#if ART_FAST_TWO_LEVEL
-  // Two levels over the spatially sorted colliders (art_bvh.hip): the chunks' union bounds
-  // (lane = chunk, 64 per pass), then the members of the candidate chunks (lane = collider).
-  for (int pb = c_lo; pb < nchunks; pb += 64) {
-    const int pc = pb + lane;
-    bool ccand = false;
-    if (pc < nchunks) {
-      const CullRec cr = sc.chunks[pc];
-      const float m = cr.factor * (cr.scale + wb.om);
-      ccand = (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) & (cr.hiy + m >= wb.ly) &
-              (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
-    }
-    unsigned long long cm_mask = __ballot(ccand);
-    while (cm_mask) {
-      const int c = pb + (int)__builtin_ctzll(cm_mask);
-      cm_mask &= cm_mask - 1;
-      int type, b, n;
-      const int g = chunk_at(c, type, b, n);
-      bool cand = false;
-      if (lane < n) {
-        const CullRec cr = sc.cull_s[g + lane];
-        const float m = cr.factor * (cr.scale + wb.om);
-        cand = (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) & (cr.hiy + m >= wb.ly) &
-               (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
-      }
-      CandSet cs;
-      cs.m[0] = __ballot(cand);
-      cs.left = __popcll(cs.m[0]);
+  } else {
+    for (int pb = c_lo; pb < nchunks; pb += 64) {
+      const int pc = pb + lane;
+      bool ccand = false;
+      if (pc < nchunks) ccand = candidate(sc.chunks[pc]);
+      unsigned long long cm_mask = __ballot(ccand);
       ++nchk;
+      while (cm_mask) {
+        const int c = pb + (int)__builtin_ctzll(cm_mask);
+        cm_mask &= cm_mask - 1;
+        int type, b, n;
+        const int g = chunk_at(c, type, b, n);
+        bool cand = false;
+        if (lane < n) cand = candidate(sc.cull_s[g + lane]);
+        CandSet cs;
+        cs.m[0] = __ballot(cand);
+        cs.left = __popcll(cs.m[0]);
+        ++nchk;
 #ifdef ART_DIAG_CULL_STATS
-      if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
+        if (lane == 0) { atomicAdd(&g_diag[1], 1u); atomicAdd(&g_diag[2], (unsigned)cs.left); }
 #endif
-#ifdef ART_DIAG_CULL_ONLY  // diagnostic build only: broad phase without the exact tests
-      blocked |= (cs.left == -1);
-      continue;
-#endif
-      if (cs.left == 0) continue;
-      if (type == 0) {
-        blocked = test_candidates<kCullU>(sc.sph_s, b, cs, blocked, done, [&](const SphereRec& r) {
-          float d;
-          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[0]);
-      } else if (type == 1) {
-        blocked = test_candidates<kCullU>(sc.aabb_s, b, cs, blocked, done, [&](const AabbRec& r) {
-          float d;
-          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[1]);
-      } else {
-        blocked = test_candidates<1>(sc.obb_s, b, cs, blocked, done, [&](const ObbRec& r) {
-          float d;
-          return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
-        }, nt[2]);
+        if (cs.left == 0) continue;
+        test_chunk(type, b, cs, sc.sph_s, sc.aabb_s, sc.obb_s);
+        if (__all(blocked || done)) break;
       }
       if (__all(blocked || done)) break;
     }
-    if (__all(blocked || done)) break;
   }
-#endif
   exec_add(ex, kExecSphere, 64ull * nt[0]);
   exec_add(ex, kExecAabb, 64ull * nt[1]);
   exec_add(ex, kExecObb, 64ull * nt[2]);
@@ -1018,6 +1066,36 @@ constexpr uint32_t kPairMuffle = 1u << 16;
 #define ART_VIS_RANGES 8
 #endif
 constexpr int kVisRanges = ART_VIS_RANGES;  // chunk ranges per 64-pair batch (work items)
+#ifndef ART_VIS_SORT
+#define ART_VIS_SORT 1  // visibility batches in (target, direction from the target) order (vis_sort_key)
+#endif
+#ifndef ART_VIS_TWO_LEVEL
+#define ART_VIS_TWO_LEVEL 1  // vis_kernel walks the sorted scene's chunk bounds first (art_bvh.hip)
+#endif
+#ifndef ART_VIS_CONE
+#define ART_VIS_CONE 1  // cone broad phase around the batch's shared end point (make_vis_cone)
+#endif
+
+// Sort key of a visibility pair: muffle rays of target t by the octahedral Morton cell (64 x 64)
+// of their direction seen from the target, so 64 consecutive sorted pairs form a thin cone with
+// apex t; echo rays keep their emission order (one key, stable sort) after them. 0xFFFF marks an
+// unused slot.
+constexpr uint16_t kKeyEcho = 0xFFFE, kKeyUnused = 0xFFFF;
+__device__ __forceinline__ uint16_t vis_sort_key(int t, vec3 u) {
+  const float n = fabsf(u.x) + fabsf(u.y) + fabsf(u.z);
+  float a = 0.0f, c = 0.0f;
+  if (n > 0.0f && isfinite(n)) {
+    const float x = u.x / n, y = u.y / n, z = u.z / n;
+    a = z < 0.0f ? (1.0f - fabsf(y)) * (x >= 0.0f ? 1.0f : -1.0f) : x;
+    c = z < 0.0f ? (1.0f - fabsf(x)) * (y >= 0.0f ? 1.0f : -1.0f) : y;
+  }
+  auto q6 = [](float v) { return (uint32_t)fminf(fmaxf((v + 1.0f) * 32.0f, 0.0f), 63.0f); };
+  auto sp = [](uint32_t v) {  // 6 bits -> even bit positions
+    v = (v | (v << 4)) & 0x0F0Fu; v = (v | (v << 2)) & 0x3333u; v = (v | (v << 1)) & 0x5555u;
+    return v;
+  };
+  return (uint16_t)(((uint32_t)t << 12) | sp(q6(a)) | (sp(q6(c)) << 1));
+}
 
 // Work item i of vis_kernel = (chunk range r, batch b), range-major: r = i / nb_max, b = i % nb_max.
 // A batch's later ranges usually start after its earlier ones finished and skip the pairs those
@@ -1026,7 +1104,7 @@ constexpr int kVisRanges = ART_VIS_RANGES;  // chunk ranges per 64-pair batch (w
 // vis_finalize writes the outputs after the kernel boundary.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
 void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restrict__ count, uint32_t nb_max,
-                uint8_t* __restrict__ block, uint32_t* __restrict__ muffle_acc, unsigned long long* ex) {
+                const uint32_t* __restrict__ order, unsigned long long* ex) {
   const int lane = threadIdx.x & 63;
   const uint32_t np = ldc(count, 0);
   const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1034,7 +1112,9 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
   const uint32_t base = b * 64u;
   if (r >= (uint32_t)kVisRanges || base >= np) return;
   const uint32_t p = base + lane;
-  PairG& gp = pairs[p < np ? p : base];
+  // batch b = 64 consecutive pairs of the sorted order (pairs of one target by direction from it)
+  const uint32_t pi = order ? order[p < np ? p : base] : (p < np ? p : base);
+  PairG& gp = pairs[pi];
   // pairs an earlier range already blocked are skipped (not loaded, and out of the wave's box)
 #if ART_VIS_PLAIN_FLAG
   // plain load: a stale 0 (another XCD's verdict not yet visible) only repeats work
@@ -1056,8 +1136,15 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
     maxd = q2.z; owner = __float_as_int(q2.w);
   }
   const int nch = (sc.ns + kChunk - 1) / kChunk + (sc.na + kChunk - 1) / kChunk + (sc.no + kChunk - 1) / kChunk;
+  const bool two = sc.chunks != nullptr && (ART_VIS_TWO_LEVEL || (ART_FAST_TWO_LEVEL && sc.nchunks > 64));
   const int c_lo = (int)(((long long)nch * r) / kVisRanges), c_hi = (int)(((long long)nch * (r + 1)) / kVisRanges);
-  const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi);
+#if ART_VIS_CONE
+  const float om = wave_max(valid ? fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd : 0.0f);
+  const VisCone vc = make_vis_cone(s, maxd, valid, om);
+  const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, &vc, two);
+#else
+  const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, nullptr, two);
+#endif
   if (valid && blocked) __hip_atomic_fetch_or(&gp.pad0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1117,7 +1204,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                const int* __restrict__ ray_order,
                                                                uint32_t* __restrict__ work,
                                                                PairG* __restrict__ pairs,
-                                                               uint32_t* __restrict__ pair_count) {
+                                                               uint32_t* __restrict__ pair_count,
+                                                               uint16_t* __restrict__ pkeys,
+                                                               uint32_t* __restrict__ pvals) {
   __shared__ float s_dist[K][64];
   __shared__ float s_best[K][64];  // running per-lane best of each wave (front-to-back pruning)
   (void)s_best;
@@ -1291,7 +1380,12 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
             r.ox = g.o.x; r.oy = g.o.y; r.oz = g.o.z; r.dx = g.d.x; r.dy = g.d.y; r.dz = g.d.z;
             r.ix = g.inv.x; r.iy = g.inv.y; r.iz = g.inv.z; r.a2 = g.a2; r.maxd = maxd;
             r.pad0 = r.pad1 = 0u;
-            pairs[pos + (uint32_t)__popcll(mq[q] & lt)] = r;
+            const uint32_t at = pos + (uint32_t)__popcll(mq[q] & lt);
+            pairs[at] = r;
+            if (pkeys) {
+              pkeys[at] = q == 0 ? kKeyEcho : vis_sort_key(q - 1, mk3(-qdir.x, -qdir.y, -qdir.z));
+              pvals[at] = at;
+            }
           }
           pos += (q <= T) ? (uint32_t)__popcll(mq[q]) : 0u;
         }
@@ -1471,22 +1565,23 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
 template <int K, bool HITS, int U, int WPE, bool MULTI>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
-                           uint32_t* pair_count, hipStream_t st) {
+                           uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
   const size_t lds = fast_lds_bytes(sc, fp.T);
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   const int resident = resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI>, 64 * K, lds);
   const int nblk = (int)std::min<long long>(groups, resident);
   hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
-                     muffle_acc, ray_order, work, pairs, pair_count);
+                     muffle_acc, ray_order, work, pairs, pair_count, pkeys, pvals);
 }
 
 template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
-                          uint32_t* pair_count, hipStream_t st) {
+                          uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
   // instantiation by scene kind (OBBs or not), hit outputs, and one or several hits per ray
 #define ART_LAUNCH(H_, U_, W_, M_) \
-  launch_fast_kh<K, H_, U_, W_, M_>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st)
+  launch_fast_kh<K, H_, U_, W_, M_>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, \
+                                    pvals, st)
   const bool multi = fp.H > 1;
   if (sc.no > 0) {
     if (L.has_hits) { if (multi) ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, true); else ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, false); }
@@ -1498,29 +1593,79 @@ static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLa
 #undef ART_LAUNCH
 }
 
-bool fast_uses_sorted_scene() { return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST; }
+bool fast_uses_sorted_scene() { return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST || (ART_FAST_SPLIT && ART_VIS_TWO_LEVEL); }
+
+// Pair buffer: PairG[max] | sort keys in/out u16[max] | pair indices in/out u32[max] | hipcub temp.
+struct PairBufs {
+  PairG* pairs;
+  uint16_t *keys, *keys_s;
+  uint32_t *vals, *order;
+  void* temp;
+  size_t temp_bytes, total;
+};
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+static PairBufs pair_bufs(void* base, size_t max_pairs) {
+  PairBufs b{};
+  uint8_t* p = static_cast<uint8_t*>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { uint8_t* q = p ? p + off : nullptr; off += align256(bytes); return q; };
+  b.pairs = reinterpret_cast<PairG*>(take(max_pairs * sizeof(PairG)));
+  if (ART_VIS_SORT && max_pairs) {
+    b.keys = reinterpret_cast<uint16_t*>(take(max_pairs * 2));
+    b.keys_s = reinterpret_cast<uint16_t*>(take(max_pairs * 2));
+    b.vals = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
+    b.order = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
+    static thread_local size_t last_n = 0, last_tb = 0;  // the size query is per item count
+    if (last_n != max_pairs) {
+      size_t tb = 0;
+      if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint16_t*)nullptr, (uint16_t*)nullptr,
+                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)max_pairs, 0, 16) != hipSuccess)
+        tb = 0;
+      last_n = max_pairs;
+      last_tb = tb;
+    }
+    const size_t tb = last_tb;
+    b.temp_bytes = tb;
+    b.temp = take(tb);
+  }
+  b.total = off;
+  return b;
+}
+
+static size_t max_pairs_of(const FrameParams& fp) { return (size_t)fp.S * fp.R * fp.H * (fp.T + 1); }
 
 size_t fast_pair_bytes(const FrameParams& fp) {
-  return ART_FAST_SPLIT ? (size_t)fp.S * fp.R * fp.H * (fp.T + 1) * sizeof(PairG) : 0;
+  return ART_FAST_SPLIT ? pair_bufs(nullptr, max_pairs_of(fp)).total : 0;
 }
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,
                           uint32_t* pair_count, hipStream_t st) {
   if (fp.S == 0) return;
-  PairG* pairs = static_cast<PairG*>(pair_buf);
+  const size_t max_pairs = max_pairs_of(fp);
+  const PairBufs pb = pair_bufs(ART_FAST_SPLIT ? pair_buf : nullptr, ART_FAST_SPLIT ? max_pairs : 0);
+  const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && max_pairs && pb.temp_bytes && max_pairs < (1u << 31);
+  static_assert(kKeyUnused == 0xFFFF, "unused slots are cleared with byte 0xFF");
+  if (sorted) (void)hipMemsetAsync(pb.keys, 0xFF, max_pairs * 2, st);  // unused slots sort last
+  uint16_t* pkeys = sorted ? pb.keys : nullptr;
+  uint32_t* pvals = sorted ? pb.vals : nullptr;
   switch (fast_split(fp.S, fp.R)) {
-    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
-    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, st); break;
+    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st); break;
+    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st); break;
   }
 #if ART_FAST_SPLIT
-  const size_t max_pairs = (size_t)fp.S * fp.R * fp.H * (fp.T + 1);
   const uint32_t nb_max = (uint32_t)((max_pairs + 63) / 64);
   const size_t items = (size_t)nb_max * kVisRanges;
   if (items) {
-    hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pairs, pair_count, nb_max, block,
-                       muffle_acc, fp.exec);
-    hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pairs, pair_count, block,
+    if (sorted) {
+      size_t tb = pb.temp_bytes;
+      (void)hipcub::DeviceRadixSort::SortPairs(pb.temp, tb, pb.keys, pb.keys_s, pb.vals, pb.order, (int)max_pairs, 0, 16, st);
+    }
+    hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.pairs, pair_count, nb_max,
+                       sorted ? (const uint32_t*)pb.order : nullptr, fp.exec);
+    hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.pairs, pair_count, block,
                        muffle_acc);
   }
 #endif
