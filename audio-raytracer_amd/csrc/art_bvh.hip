@@ -143,9 +143,12 @@ size_t sort_scene_temp_bytes(int n) {
   return bytes;
 }
 
+int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
+
 int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   const int n = sc.ns + sc.na + sc.no;
   sc.nchunks = 0;
+  sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
   if (n == 0) return 0;
   hipLaunchKernelGGL(scene_box_kernel, dim3(1), dim3(1024), 0, st, sc.cull, n, sb.box);
   hipLaunchKernelGGL(morton_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, sc.ns, sc.na, sc.no, sb.box, sb.keys,
@@ -159,6 +162,146 @@ int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   hipLaunchKernelGGL(chunk_bounds_kernel, dim3(nch), dim3(64), 0, st, sb.cull_s, sc.ns, sc.na, sc.no, sb.chunks);
   sc.sph_s = sb.sph_s; sc.aabb_s = sb.aabb_s; sc.obb_s = sb.obb_s; sc.cull_s = sb.cull_s; sc.chunks = sb.chunks;
   sc.nchunks = nch;
+  // the BVH reuses the key / value / temp buffers: stream order puts it after the gather above
+  return fast_uses_bvh() ? launch_build_bvh(sc, sb, st) : 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// BVH for per-lane nearest-hit traversal (raytrace_fast_kernel<..., BVH = true>): all colliders in
+// one Morton order of their bounds' centres (types mixed), kBvhLeaf per leaf, an implicit complete
+// 4-ary tree above. Node bounds are unions of CullRecs with the largest margin scale and factor,
+// so a node's widened box contains every widened member box (broad phase).
+// ------------------------------------------------------------------------------------------
+// Levels of the heap-ordered tree over n colliders: the smallest L with 4^(L-1) leaves holding n.
+static int bvh_layout(int n, int& leaf0, int& total) {
+  if (n <= 0) return 0;
+  const int nleaf = (n + kBvhLeaf - 1) / kBvhLeaf;
+  int L = 1, w = 1;
+  while (w < nleaf) { w *= 4; ++L; if (L > kBvhMaxLevels) return 0; }
+  leaf0 = (w - 1) / 3;           // nodes above the leaf level: (4^(L-1) - 1) / 3
+  total = leaf0 + w;
+  return L;
+}
+
+size_t bvh_node_count(int n) {
+  int leaf0 = 0, total = 0;
+  return bvh_layout(n, leaf0, total) ? (size_t)total : 0;
+}
+
+size_t bvh_slot_count(int n) {
+  int leaf0 = 0, total = 0;
+  return bvh_layout(n, leaf0, total) ? (size_t)(total - leaf0) * kBvhLeaf : 0;
+}
+
+__global__ void morton_all_kernel(const CullRec* __restrict__ cull, int n, const float* __restrict__ box,
+                                  uint32_t* __restrict__ keys, int* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float c[3];
+  uint32_t code = 0;
+  if (bound_centre(cull[i], c[0], c[1], c[2])) {
+    uint32_t q[3];
+    for (int a = 0; a < 3; ++a) {
+      const float ext = box[3 + a] - box[a];
+      const float t = ext > 0.0f ? (c[a] - box[a]) / ext : 0.0f;
+      q[a] = (uint32_t)fminf(fmaxf(t * 1023.0f, 0.0f), 1023.0f);
+    }
+    code = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+  }
+  keys[i] = code;
+  vals[i] = i;
+}
+
+__device__ __forceinline__ void cull_union(CullRec& a, const CullRec& b) {
+  a.lox = fminf(a.lox, b.lox); a.loy = fminf(a.loy, b.loy); a.loz = fminf(a.loz, b.loz);
+  a.hix = fmaxf(a.hix, b.hix); a.hiy = fmaxf(a.hiy, b.hiy); a.hiz = fmaxf(a.hiz, b.hiz);
+  a.scale = fmaxf(a.scale, b.scale); a.factor = fmaxf(a.factor, b.factor);
+}
+
+__device__ __forceinline__ CullRec cull_empty() {
+  CullRec r;
+  r.lox = r.loy = r.loz = INFINITY; r.hix = r.hiy = r.hiz = -INFINITY; r.scale = 0.0f; r.factor = 0.0f;
+  return r;
+}
+
+// Leaf j = sorted colliders [kBvhLeaf j, kBvhLeaf (j + 1)) (empty past the last); writes the
+// leaf references.
+__global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __restrict__ perm, int ns, int na, int n,
+                                const SphereRec* __restrict__ sph, const AabbRec* __restrict__ aabb,
+                                const ObbRec* __restrict__ obb, CullRec* __restrict__ leaves, int nleaf,
+                                uint32_t* __restrict__ ref, float4* __restrict__ slots) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nleaf) return;
+  CullRec u = cull_empty();
+  // slot (64 B): a = first 16 B, b = next 16 B (b.w = code), c, d = an OBB's local bounds
+  //   sphere: a = (cx, cy, cz, r2), b.z = AudioTargetId
+  //   AABB:   a = (mn.xyz, mx.x), b.xy = mx.yz, b.z = AudioTargetId
+  //   OBB:    a = (c.xyz, q.x), b.xyz = q.yzw, c = (lmn.xyz, lmx.x), d.xy = lmx.yz, d.z = AudioTargetId
+  for (int k = j * kBvhLeaf; k < (j + 1) * kBvhLeaf; ++k) {
+    float4* sl = slots + 4 * (size_t)k;
+    float4 a = make_float4(0, 0, 0, 0), b = a, c = a, d = a;
+    int code = -1;
+    if (k < n) {
+      const int g = perm[k];
+      cull_union(u, cull[g]);
+      if (g < ns) {
+        ref[k] = (uint32_t)g;
+        const SphereRec r = sph[g];
+        a = make_float4(r.cx, r.cy, r.cz, r.r2);
+        b.z = __int_as_float(r.tid);
+        code = g;
+      } else if (g < ns + na) {
+        ref[k] = (1u << 30) | (uint32_t)(g - ns);
+        const AabbRec r = aabb[g - ns];
+        a = make_float4(r.mnx, r.mny, r.mnz, r.mxx);
+        b = make_float4(r.mxy, r.mxz, __int_as_float(r.tid), 0.0f);
+        code = (1 << 28) | (g - ns);
+      } else {
+        ref[k] = (2u << 30) | (uint32_t)(g - ns - na);
+        const ObbRec r = obb[g - ns - na];
+        a = make_float4(r.cx, r.cy, r.cz, r.qx);
+        b = make_float4(r.qy, r.qz, r.qw, 0.0f);
+        c = make_float4(r.lmnx, r.lmny, r.lmnz, r.lmxx);
+        d = make_float4(r.lmxy, r.lmxz, __int_as_float(r.tid), 0.0f);
+        code = (2 << 28) | (g - ns - na);
+      }
+    }
+    b.w = __int_as_float(code);
+    sl[0] = a; sl[1] = b; sl[2] = c; sl[3] = d;
+  }
+  leaves[j] = u;
+}
+
+// Inner levels, bottom-up, in one workgroup (they hold a third of the leaf count).
+__global__ __launch_bounds__(1024) void bvh_upper_kernel(CullRec* __restrict__ nodes, int levels) {
+  for (int l = levels - 2; l >= 0; --l) {
+    const int first = ((1 << (2 * l)) - 1) / 3, cnt = 1 << (2 * l);
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+      const int g = first + i;
+      CullRec u = cull_empty();
+      for (int k = 1; k <= 4; ++k) cull_union(u, nodes[4 * g + k]);
+      nodes[g] = u;
+    }
+    __syncthreads();
+  }
+}
+
+int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
+  const int n = sc.ns + sc.na + sc.no;
+  int leaf0 = 0, total = 0;
+  const int L = bvh_layout(n, leaf0, total);
+  sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0; sc.bvh_leaf0 = 0;
+  if (L == 0 || !sb.bvh || !sb.bvh_ref || !sb.bvh_leaf) return 0;
+  hipLaunchKernelGGL(scene_box_kernel, dim3(1), dim3(1024), 0, st, sc.cull, n, sb.box);
+  hipLaunchKernelGGL(morton_all_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, sb.box, sb.keys, sb.vals);
+  size_t bytes = sb.temp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, sb.keys, sb.keys_s, sb.vals, sb.perm, n, 0, 30, st) != hipSuccess)
+    return -1;
+  const int nleaf = total - leaf0;
+  hipLaunchKernelGGL(bvh_leaf_kernel, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, sb.perm, sc.ns, sc.na, n,
+                     sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
+  if (L > 1) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, sb.bvh, L);
+  sc.bvh = sb.bvh; sc.bvh_ref = sb.bvh_ref; sc.bvh_leaf = sb.bvh_leaf; sc.bvh_levels = L; sc.bvh_leaf0 = leaf0;
   return 0;
 }
 

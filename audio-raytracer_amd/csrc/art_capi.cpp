@@ -93,7 +93,7 @@ struct Frame {
          off_reset = 0, off_order = 0, raw_bytes = 0;
   size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_cull = 0, soa_bytes = 0;
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
-  size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0;
+  size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
 };
 
 struct Device {
@@ -349,6 +349,9 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_obb_s = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
     f.soa_cull_s = s; s = align_up(s + n * sizeof(CullRec), 256);
     f.soa_chunks = s; s = align_up(s + nch * sizeof(CullRec), 256);
+    f.soa_bvh = s; s = align_up(s + bvh_node_count((int)n) * sizeof(CullRec), 256);
+    f.soa_bvh_ref = s; s = align_up(s + n * 4, 256);
+    f.soa_bvh_leaf = s; s = align_up(s + bvh_slot_count((int)n) * 64, 256);
   }
   f.soa_bytes = s;
 }
@@ -406,7 +409,11 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sb.sph_s = reinterpret_cast<SphereRec*>(soa + f.soa_sph_s); sb.aabb_s = reinterpret_cast<AabbRec*>(soa + f.soa_aabb_s);
   sb.obb_s = reinterpret_cast<ObbRec*>(soa + f.soa_obb_s); sb.cull_s = reinterpret_cast<CullRec*>(soa + f.soa_cull_s);
   sb.chunks = reinterpret_cast<CullRec*>(soa + f.soa_chunks);
+  sb.bvh = bvh_node_count(f.ns + f.na + f.no) ? reinterpret_cast<CullRec*>(soa + f.soa_bvh) : nullptr;
+  sb.bvh_ref = reinterpret_cast<uint32_t*>(soa + f.soa_bvh_ref);
+  sb.bvh_leaf = reinterpret_cast<float4*>(soa + f.soa_bvh_leaf);
   sc.sph_s = nullptr; sc.aabb_s = nullptr; sc.obb_s = nullptr; sc.cull_s = nullptr; sc.chunks = nullptr; sc.nchunks = 0;
+  sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
   dv.sb = sb;
   if (fast_uses_sorted_scene() && launch_sort_scene(sc, sb, dv.stream) != 0)
     return fail(c, ART_E_DEVICE, "collider sort failed");
@@ -554,7 +561,10 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       FrameParams fps = fpx;
       fps.S = fan_count;
       if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
-      launch_raytrace_fast(dv.sc, fpx, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), dv.pairs.p,
+      DevScene scx = dv.sc;
+      if (c->flags & ART_CTX_NO_BVH) scx.bvh_levels = 0;  // cone / K-way split path
+      fpx.vis_bvh = (c->flags & ART_CTX_VIS_BVH) ? 1 : 0;
+      launch_raytrace_fast(scx, fpx, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), dv.pairs.p,
                            pair_count, st);
     } else if (f.T <= 31) {
       int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);

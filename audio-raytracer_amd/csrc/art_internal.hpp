@@ -76,13 +76,30 @@ struct DevScene {
   const CullRec* cull_s;          // [ns + na + no], sorted order
   const CullRec* chunks;          // [nchunks]: union bounds of 64 sorted colliders of one type
   int nchunks;
+  // BVH over all colliders (art_bvh.hip): a complete 4-ary tree in heap order (root 0, children
+  // of node g at 4g + 1 .. 4g + 4) over the Morton order of the bounds' centres, kBvhLeaf colliders
+  // per leaf; the leaves are nodes bvh_leaf0 .. bvh_leaf0 + 4^(levels - 1) - 1 (those past the
+  // last collider are empty). A node's CullRec is the union of its colliders' bounds with their
+  // largest margin scale and factor; an empty node has lo > hi.
+  const CullRec* bvh;
+  const uint32_t* bvh_ref;        // [ns + na + no] in Morton order: type rank << 30 | in-type index
+  const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] 64-B slots in Morton order: the
+                                  // hot record's test fields and the global order code (rank << 28 |
+                                  // index; -1: empty slot) in the first 32 B (bvh_leaf_kernel)
+  int bvh_levels;                 // 0: no BVH
+  int bvh_leaf0;
 };
+constexpr int kBvhLeaf = 4;       // colliders per leaf
+constexpr int kBvhMaxLevels = 8;  // <= 4 * 4^7 colliders; node ids fit the u16 traversal stack
+constexpr int kBvhStack = 3 * (kBvhMaxLevels - 1);
 
 struct SortBufs {
   float* box;                     // 6 floats
   uint32_t* keys; uint32_t* keys_s; int* vals; int* perm;
   void* temp; size_t temp_bytes;
   SphereRec* sph_s; AabbRec* aabb_s; ObbRec* obb_s; CullRec* cull_s; CullRec* chunks;
+  CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count) and leaf references
+  float4* bvh_leaf;                 // leaf slots (bvh_slot_count)
 };
 // per-sample spatializer DSP (art_dsp.hip)
 int dsp_source_params(const art_spatializer_settings& st, const art_audio_source& src, int sample_rate,
@@ -91,8 +108,14 @@ void launch_dsp(float* data, unsigned long long data_bytes, const long long* off
                 int frames_all, const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st);
 
 size_t sort_scene_temp_bytes(int n);
-bool fast_uses_sorted_scene();  // whether the throughput kernel reads the sorted copies
+bool fast_uses_sorted_scene();  // whether the throughput kernel reads the sorted copies (or the BVH)
+bool fast_uses_bvh();           // whether launch_sort_scene also builds the BVH
 int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
+// Node count of the BVH over n colliders (0 when n is 0 or too large for the u16 stack), and its
+// build (after launch_sort_scene's buffers are free again; same stream).
+size_t bvh_node_count(int n);
+size_t bvh_slot_count(int n);
+int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
 
 // Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
 struct FanLayout {
@@ -113,6 +136,7 @@ struct FrameParams {
   const float* muf_curve; int muf_n; float muf_len;
   int sample_rate;
   unsigned long long* exec;  // executed-work counters (ExecSlot order) or nullptr
+  int vis_bvh;               // ART_CTX_VIS_BVH: visibility by per-lane BVH traversal
 };
 
 // Slots of FrameParams::exec (art_exec_counts order).

@@ -376,6 +376,135 @@ __device__ __forceinline__ void nearest_sorted(const DevScene& sc, const Seg& s,
   exec_add(ex, kExecCullCone, 64ull * (nchk + (unsigned)nmine));
 }
 
+// ------------------------------------------------------------------------------------------
+// Per-lane nearest hit over the BVH (DevScene::bvh, art_bvh.hip), for any ray origin (first and
+// later bounces). The lane descends into the nearest child whose widened box (margin
+// factor * (scale + |o|_1), the bound of the exact tests' rounding) its ray enters
+// no later than its current best distance; the farther such children wait on a per-lane LDS stack.
+// A collider the ray can hit lies in every ancestor's widened box at least 3/4 of the margin
+// inside, so its computed distance is strictly greater than each ancestor's computed entry and no
+// ancestor is skipped while it could still win or tie. Leaves run the sweeps' exact tests, and
+// (distance, type rank << 28 | index) decides, which is the reference's first minimum over
+// Sphere, AABB, OBB order (ShootRayCast :225-280). Lanes with a non-finite or zero ray visit every
+// node (the box tests then say nothing).
+// ------------------------------------------------------------------------------------------
+// Nodes of the BVH's top levels held in the workgroup's LDS (the rest is read from HBM / L2):
+// levels 0..5, i.e. the whole tree up to 4096 colliders (44 KB).
+constexpr int kBvhLdsNodes = 1365;
+__host__ __device__ __forceinline__ int bvh_lds_nodes(const DevScene& sc) {
+  return sc.bvh_levels ? min(4 * sc.bvh_leaf0 + 1, kBvhLdsNodes) : 0;
+}
+
+__device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bool alive, const CullRec* s_nodes, int nl,
+                                            uint16_t* stk, int lane, float& best, int& code, unsigned long long* ex) {
+  best = FLT_MAX;
+  code = kNoHit;
+  unsigned nt0 = 0, nt1 = 0, nt2 = 0, nnode = 0, ndiag = 0;
+  (void)ndiag;
+  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
+  const bool force = !(isfinite(om) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
+                     (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
+  const int leaf0 = sc.bvh_leaf0;
+  int g = alive ? 0 : -1, sp = 0;  // current node (heap order; -1: done), stack depth
+  // while-while (Aila & Laine): descend inner nodes until every lane holds a leaf or is done, then
+  // test the leaves together, so the two kinds of step do not interleave within the wave
+  while (__any(g >= 0)) {
+    while (g >= 0 && g < leaf0) {
+#ifdef ART_DIAG_BVH_ITERS
+      ++ndiag;
+#endif
+      const int c0 = 4 * g + 1;
+      ++nnode;
+      float e[4];
+      int c[4] = {0, 1, 2, 3};
+      CullRec rr[4];
+      if (c0 + 3 < nl) {  // the 4 children: from LDS, or (deep levels of big scenes) from L2
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rr[k] = s_nodes[c0 + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rr[k] = sc.bvh[c0 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const CullRec& r = rr[k];
+        const float m = r.factor * (r.scale + om);
+        float tn, tf;
+        const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m,
+                                   r.hix + m, r.hiy + m, r.hiz + m, tn, tf);
+        const float en = fmaxf(tn, 0.0f);
+        const bool live = r.lox <= r.hix;  // empty nodes (past the last collider) have lo > hi
+        e[k] = INFINITY;
+        if (live && (force || (h && en <= best))) e[k] = force ? 0.0f : en;
+      }
+      auto cswap = [&](int a, int b) {
+        if (e[b] < e[a]) { const float te = e[a]; e[a] = e[b]; e[b] = te; const int tc = c[a]; c[a] = c[b]; c[b] = tc; }
+      };
+      cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
+      if (e[0] < INFINITY) {
+#pragma unroll
+        for (int k = 3; k >= 1; --k)
+          if (e[k] < INFINITY) { stk[sp * 64 + lane] = (uint16_t)(c0 + c[k]); ++sp; }
+        g = c0 + c[0];
+      } else {
+        g = sp ? (int)stk[(sp - 1) * 64 + lane] : -1;
+        sp = sp ? sp - 1 : 0;
+      }
+    }
+    if (g >= leaf0) {
+#ifdef ART_DIAG_BVH_ITERS
+      ++ndiag;
+#endif
+      // the leaf's kBvhLeaf 64-B slots: the first 32 B of each (everything but an OBB's local
+      // bounds) loaded together, one memory latency per leaf
+      const float4* sl = sc.bvh_leaf + (size_t)(g - leaf0) * (4 * kBvhLeaf);
+      float4 qa[kBvhLeaf], qb[kBvhLeaf];
+#pragma unroll
+      for (int k = 0; k < kBvhLeaf; ++k) { qa[k] = sl[4 * k]; qb[k] = sl[4 * k + 1]; }
+#pragma unroll
+      for (int k = 0; k < kBvhLeaf; ++k) {
+        const int cc = __float_as_int(qb[k].w);
+        if (cc < 0) continue;  // empty slot past the last collider
+        const int t = cc >> 28;
+        float d = 0.0f;
+        bool h;
+        if (t == 0) {
+          SphereRec r;
+          r.cx = qa[k].x; r.cy = qa[k].y; r.cz = qa[k].z; r.r2 = qa[k].w;
+          h = sphere_hit_dist(s, r, d); ++nt0;
+        } else if (t == 1) {
+          AabbRec r;
+          r.mnx = qa[k].x; r.mny = qa[k].y; r.mnz = qa[k].z; r.mxx = qa[k].w; r.mxy = qb[k].x; r.mxz = qb[k].y;
+          h = aabb_test<false>(s, r, d); ++nt1;
+        } else {
+          const float4 qc = sl[4 * k + 2], qd = sl[4 * k + 3];
+          ObbRec r;
+          r.cx = qa[k].x; r.cy = qa[k].y; r.cz = qa[k].z;
+          r.qx = qa[k].w; r.qy = qb[k].x; r.qz = qb[k].y; r.qw = qb[k].z;
+          r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qd.x; r.lmxz = qd.y;
+          h = obb_test<false>(s, r, stored_q(r), d); ++nt2;
+        }
+        if (h && (d < best || (d == best && cc < code))) { best = d; code = cc; }
+      }
+      g = sp ? (int)stk[(sp - 1) * 64 + lane] : -1;
+      sp = sp ? sp - 1 : 0;
+    }
+  }
+  if (ex) {
+    exec_add(ex, kExecSphere, wave_sum_u32(nt0));
+    exec_add(ex, kExecAabb, wave_sum_u32(nt1));
+    exec_add(ex, kExecObb, wave_sum_u32(nt2));
+    exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nnode));
+#ifdef ART_DIAG_BVH_ITERS  // lane trips (sum) and wave trips (max) x 2^32
+    {
+      unsigned mx = ndiag;
+      for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+      exec_add(ex, kExecCullCone, wave_sum_u32(ndiag) + ((unsigned long long)mx << 32));
+    }
+#endif
+  }
+}
+
 // brute-force nearest sweep of this wave's ranges (nearest_chunk): every collider of the range
 __device__ __forceinline__ void exec_brute(const DevScene& sc, int w, int K, unsigned long long* ex) {
   if (!ex) return;
@@ -1148,6 +1277,134 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
   if (valid && blocked) __hip_atomic_fetch_or(&gp.pad0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------------------------------------------------
+// Any-hit visibility by per-lane BVH traversal (CanRaySeePoint :365-397 / CanRaySeeAudioTarget
+// :405-449): the lane's segment [o, o + maxd d] visits the nodes whose widened box (margin
+// factor * (scale + |o|_1 + maxd), the box broad phase's bound) it enters before maxd, and stops at
+// its first blocker. A blocker's computed distance d < maxd lies strictly after the entry of every
+// ancestor (nearest_bvh), so no ancestor of a blocker is skipped; the verdict is the OR over all
+// colliders, the reference's verdict (order-free).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool anyhit_bvh(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid,
+                                           const CullRec* s_nodes, int nl, uint16_t* stk, int lane, unsigned* nt) {
+  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+  const bool force = !(isfinite(om) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
+                     (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
+  const int leaf0 = sc.bvh_leaf0;
+  bool blocked = false;
+  int g = valid ? 0 : -1, sp = 0;
+  while (__any(g >= 0)) {
+    while (g >= 0 && g < leaf0) {
+      const int c0 = 4 * g + 1;
+      ++nt[3];
+      CullRec rr[4];
+      if (c0 + 3 < nl) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rr[k] = s_nodes[c0 + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rr[k] = sc.bvh[c0 + k];
+      }
+      int nxt = -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const CullRec& r = rr[k];
+        const float m = r.factor * (r.scale + om);
+        float tn, tf;
+        const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m,
+                                   r.hix + m, r.hiy + m, r.hiz + m, tn, tf);
+        const bool live = r.lox <= r.hix;
+        if (live && (force || (h && tn <= maxd))) {
+          if (nxt < 0) nxt = c0 + k;
+          else { stk[sp * 64 + lane] = (uint16_t)(c0 + k); ++sp; }
+        }
+      }
+      if (nxt >= 0) g = nxt;
+      else { g = sp ? (int)stk[(sp - 1) * 64 + lane] : -1; sp = sp ? sp - 1 : 0; }
+    }
+    if (g >= leaf0) {
+      const float4* sl = sc.bvh_leaf + (size_t)(g - leaf0) * (4 * kBvhLeaf);
+      float4 qa[kBvhLeaf], qb[kBvhLeaf];
+#pragma unroll
+      for (int k = 0; k < kBvhLeaf; ++k) { qa[k] = sl[4 * k]; qb[k] = sl[4 * k + 1]; }
+#pragma unroll
+      for (int k = 0; k < kBvhLeaf; ++k) {
+        const int cc = __float_as_int(qb[k].w);
+        if (cc < 0 || blocked) continue;
+        const int t = cc >> 28;
+        float d = 0.0f;
+        bool h;
+        int tid;
+        if (t == 0) {
+          SphereRec r;
+          r.cx = qa[k].x; r.cy = qa[k].y; r.cz = qa[k].z; r.r2 = qa[k].w;
+          h = sphere_hit_dist(s, r, d); tid = __float_as_int(qb[k].z); ++nt[0];
+        } else if (t == 1) {
+          AabbRec r;
+          r.mnx = qa[k].x; r.mny = qa[k].y; r.mnz = qa[k].z; r.mxx = qa[k].w; r.mxy = qb[k].x; r.mxz = qb[k].y;
+          h = aabb_test<false>(s, r, d); tid = __float_as_int(qb[k].z); ++nt[1];
+        } else {
+          const float4 qc = sl[4 * k + 2], qd = sl[4 * k + 3];
+          ObbRec r;
+          r.cx = qa[k].x; r.cy = qa[k].y; r.cz = qa[k].z;
+          r.qx = qa[k].w; r.qy = qb[k].x; r.qz = qb[k].y; r.qw = qb[k].z;
+          r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qd.x; r.lmxz = qd.y;
+          h = obb_test<false>(s, r, stored_q(r), d); tid = __float_as_int(qd.z); ++nt[2];
+        }
+        blocked = h && d < maxd && tid != owner;  // :373-394, :411-447
+      }
+      if (blocked) { g = -1; sp = 0; }
+      else { g = sp ? (int)stk[(sp - 1) * 64 + lane] : -1; sp = sp ? sp - 1 : 0; }
+    }
+  }
+  return blocked;
+}
+
+constexpr int kVisBvhWaves = 8;
+
+// One wave per batch of 64 sorted pairs, the block's waves sharing the LDS copy of the top BVH
+// nodes; the verdict goes to PairG::pad0 (vis_finalize writes the outputs).
+__global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc, PairG* __restrict__ pairs,
+                                                                    const uint32_t* __restrict__ count, uint32_t nb_max,
+                                                                    const uint32_t* __restrict__ order,
+                                                                    unsigned long long* ex) {
+  extern __shared__ CullRec s_vnodes[];
+  __shared__ uint16_t s_vstk[kVisBvhWaves * kBvhStack * 64];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nl = bvh_lds_nodes(sc);
+  for (int i = threadIdx.x; i < nl; i += blockDim.x) s_vnodes[i] = sc.bvh[i];
+  __syncthreads();
+  const uint32_t np = ldc(count, 0);
+  const uint32_t b = blockIdx.x * (uint32_t)kVisBvhWaves + (uint32_t)w;
+  const uint32_t base = b * 64u;
+  if (b >= nb_max || base >= np) return;
+  const uint32_t p = base + lane;
+  const bool valid = p < np;
+  const uint32_t pi = order ? order[valid ? p : base] : (valid ? p : base);
+  PairG& gp = pairs[pi];
+  Seg s;
+  float maxd = 0.0f;
+  int owner = kNoOwner;
+  s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
+  s.a2 = s.a4 = 0.0f;
+  if (valid) {
+    const float4* q = reinterpret_cast<const float4*>(&gp);  // the 48-B segment only
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+    s.o = mk3(q0.x, q0.y, q0.z); s.d = mk3(q0.w, q1.x, q1.y); s.inv = mk3(q1.z, q1.w, q2.x);
+    s.a2 = q2.y; s.a4 = 2.0f * q2.y;
+    maxd = q2.z; owner = __float_as_int(q2.w);
+  }
+  unsigned nt[4] = {0u, 0u, 0u, 0u};
+  const bool blocked = anyhit_bvh(sc, s, maxd, owner, valid, s_vnodes, nl, s_vstk + w * (kBvhStack * 64), lane, nt);
+  if (valid && blocked) gp.pad0 = 1u;
+  if (ex) {
+    exec_add(ex, kExecSphere, wave_sum_u32(nt[0]));
+    exec_add(ex, kExecAabb, wave_sum_u32(nt[1]));
+    exec_add(ex, kExecObb, wave_sum_u32(nt[2]));
+    exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nt[3]));
+  }
+}
+
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
 // visible): visible echoes are stored, visible muffle rays counted.
 __global__ __launch_bounds__(256) void vis_finalize(const PairG* __restrict__ pairs, const uint32_t* __restrict__ count,
@@ -1181,6 +1438,12 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 // Occupancy target (amdgpu_waves_per_eu) and sweep unroll per scene kind, chosen by measurement on
 // MI355X: scenes without OBBs (config 2) run best at 6 waves/SIMD with 8 records per scalar-load
 // group (more loads in flight per s_waitcnt); OBB scenes (configs 3-5) at 7 waves/SIMD, unroll 4.
+#ifndef ART_FAST_BVH
+#define ART_FAST_BVH 1  // nearest hits by per-lane BVH traversal (nearest_bvh) when the scene has a BVH
+#endif
+#ifndef ART_FAST_WPE_BVH
+#define ART_FAST_WPE_BVH 4  // 122 VGPRs, no scratch (8: 82 VGPR spills)
+#endif
 #ifndef ART_FAST_WPE_NO_OBB
 #define ART_FAST_WPE_NO_OBB 6
 #endif
@@ -1196,7 +1459,7 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 
 // MULTI = false: frames with one hit per ray (H == 1, configs 2-4) compile without the later-bounce
 // nearest sweep and the reflection, which removes their registers from the kernel.
-template <int K, bool HITS, int U, int WPE, bool MULTI>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH>
 __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
@@ -1207,6 +1470,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                uint32_t* __restrict__ pair_count,
                                                                uint16_t* __restrict__ pkeys,
                                                                uint32_t* __restrict__ pvals) {
+  // BVH: the K waves of a workgroup are independent (each pulls its own 64-ray groups and owns
+  // their writes); they share the workgroup's LDS copy of the top BVH nodes.
+  constexpr bool IND = BVH;
   __shared__ float s_dist[K][64];
   __shared__ float s_best[K][64];  // running per-lane best of each wave (front-to-back pruning)
   (void)s_best;
@@ -1216,8 +1482,10 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   __shared__ uint8_t s_res[kMaxQueries * 64];
   __shared__ int s_head, s_np;
   __shared__ uint32_t s_muf[kMaxTargets];
-  __shared__ int s_ticket;
+  __shared__ int s_ticket[IND ? K : 1];
   __shared__ int s_go[3];  // staged visibility only
+  __shared__ uint16_t s_stk[BVH ? kBvhStack * 64 * K : 1];  // per-lane BVH traversal stacks
+  (void)s_stk;
   (void)s_go; (void)s_pairof; (void)s_res; (void)s_head; (void)s_np;
 #ifdef ART_TEST_NO_OBB
   sc.no = 0;
@@ -1227,23 +1495,43 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   (void)s_stage;
   // wave index as an SGPR value: chunk bounds and loop counters of the sweeps stay scalar
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const bool lead = IND || w == 0;  // the wave that owns the group's global writes
   const int nrb = (fp.R + 63) >> 6;  // 64-ray groups per fan
   const int ngroups = fp.S * nrb;
+  // BVH: the top bvh_lds_nodes(...) nodes in LDS (dynamic shared memory, BVH mode only)
+  const CullRec* s_nodes = reinterpret_cast<const CullRec*>(s_seg);
+  const int nl = BVH ? bvh_lds_nodes(sc) : 0;
+  (void)s_nodes; (void)nl;
+  if (BVH) {
+    CullRec* dst = reinterpret_cast<CullRec*>(s_seg);
+    for (int i = threadIdx.x; i < nl; i += blockDim.x) dst[i] = sc.bvh[i];
+    __syncthreads();
+  }
   // Persistent grid: the launch holds as many workgroups as are co-resident, and each pulls
   // 64-ray groups from a global ticket counter until the frame is drained (no partial last
   // round of workgroups, and uneven visibility work balances itself).
+  // BVH (independent waves): a static grid-stride assignment of groups to waves (a ticket per wave
+  // would serialize on one counter: about 88 dequeues per microsecond).
+  int gnext = (int)blockIdx.x * K + w;
   for (;;) {
-  __syncthreads();  // the previous group's LDS reads are done
-  if (threadIdx.x == 0) s_ticket = (int)atomicAdd(&work[0], 1u);
-  __syncthreads();
-  const int g = __builtin_amdgcn_readfirstlane(s_ticket);
+  int g;
+  if (IND) {
+    g = gnext;
+    gnext += (int)gridDim.x * K;
+  } else {
+    __syncthreads();  // the previous group's LDS reads are done
+    if (threadIdx.x == 0) s_ticket[0] = (int)atomicAdd(&work[0], 1u);
+    __syncthreads();
+    g = __builtin_amdgcn_readfirstlane(s_ticket[0]);
+  }
   if (g >= ngroups) break;
   const int fan = g / nrb;
   const int slot = (g - fan * nrb) * 64 + lane;
   const bool valid = slot < fp.R;
   const int ray = valid ? ray_order[slot] : 0;
   const int T = fp.T, H = MULTI ? fp.H : 1;
-  for (int t = threadIdx.x; t < T; t += blockDim.x) s_muf[t] = 0;
+  if (!IND)
+    for (int t = threadIdx.x; t < T; t += blockDim.x) s_muf[t] = 0;
 
   uint8_t* fb = block + (size_t)fan * L.stride;
   uint16_t* echo = reinterpret_cast<uint16_t*>(fb + L.echo_off);
@@ -1261,14 +1549,16 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
       bool any_reset;
       const int keep = batch_slot_state(fp, j, my_batch, any_reset);
       if (!keep) frozen |= 1u << k;
-      if (w == 0 && !single_slot && (!keep || any_reset)) {  // TC == 1: every slot is written once below
+      if (lead && !single_slot && (!keep || any_reset)) {  // TC == 1: every slot is written once below
         echo[j] = 0;
         if (HITS) hpo[j] = z;
       }
     }
   }
-  if (threadIdx.x == 0) s_chead = 0;
-  __syncthreads();
+  if (!IND) {
+    if (threadIdx.x == 0) s_chead = 0;
+    __syncthreads();
+  }
 
   const vec3 O = load3(origins, fan);
   vec3 o = O;
@@ -1283,7 +1573,13 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     float best;
     int code;
 #if ART_FAST_CULL
-    if (!MULTI || bounce == 0) {  // first segment: every ray of the fan starts at O
+    if (BVH) {
+#ifdef ART_DIAG_NO_NEAREST  // diagnostic build only: every live ray hits sphere 0 at distance 1
+      best = alive ? 1.0f : FLT_MAX; code = alive ? 0 : kNoHit;
+#else
+      nearest_bvh(sc, s, alive, s_nodes, nl, s_stk + w * (kBvhStack * 64), lane, best, code, fp.exec);
+#endif
+    } else if (!MULTI || bounce == 0) {  // first segment: every ray of the fan starts at O
       const WaveCone wc = make_cone(O, d, alive);
 #if ART_FAST_SORTED_NEAREST
       nearest_sorted<K>(sc, s, wc, w, lane, alive, s_best, best, code, fp.exec);
@@ -1298,16 +1594,20 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     nearest_chunk<U>(sc, s, w, K, best, code);
     exec_brute(sc, w, K, fp.exec);
 #endif
-    s_dist[w][lane] = best;
-    s_code[w][lane] = code;
-    __syncthreads();
-    float bd = s_dist[0][lane];
-    int bc = s_code[0][lane];
+    float bd = best;
+    int bc = code;
+    if (!IND) {
+      s_dist[w][lane] = best;
+      s_code[w][lane] = code;
+      __syncthreads();
+      bd = s_dist[0][lane];
+      bc = s_code[0][lane];
 #pragma unroll
-    for (int k = 1; k < K; ++k) {
-      const float dk = s_dist[k][lane];
-      const int ck = s_code[k][lane];
-      if (dk < bd || (dk == bd && ck < bc)) { bd = dk; bc = ck; }
+      for (int k = 1; k < K; ++k) {
+        const float dk = s_dist[k][lane];
+        const int ck = s_code[k][lane];
+        if (dk < bd || (dk == bd && ck < bc)) { bd = dk; bc = ck; }
+      }
     }
     const bool hit = alive && bc != kNoHit;
     alive = hit;  // a miss ends the ray (:200-207)
@@ -1326,7 +1626,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     }
     const int k = hits - 1;
     const bool live_slot = hit && !((frozen >> k) & 1u);
-    if (HITS && w == 0 && live_slot) {  // :118, :197
+    if (HITS && lead && live_slot) {  // :118, :197
       art_half3 p;
       p.x = f32tof16(o.x); p.y = f32tof16(o.y); p.z = f32tof16(o.z);
       hpo[ray * H + k] = p;
@@ -1337,7 +1637,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const float dist0 = distance(O, o);            // :130 (un-offset hit point)
 #if ART_FAST_SPLIT
     // Emit the pairs with their output destinations for vis_kernel (wave 0 owns the group's rays).
-    if (w == 0) {
+    if (lead) {
       const unsigned long long lt = (1ull << lane) - 1ull;
       unsigned long long mq[kMaxQueries];
       uint32_t actbits = 0;
@@ -1353,6 +1653,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
         actbits |= act ? (1u << q) : 0u;
         np += (uint32_t)__popcll(mq[q]);
       }
+#ifdef ART_DIAG_NO_EMIT  // diagnostic build only: time the path without the pair emission
+      np = 0;
+#endif
       if (np) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(pair_count, np);
@@ -1497,7 +1800,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     }
     ++bounce;
   }
-  if (valid && w == 0) {
+  if (valid && lead) {
     if (single_slot) {  // slots past the last hit keep the reset value 0 (:72-80)
       const art_half3 z = {0, 0, 0};
       for (int k = hits; k < H; ++k) {
@@ -1507,14 +1810,16 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     }
     if (HITS) fb[L.hit_counts_off + ray] = (uint8_t)hits;  // :204, :212
   }
-  __syncthreads();
-  if (single_slot)
-    for (int t = threadIdx.x; t < T; t += blockDim.x)
-      if (s_muf[t]) atomicAdd(&muffle_acc[(size_t)fan * T + t], s_muf[t]);
+  if (!IND) {  // muffle counts of the fused visibility (the split path counts in vis_finalize)
+    __syncthreads();
+    if (single_slot)
+      for (int t = threadIdx.x; t < T; t += blockDim.x)
+        if (s_muf[t]) atomicAdd(&muffle_acc[(size_t)fan * T + t], s_muf[t]);
+  }
   }
   // Every workgroup has drawn its final (out-of-range) ticket before it arrives here, so the last
   // arrival can rearm the counter for the next launch on this stream.
-  if (threadIdx.x == 0 && atomicAdd(&work[1], 1u) == gridDim.x - 1) {
+  if (!IND && threadIdx.x == 0 && atomicAdd(&work[1], 1u) == gridDim.x - 1) {
     atomicExch(&work[0], 0u);
     atomicExch(&work[1], 0u);
 #ifdef ART_DIAG_CULL_STATS
@@ -1562,16 +1867,19 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
   return blocks;
 }
 
-template <int K, bool HITS, int U, int WPE, bool MULTI>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
                            uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
-  const size_t lds = fast_lds_bytes(sc, fp.T);
+  const size_t lds = BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T);
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
-  const int resident = resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI>, 64 * K, lds);
-  const int nblk = (int)std::min<long long>(groups, resident);
-  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins, block,
-                     muffle_acc, ray_order, work, pairs, pair_count, pkeys, pvals);
+  // BVH: K independent waves per workgroup, one group each (grid-stride past 2^31 / K groups);
+  // otherwise a persistent grid of co-resident workgroups pulling groups from a ticket counter
+  const int nblk = BVH ? (int)std::min<long long>((groups + K - 1) / K, 1ll << 30)
+                       : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH>,
+                                                                          64 * K, lds));
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins,
+                     block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, pvals);
 }
 
 template <int K>
@@ -1580,8 +1888,8 @@ static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLa
                           uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
   // instantiation by scene kind (OBBs or not), hit outputs, and one or several hits per ray
 #define ART_LAUNCH(H_, U_, W_, M_) \
-  launch_fast_kh<K, H_, U_, W_, M_>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, \
-                                    pvals, st)
+  launch_fast_kh<K, H_, U_, W_, M_, false>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, \
+                                           pkeys, pvals, st)
   const bool multi = fp.H > 1;
   if (sc.no > 0) {
     if (L.has_hits) { if (multi) ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, true); else ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, false); }
@@ -1593,7 +1901,29 @@ static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLa
 #undef ART_LAUNCH
 }
 
-bool fast_uses_sorted_scene() { return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST || (ART_FAST_SPLIT && ART_VIS_TWO_LEVEL); }
+static_assert(!ART_FAST_BVH || ART_FAST_SPLIT, "the BVH path kernel emits visibility pairs (split visibility)");
+#ifndef ART_FAST_BVH_WAVES
+#define ART_FAST_BVH_WAVES 8  // independent waves per workgroup sharing the LDS node cache
+#endif
+
+// BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal.
+static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
+                            uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
+#define ART_LAUNCH(H_, M_) \
+  launch_fast_kh<ART_FAST_BVH_WAVES, H_, 1, ART_FAST_WPE_BVH, M_, true>(sc, fp, L, origins, block, muffle_acc, ray_order, \
+                                                                        work, pairs, pair_count, pkeys, pvals, st)
+  const bool multi = fp.H > 1;
+  if (L.has_hits) { if (multi) ART_LAUNCH(true, true); else ART_LAUNCH(true, false); }
+  else { if (multi) ART_LAUNCH(false, true); else ART_LAUNCH(false, false); }
+#undef ART_LAUNCH
+}
+
+bool fast_uses_bvh() { return ART_FAST_BVH != 0; }
+
+bool fast_uses_sorted_scene() {
+  return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST || (ART_FAST_SPLIT && ART_VIS_TWO_LEVEL) || ART_FAST_BVH;
+}
 
 // Pair buffer: PairG[max] | sort keys in/out u16[max] | pair indices in/out u32[max] | hipcub temp.
 struct PairBufs {
@@ -1651,7 +1981,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   if (sorted) (void)hipMemsetAsync(pb.keys, 0xFF, max_pairs * 2, st);  // unused slots sort last
   uint16_t* pkeys = sorted ? pb.keys : nullptr;
   uint32_t* pvals = sorted ? pb.vals : nullptr;
-  switch (fast_split(fp.S, fp.R)) {
+  if (ART_FAST_BVH && sc.bvh_levels > 0) {
+    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st);
+  } else switch (fast_split(fp.S, fp.R)) {
     case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st); break;
     default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st); break;
   }
@@ -1663,8 +1995,13 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
       size_t tb = pb.temp_bytes;
       (void)hipcub::DeviceRadixSort::SortPairs(pb.temp, tb, pb.keys, pb.keys_s, pb.vals, pb.order, (int)max_pairs, 0, 16, st);
     }
-    hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.pairs, pair_count, nb_max,
-                       sorted ? (const uint32_t*)pb.order : nullptr, fp.exec);
+    if (fp.vis_bvh && sc.bvh_levels > 0)  // ART_CTX_VIS_BVH (measured 1.7x slower than vis_kernel on config 2)
+      hipLaunchKernelGGL(vis_bvh_kernel, dim3((unsigned)((nb_max + kVisBvhWaves - 1) / kVisBvhWaves)), dim3(64 * kVisBvhWaves),
+                         (size_t)bvh_lds_nodes(sc) * sizeof(CullRec), st, sc, pb.pairs, pair_count, nb_max,
+                         sorted ? (const uint32_t*)pb.order : nullptr, fp.exec);
+    else
+      hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.pairs, pair_count, nb_max,
+                         sorted ? (const uint32_t*)pb.order : nullptr, fp.exec);
     hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.pairs, pair_count, block,
                        muffle_acc);
   }

@@ -182,3 +182,29 @@ def test_razor_thin_segments_tiny_spheres(ctx):
     out, _ = gpu_vs_oracle(ctx, scene, params, org, counts=False)
     # the scene must contain both verdicts: some muffle rays blocked by a sphere, some clear
     assert (out.muffle != 0).any() and (out.muffle != R).any()
+
+
+def test_bvh_exact_ties_across_leaves(ctx):
+    """Exact distance ties spread over many BVH leaves: along each axis a sphere and an AABB both
+    report distance 8 (K11), each duplicated 40 times at random list positions among 2000 clutter
+    colliders, so the copies land in different leaves and subtrees. The nearest hit must still be
+    the reference's first minimum (the lowest-index sphere), which needs every node whose entry
+    equals the current best to be visited."""
+    rng = np.random.default_rng(41)
+    axes = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float32)
+    dirs = f16bits(axes).reshape(-1, 3)
+    n_clutter, dup = 2000, 40
+    sc_c = rng.uniform(-60, 60, (n_clutter, 3)).astype(np.float32)
+    sc_c[np.abs(sc_c).min(1) < 12] += 30.0  # keep clutter off the axes near the origin
+    s_centers = np.concatenate([sc_c[:1000], np.repeat(axes * 10.0, dup, 0)])
+    s_radii = np.concatenate([rng.uniform(0.1, 2, 1000), np.full(6 * dup, 2.0)]).astype(np.float32)
+    a_centers = np.concatenate([sc_c[1000:], np.repeat(axes * 9.0, dup, 0)])
+    a_halves = np.concatenate([rng.uniform(0.1, 2, (1000, 3)), np.ones((6 * dup, 3))]).astype(np.float32)
+    ps, pa = rng.permutation(len(s_radii)), rng.permutation(len(a_halves))
+    scene = art.Scene(dirs=dirs, targets=np.array([[0, 0, 30], [25, 25, 0]], np.float32),
+                      spheres=spheres(s_centers[ps], s_radii[ps], rng), aabbs=aabbs(a_centers[pa], a_halves[pa], rng))
+    org = np.zeros((3, 3), np.float32)
+    params = art.FrameParams(max_hits_per_ray=3, max_ray_life=1e4, max_muffle_hit_distance=1e5,
+                             stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
+    o_gpu, _ = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
+    assert (o_gpu.hit_counts != 0).all()

@@ -33,10 +33,11 @@ def _diff_report(a: art.FanOutputs, b: art.FanOutputs) -> str:
 
 
 def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True, wavefront=True):
-    """Run the frame through every raytrace implementation — the throughput block kernel (K-way
-    split, coherent ray order), the wavefront pipeline (ART_CTX_WAVEFRONT) and the reference-order
-    counting kernel — and require each to equal the oracle bit for bit; the counting run's test
-    counts must equal the oracle's."""
+    """Run the frame through every raytrace implementation — the throughput path kernel (BVH
+    nearest hits, sorted-batch visibility), the same with BVH visibility (ART_CTX_VIS_BVH) and
+    without the BVH (ART_CTX_NO_BVH: shared-origin cone, K-way split), the wavefront pipeline
+    (ART_CTX_WAVEFRONT) and the reference-order counting kernel — and require each to equal the
+    oracle bit for bit; the counting run's test counts must equal the oracle's."""
     S = org.shape[0]
     o_gpu = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, params.thread_count, hits=hits,
                            dsp=params.dsp is not None)
@@ -49,6 +50,13 @@ def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True, 
     ctx.run(art.Frame(scene, params, org, o_gpu))
     eq = o_gpu.equal(o_ref)
     assert all(eq.values()), f"fast kernel: {eq}\n{_diff_report(o_gpu, o_ref)}"
+    for flag, name in ((abi.ART_CTX_VIS_BVH, "BVH visibility"), (abi.ART_CTX_NO_BVH, "no-BVH kernel")):
+        o_v = o_cnt.copy()
+        ctx.set_flags(flag)
+        ctx.run(art.Frame(scene, params, org, o_v))
+        ctx.set_flags(0)
+        eq = o_v.equal(o_ref)
+        assert all(eq.values()), f"{name}: {eq}\n{_diff_report(o_v, o_ref)}"
     if wavefront:
         o_wf = o_cnt.copy()
         ctx.set_flags(abi.ART_CTX_WAVEFRONT)
