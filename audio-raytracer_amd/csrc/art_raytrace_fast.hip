@@ -1173,17 +1173,29 @@ __device__ __forceinline__ void visibility_culled(const DevScene& sc, const Pair
 // (echo :124-145 and muffle :150-173 only write outputs), so the two kernels give the same
 // results as the fused sweep, and each runs with its own, much smaller, register state.
 // ------------------------------------------------------------------------------------------
-struct alignas(16) PairG {
-  float ox, oy, oz, dx;
-  float dy, dz, ix, iy;
-  float iz, a2, maxd;
-  int owner;
-  uint32_t dest;   // echo: u16 index into the fan blocks; muffle: index into muffle_acc
-  uint32_t val;    // bits 0-15: echo half (f32tof16(dist * echo)); bit 16: muffle pair
-  uint32_t pad0, pad1;
+// Pair arrays (struct of arrays, pair index = emission order):
+//   seg[2 i], seg[2 i + 1]  (o.xyz, maxd), (d.xyz, owner)   32 B, read by the visibility sweep;
+//                           1/d and dot(d, d) are recomputed there by make_seg (same operations)
+//   out[i]                  (dest, val)                      8 B, read by vis_finalize
+//   flag[i]                 0 = no blocker found yet, 1 = blocked
+// Echo pairs fill [0, echo_cap) in emission order (the 64 rays of a wave share the fan origin, one
+// batch each); muffle pairs fill [echo_cap, echo_cap + S R H T). counts[0] / counts[1] = echo /
+// muffle pairs emitted.
+struct VisPairs {
+  float4* seg;
+  uint2* out;      // dest: echo u16 index into the fan blocks / muffle_acc index; val: echo half | kPairMuffle
+  uint32_t* flag;
+  uint32_t echo_cap;  // multiple of 64
 };
-static_assert(sizeof(PairG) == 64 && offsetof(PairG, dest) == 48, "PairG layout");
 constexpr uint32_t kPairMuffle = 1u << 16;
+
+// The segment of pair i as the sweeps see it.
+__device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Seg& s, float& maxd, int& owner) {
+  const float4 q0 = vp.seg[2 * (size_t)i], q1 = vp.seg[2 * (size_t)i + 1];
+  s = make_seg(mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z));
+  maxd = q0.w;
+  owner = __float_as_int(q1.w);
+}
 
 #ifndef ART_VIS_WPE
 #define ART_VIS_WPE 6
@@ -1191,10 +1203,16 @@ constexpr uint32_t kPairMuffle = 1u << 16;
 #ifndef ART_VIS_PLAIN_FLAG
 #define ART_VIS_PLAIN_FLAG 0
 #endif
-#ifndef ART_VIS_RANGES
-#define ART_VIS_RANGES 8
+// Chunk ranges per 64-pair batch (work items of vis_kernel), by scene kind: OBB tests are long,
+// so OBB scenes balance better over 8 ranges (config 3: 1.46 vs 1.54 ms at 4); otherwise each
+// range repeats the batch's setup, and 4 measured best (config 2 vis_kernel 296 vs 315 us).
+#ifndef ART_VIS_RANGES_OBB
+#define ART_VIS_RANGES_OBB 8
 #endif
-constexpr int kVisRanges = ART_VIS_RANGES;  // chunk ranges per 64-pair batch (work items)
+#ifndef ART_VIS_RANGES
+#define ART_VIS_RANGES 4
+#endif
+__host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) { return sc.no > 0 ? ART_VIS_RANGES_OBB : ART_VIS_RANGES; }
 #ifndef ART_VIS_SORT
 #define ART_VIS_SORT 1  // visibility batches in (target, direction from the target) order (vis_sort_key)
 #endif
@@ -1205,11 +1223,13 @@ constexpr int kVisRanges = ART_VIS_RANGES;  // chunk ranges per 64-pair batch (w
 #define ART_VIS_CONE 1  // cone broad phase around the batch's shared end point (make_vis_cone)
 #endif
 
-// Sort key of a visibility pair: muffle rays of target t by the octahedral Morton cell (64 x 64)
-// of their direction seen from the target, so 64 consecutive sorted pairs form a thin cone with
-// apex t; echo rays keep their emission order (one key, stable sort) after them. 0xFFFF marks an
-// unused slot.
-constexpr uint16_t kKeyEcho = 0xFFFE, kKeyUnused = 0xFFFF;
+// Sort key of a muffle pair: target t and the octahedral Morton cell (32 x 32) of the ray's
+// direction seen from the target, so 64 consecutive sorted pairs form a thin cone with apex t
+// (1024 cells per target: 1.8 % broad-phase candidates in simulation, 4096: 1.6 %).
+#ifndef ART_SORT_DIR_BITS
+#define ART_SORT_DIR_BITS 10
+#endif
+constexpr int kSortDirBits = ART_SORT_DIR_BITS, kSortBins = kMaxQueries << kSortDirBits;
 __device__ __forceinline__ uint16_t vis_sort_key(int t, vec3 u) {
   const float n = fabsf(u.x) + fabsf(u.y) + fabsf(u.z);
   float a = 0.0f, c = 0.0f;
@@ -1218,38 +1238,53 @@ __device__ __forceinline__ uint16_t vis_sort_key(int t, vec3 u) {
     a = z < 0.0f ? (1.0f - fabsf(y)) * (x >= 0.0f ? 1.0f : -1.0f) : x;
     c = z < 0.0f ? (1.0f - fabsf(x)) * (y >= 0.0f ? 1.0f : -1.0f) : y;
   }
-  auto q6 = [](float v) { return (uint32_t)fminf(fmaxf((v + 1.0f) * 32.0f, 0.0f), 63.0f); };
-  auto sp = [](uint32_t v) {  // 6 bits -> even bit positions
+  constexpr float kCells = (float)(1 << (kSortDirBits / 2));  // cells per octahedral axis
+  auto q5 = [](float v) { return (uint32_t)fminf(fmaxf((v + 1.0f) * (0.5f * kCells), 0.0f), kCells - 1.0f); };
+  auto sp = [](uint32_t v) {  // 5 bits -> even bit positions
     v = (v | (v << 4)) & 0x0F0Fu; v = (v | (v << 2)) & 0x3333u; v = (v | (v << 1)) & 0x5555u;
     return v;
   };
-  return (uint16_t)(((uint32_t)t << 12) | sp(q6(a)) | (sp(q6(c)) << 1));
+  return (uint16_t)(((uint32_t)t << kSortDirBits) | sp(q5(a)) | (sp(q5(c)) << 1));
+}
+
+// Pair of lane `lane` in batch b: echo batches cover [0, echo_cap) in emission order, muffle batches
+// the sorted muffle pairs (order = sorted position -> muffle pair, or identity). Returns false for
+// a batch past the emitted pairs; n_in = the batch's valid lanes (the others get the batch's first
+// pair, so every lane holds a real segment).
+__device__ __forceinline__ bool batch_pair(const VisPairs& vp, const uint32_t* count, const uint32_t* order, uint32_t b,
+                                           int lane, uint32_t& pi, uint32_t& n_in) {
+  const uint32_t base = b * 64u;
+  uint32_t rel, n, off;
+  if (base < vp.echo_cap) { rel = base; n = ldc(count, 0); off = 0u; }
+  else { rel = base - vp.echo_cap; n = ldc(count, 1); off = vp.echo_cap; }
+  if (rel >= n) return false;
+  n_in = min(64u, n - rel);
+  const uint32_t q = rel + ((uint32_t)lane < n_in ? (uint32_t)lane : 0u);
+  pi = off + ((order && off) ? order[q] : q);
+  return true;
 }
 
 // Work item i of vis_kernel = (chunk range r, batch b), range-major: r = i / nb_max, b = i % nb_max.
 // A batch's later ranges usually start after its earlier ones finished and skip the pairs those
-// already blocked (a stale read only costs work). Verdicts meet in PairG::pad0 through relaxed
+// already blocked (a stale read only costs work). Verdicts meet in VisPairs::flag through relaxed
 // device-scope atomicOr (no fences: an agent-scope release writes back the XCD's L2);
 // vis_finalize writes the outputs after the kernel boundary.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
-void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restrict__ count, uint32_t nb_max,
+void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
                 const uint32_t* __restrict__ order, unsigned long long* ex) {
   const int lane = threadIdx.x & 63;
-  const uint32_t np = ldc(count, 0);
   const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t r = item / nb_max, b = item - r * nb_max;
-  const uint32_t base = b * 64u;
-  if (r >= (uint32_t)kVisRanges || base >= np) return;
-  const uint32_t p = base + lane;
-  // batch b = 64 consecutive pairs of the sorted order (pairs of one target by direction from it)
-  const uint32_t pi = order ? order[p < np ? p : base] : (p < np ? p : base);
-  PairG& gp = pairs[pi];
+  const int nranges = vis_ranges(sc);
+  uint32_t pi, n_in;
+  if (r >= (uint32_t)nranges || !batch_pair(vp, count, order, b, lane, pi, n_in)) return;
+  uint32_t* flag = vp.flag + pi;
   // pairs an earlier range already blocked are skipped (not loaded, and out of the wave's box)
 #if ART_VIS_PLAIN_FLAG
   // plain load: a stale 0 (another XCD's verdict not yet visible) only repeats work
-  const bool valid = p < np && gp.pad0 == 0u;
+  const bool valid = (uint32_t)lane < n_in && *flag == 0u;
 #else
-  const bool valid = p < np && __hip_atomic_load(&gp.pad0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  const bool valid = (uint32_t)lane < n_in && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
 #endif
   if (!__any(valid)) return;
   Seg s;
@@ -1257,16 +1292,10 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
   int owner = kNoOwner;
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
   s.a2 = s.a4 = 0.0f;
-  if (valid) {
-    const float4* q = reinterpret_cast<const float4*>(&gp);  // the 48-B segment only
-    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-    s.o = mk3(q0.x, q0.y, q0.z); s.d = mk3(q0.w, q1.x, q1.y); s.inv = mk3(q1.z, q1.w, q2.x);
-    s.a2 = q2.y; s.a4 = 2.0f * q2.y;
-    maxd = q2.z; owner = __float_as_int(q2.w);
-  }
+  if (valid) load_pair_seg(vp, pi, s, maxd, owner);
   const int nch = (sc.ns + kChunk - 1) / kChunk + (sc.na + kChunk - 1) / kChunk + (sc.no + kChunk - 1) / kChunk;
   const bool two = sc.chunks != nullptr && (ART_VIS_TWO_LEVEL || (ART_FAST_TWO_LEVEL && sc.nchunks > 64));
-  const int c_lo = (int)(((long long)nch * r) / kVisRanges), c_hi = (int)(((long long)nch * (r + 1)) / kVisRanges);
+  const int c_lo = (int)(((long long)nch * r) / nranges), c_hi = (int)(((long long)nch * (r + 1)) / nranges);
 #if ART_VIS_CONE
   const float om = wave_max(valid ? fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd : 0.0f);
   const VisCone vc = make_vis_cone(s, maxd, valid, om);
@@ -1274,7 +1303,7 @@ void vis_kernel(DevScene sc, PairG* __restrict__ pairs, const uint32_t* __restri
 #else
   const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, nullptr, two);
 #endif
-  if (valid && blocked) __hip_atomic_fetch_or(&gp.pad0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (valid && blocked) __hip_atomic_fetch_or(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1363,8 +1392,8 @@ __device__ __forceinline__ bool anyhit_bvh(const DevScene& sc, const Seg& s, flo
 constexpr int kVisBvhWaves = 8;
 
 // One wave per batch of 64 sorted pairs, the block's waves sharing the LDS copy of the top BVH
-// nodes; the verdict goes to PairG::pad0 (vis_finalize writes the outputs).
-__global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc, PairG* __restrict__ pairs,
+// nodes; the verdict goes to VisPairs::flag (vis_finalize writes the outputs).
+__global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc, VisPairs vp,
                                                                     const uint32_t* __restrict__ count, uint32_t nb_max,
                                                                     const uint32_t* __restrict__ order,
                                                                     unsigned long long* ex) {
@@ -1374,29 +1403,19 @@ __global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc,
   const int nl = bvh_lds_nodes(sc);
   for (int i = threadIdx.x; i < nl; i += blockDim.x) s_vnodes[i] = sc.bvh[i];
   __syncthreads();
-  const uint32_t np = ldc(count, 0);
   const uint32_t b = blockIdx.x * (uint32_t)kVisBvhWaves + (uint32_t)w;
-  const uint32_t base = b * 64u;
-  if (b >= nb_max || base >= np) return;
-  const uint32_t p = base + lane;
-  const bool valid = p < np;
-  const uint32_t pi = order ? order[valid ? p : base] : (valid ? p : base);
-  PairG& gp = pairs[pi];
+  uint32_t pi, n_in;
+  if (b >= nb_max || !batch_pair(vp, count, order, b, lane, pi, n_in)) return;
+  const bool valid = (uint32_t)lane < n_in;
   Seg s;
   float maxd = 0.0f;
   int owner = kNoOwner;
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
   s.a2 = s.a4 = 0.0f;
-  if (valid) {
-    const float4* q = reinterpret_cast<const float4*>(&gp);  // the 48-B segment only
-    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-    s.o = mk3(q0.x, q0.y, q0.z); s.d = mk3(q0.w, q1.x, q1.y); s.inv = mk3(q1.z, q1.w, q2.x);
-    s.a2 = q2.y; s.a4 = 2.0f * q2.y;
-    maxd = q2.z; owner = __float_as_int(q2.w);
-  }
+  if (valid) load_pair_seg(vp, pi, s, maxd, owner);
   unsigned nt[4] = {0u, 0u, 0u, 0u};
   const bool blocked = anyhit_bvh(sc, s, maxd, owner, valid, s_vnodes, nl, s_vstk + w * (kBvhStack * 64), lane, nt);
-  if (valid && blocked) gp.pad0 = 1u;
+  if (valid && blocked) vp.flag[pi] = 1u;
   if (ex) {
     exec_add(ex, kExecSphere, wave_sum_u32(nt[0]));
     exec_add(ex, kExecAabb, wave_sum_u32(nt[1]));
@@ -1407,15 +1426,16 @@ __global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc,
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
 // visible): visible echoes are stored, visible muffle rays counted.
-__global__ __launch_bounds__(256) void vis_finalize(const PairG* __restrict__ pairs, const uint32_t* __restrict__ count,
+__global__ __launch_bounds__(256) void vis_finalize(VisPairs vp, const uint32_t* __restrict__ count,
                                                     uint8_t* __restrict__ block, uint32_t* __restrict__ muffle_acc) {
   const int lane = threadIdx.x & 63;
-  const uint32_t np = ldc(count, 0);
-  const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-  if (__builtin_amdgcn_readfirstlane(p - lane) >= np) return;
-  const bool valid = p < np;
+  const uint32_t p = blockIdx.x * 256u + threadIdx.x, wbase = __builtin_amdgcn_readfirstlane(p - lane);
+  const bool echo_region = wbase < vp.echo_cap;  // echo_cap is a multiple of 64: one region per wave
+  const uint32_t n = echo_region ? ldc(count, 0) : ldc(count, 1), rel = echo_region ? p : p - vp.echo_cap;
+  if (__builtin_amdgcn_readfirstlane(rel - lane) >= n) return;
+  const bool valid = rel < n;
   uint32_t flag = 1u, dest = 0u, val = 0u;
-  if (valid) { flag = pairs[p].pad0; dest = pairs[p].dest; val = pairs[p].val; }
+  if (valid) { flag = vp.flag[p]; const uint2 o = vp.out[p]; dest = o.x; val = o.y; }
   const bool vis = valid && flag == 0u;
   const bool muf = (val & kPairMuffle) != 0;
   if (vis && !muf) reinterpret_cast<uint16_t*>(block)[dest] = (uint16_t)(val & 0xffffu);  // :142-144
@@ -1466,10 +1486,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                uint32_t* __restrict__ muffle_acc,
                                                                const int* __restrict__ ray_order,
                                                                uint32_t* __restrict__ work,
-                                                               PairG* __restrict__ pairs,
+                                                               VisPairs vp,
                                                                uint32_t* __restrict__ pair_count,
-                                                               uint16_t* __restrict__ pkeys,
-                                                               uint32_t* __restrict__ pvals) {
+                                                               uint16_t* __restrict__ pkeys) {
   // BVH: the K waves of a workgroup are independent (each pulls its own 64-ray groups and owns
   // their writes); they share the workgroup's LDS copy of the top BVH nodes.
   constexpr bool IND = BVH;
@@ -1657,40 +1676,44 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
       np = 0;
 #endif
       if (np) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(pair_count, np);
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
-        uint32_t pos = base;
+        // echo pairs to the echo region, muffle pairs to the muffle region (one reservation each)
+        const uint32_t ne = (uint32_t)__popcll(mq[0]), nm = np - ne;
+        uint32_t eb = 0, mb = 0;
+        if (lane == 0) {
+          if (ne) eb = atomicAdd(&pair_count[0], ne);
+          if (nm) mb = atomicAdd(&pair_count[1], nm);
+        }
+        eb = __builtin_amdgcn_readfirstlane(__shfl(eb, 0, 64));
+        mb = __builtin_amdgcn_readfirstlane(__shfl(mb, 0, 64));
+        uint32_t pos = mb;  // muffle position (region-relative)
 #pragma unroll
         for (int q = 0; q < kMaxQueries; ++q) {
           if (q <= T && ((actbits >> q) & 1u)) {
             vec3 qdir;
             float maxd;
-            PairG r;
+            int owner;
+            uint2 ov;
             if (q == 0) {
-              qdir = normalize(O - off); maxd = dist0; r.owner = kNoOwner;
-              r.dest = (uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k);
-              r.val = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
+              qdir = normalize(O - off); maxd = dist0; owner = kNoOwner;
+              ov.x = (uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k);
+              ov.y = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
             } else {
               const vec3 tp = load3(sc.targets, q - 1);
               maxd = distance(off, tp);
               qdir = normalize(tp - off);
-              r.owner = q - 1;                                    // :413, :426, :439
-              r.dest = (uint32_t)(((size_t)fan * fp.TC + my_slot) * T + (q - 1));
-              r.val = kPairMuffle;
+              owner = q - 1;                                      // :413, :426, :439
+              ov.x = (uint32_t)(((size_t)fan * fp.TC + my_slot) * T + (q - 1));
+              ov.y = kPairMuffle;
             }
-            const Seg g = make_seg(off, qdir);
-            r.ox = g.o.x; r.oy = g.o.y; r.oz = g.o.z; r.dx = g.d.x; r.dy = g.d.y; r.dz = g.d.z;
-            r.ix = g.inv.x; r.iy = g.inv.y; r.iz = g.inv.z; r.a2 = g.a2; r.maxd = maxd;
-            r.pad0 = r.pad1 = 0u;
-            const uint32_t at = pos + (uint32_t)__popcll(mq[q] & lt);
-            pairs[at] = r;
-            if (pkeys) {
-              pkeys[at] = q == 0 ? kKeyEcho : vis_sort_key(q - 1, mk3(-qdir.x, -qdir.y, -qdir.z));
-              pvals[at] = at;
-            }
+            const uint32_t rank = (uint32_t)__popcll(mq[q] & lt);
+            const uint32_t at = q == 0 ? eb + rank : vp.echo_cap + pos + rank;
+            vp.seg[2 * (size_t)at] = make_float4(off.x, off.y, off.z, maxd);
+            vp.seg[2 * (size_t)at + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(owner));
+            vp.out[at] = ov;
+            vp.flag[at] = 0u;
+            if (q > 0 && pkeys) pkeys[pos + rank] = vis_sort_key(q - 1, mk3(-qdir.x, -qdir.y, -qdir.z));
           }
-          pos += (q <= T) ? (uint32_t)__popcll(mq[q]) : 0u;
+          if (q > 0 && q <= T) pos += (uint32_t)__popcll(mq[q]);
         }
       }
       // a blocked echo leaves the reset value (:76); vis_kernel overwrites the visible ones
@@ -1869,8 +1892,8 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
 
 template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
-                           uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
+                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
+                           uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
   const size_t lds = BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T);
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   // BVH: K independent waves per workgroup, one group each (grid-stride past 2^31 / K groups);
@@ -1879,17 +1902,17 @@ static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanL
                        : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH>,
                                                                           64 * K, lds));
   hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins,
-                     block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, pvals);
+                     block, muffle_acc, ray_order, work, pairs, pair_count, pkeys);
 }
 
 template <int K>
 static void launch_fast_k(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
-                          uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
+                          uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
   // instantiation by scene kind (OBBs or not), hit outputs, and one or several hits per ray
 #define ART_LAUNCH(H_, U_, W_, M_) \
   launch_fast_kh<K, H_, U_, W_, M_, false>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, \
-                                           pkeys, pvals, st)
+                                           pkeys, st)
   const bool multi = fp.H > 1;
   if (sc.no > 0) {
     if (L.has_hits) { if (multi) ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, true); else ART_LAUNCH(true, ART_FAST_U_OBB, ART_FAST_WPE_OBB, false); }
@@ -1908,11 +1931,11 @@ static_assert(!ART_FAST_BVH || ART_FAST_SPLIT, "the BVH path kernel emits visibi
 
 // BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal.
 static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, PairG* pairs,
-                            uint32_t* pair_count, uint16_t* pkeys, uint32_t* pvals, hipStream_t st) {
+                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
+                            uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
 #define ART_LAUNCH(H_, M_) \
   launch_fast_kh<ART_FAST_BVH_WAVES, H_, 1, ART_FAST_WPE_BVH, M_, true>(sc, fp, L, origins, block, muffle_acc, ray_order, \
-                                                                        work, pairs, pair_count, pkeys, pvals, st)
+                                                                        work, pairs, pair_count, pkeys, st)
   const bool multi = fp.H > 1;
   if (L.has_hits) { if (multi) ART_LAUNCH(true, true); else ART_LAUNCH(true, false); }
   else { if (multi) ART_LAUNCH(false, true); else ART_LAUNCH(false, false); }
@@ -1925,84 +1948,131 @@ bool fast_uses_sorted_scene() {
   return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST || (ART_FAST_SPLIT && ART_VIS_TWO_LEVEL) || ART_FAST_BVH;
 }
 
-// Pair buffer: PairG[max] | sort keys in/out u16[max] | pair indices in/out u32[max] | hipcub temp.
+// Counting sort of the muffle pairs by key (kSortBins buckets; the order inside a bucket is free:
+// the any-hit verdicts do not depend on it). Block j of kSortBlock pairs: LDS histogram -> column j
+// of hist[bin][block]; an exclusive scan over the matrix in (bin, block) order gives each block its
+// first position per bucket; the scatter hands out positions with LDS atomics.
+constexpr int kSortThreads = 256, kSortBlock = 16 * kSortThreads;
+
+__global__ __launch_bounds__(kSortThreads) void pair_hist_kernel(const uint16_t* __restrict__ keys,
+                                                                 const uint32_t* __restrict__ count,
+                                                                 uint32_t* __restrict__ hist, int nblk, int nbins) {
+  __shared__ uint32_t h[kSortBins];
+  for (int i = threadIdx.x; i < nbins; i += kSortThreads) h[i] = 0u;
+  __syncthreads();
+  // each thread counts 16 consecutive keys, one LDS atomic per run of equal keys (the keys of a
+  // wave's rays are coherent, so per-key atomics would serialize on a few bins)
+  const uint32_t n = ldc(count, 1), i0 = blockIdx.x * (uint32_t)kSortBlock + threadIdx.x * 16u;
+  const uint32_t e = min(n, i0 + 16u);
+  uint32_t run = 0, rk = 0;
+  for (uint32_t i = i0; i < e; ++i) {
+    const uint32_t k = keys[i];
+    if (run && k != rk) { atomicAdd(&h[rk], run); run = 0; }
+    rk = k;
+    ++run;
+  }
+  if (run) atomicAdd(&h[rk], run);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nbins; i += kSortThreads) hist[(size_t)i * nblk + blockIdx.x] = h[i];
+}
+
+__global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16_t* __restrict__ keys,
+                                                                    const uint32_t* __restrict__ count,
+                                                                    const uint32_t* __restrict__ start,
+                                                                    uint32_t* __restrict__ order, int nblk, int nbins) {
+  __shared__ uint32_t cur[kSortBins];
+  for (int i = threadIdx.x; i < nbins; i += kSortThreads) cur[i] = start[(size_t)i * nblk + blockIdx.x];
+  __syncthreads();
+  const uint32_t n = ldc(count, 1), i0 = blockIdx.x * (uint32_t)kSortBlock + threadIdx.x * 16u;
+  const uint32_t e = min(n, i0 + 16u);
+  for (uint32_t i = i0; i < e; ++i) order[atomicAdd(&cur[keys[i]], 1u)] = i;
+}
+
+// Pair buffer: VisPairs (seg | out | flag) | muffle keys u16 | sorted order u32 | hist, scanned
+// hist u32[bins x blocks] | scan temp.
 struct PairBufs {
-  PairG* pairs;
-  uint16_t *keys, *keys_s;
-  uint32_t *vals, *order;
+  VisPairs vp;
+  uint16_t* keys;
+  uint32_t *order, *hist, *start;
   void* temp;
   size_t temp_bytes, total;
+  int nblk, nbins;
 };
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-static PairBufs pair_bufs(void* base, size_t max_pairs) {
+static size_t echo_cap_of(const FrameParams& fp) { return ((size_t)fp.S * fp.R * fp.H + 63) & ~(size_t)63; }
+static size_t muffle_cap_of(const FrameParams& fp) { return (size_t)fp.S * fp.R * fp.H * fp.T; }
+
+static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   PairBufs b{};
+  const size_t ecap = echo_cap_of(fp), mcap = muffle_cap_of(fp), max_pairs = ecap + mcap;
   uint8_t* p = static_cast<uint8_t*>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) { uint8_t* q = p ? p + off : nullptr; off += align256(bytes); return q; };
-  b.pairs = reinterpret_cast<PairG*>(take(max_pairs * sizeof(PairG)));
-  if (ART_VIS_SORT && max_pairs) {
-    b.keys = reinterpret_cast<uint16_t*>(take(max_pairs * 2));
-    b.keys_s = reinterpret_cast<uint16_t*>(take(max_pairs * 2));
-    b.vals = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
-    b.order = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
+  b.vp.seg = reinterpret_cast<float4*>(take(max_pairs * 32));
+  b.vp.out = reinterpret_cast<uint2*>(take(max_pairs * 8));
+  b.vp.flag = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
+  b.vp.echo_cap = (uint32_t)ecap;
+  if (ART_VIS_SORT && mcap) {
+    b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
+    b.nbins = fp.T << kSortDirBits;  // keys (target << kSortDirBits | cell) < T << kSortDirBits
+    const size_t cells = (size_t)b.nbins * b.nblk;
+    b.keys = reinterpret_cast<uint16_t*>(take(mcap * 2));
+    b.order = reinterpret_cast<uint32_t*>(take(mcap * 4));
+    b.hist = reinterpret_cast<uint32_t*>(take(cells * 4));
+    b.start = reinterpret_cast<uint32_t*>(take(cells * 4));
     static thread_local size_t last_n = 0, last_tb = 0;  // the size query is per item count
-    if (last_n != max_pairs) {
+    if (last_n != cells) {
       size_t tb = 0;
-      if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint16_t*)nullptr, (uint16_t*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)max_pairs, 0, 16) != hipSuccess)
+      if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells) != hipSuccess)
         tb = 0;
-      last_n = max_pairs;
+      last_n = cells;
       last_tb = tb;
     }
-    const size_t tb = last_tb;
-    b.temp_bytes = tb;
-    b.temp = take(tb);
+    b.temp_bytes = last_tb;
+    b.temp = take(last_tb);
   }
   b.total = off;
   return b;
 }
 
-static size_t max_pairs_of(const FrameParams& fp) { return (size_t)fp.S * fp.R * fp.H * (fp.T + 1); }
-
-size_t fast_pair_bytes(const FrameParams& fp) {
-  return ART_FAST_SPLIT ? pair_bufs(nullptr, max_pairs_of(fp)).total : 0;
-}
+size_t fast_pair_bytes(const FrameParams& fp) { return ART_FAST_SPLIT ? pair_bufs(nullptr, fp).total : 0; }
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,
                           uint32_t* pair_count, hipStream_t st) {
   if (fp.S == 0) return;
-  const size_t max_pairs = max_pairs_of(fp);
-  const PairBufs pb = pair_bufs(ART_FAST_SPLIT ? pair_buf : nullptr, ART_FAST_SPLIT ? max_pairs : 0);
-  const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && max_pairs && pb.temp_bytes && max_pairs < (1u << 31);
-  static_assert(kKeyUnused == 0xFFFF, "unused slots are cleared with byte 0xFF");
-  if (sorted) (void)hipMemsetAsync(pb.keys, 0xFF, max_pairs * 2, st);  // unused slots sort last
+  const PairBufs pb = pair_bufs(ART_FAST_SPLIT ? pair_buf : nullptr, fp);
+  const size_t mcap = muffle_cap_of(fp), max_pairs = (size_t)pb.vp.echo_cap + mcap;
+  const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && mcap && pb.temp_bytes && max_pairs < (1u << 31);
   uint16_t* pkeys = sorted ? pb.keys : nullptr;
-  uint32_t* pvals = sorted ? pb.vals : nullptr;
   if (ART_FAST_BVH && sc.bvh_levels > 0) {
-    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st);
+    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st);
   } else switch (fast_split(fp.S, fp.R)) {
-    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st); break;
-    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.pairs, pair_count, pkeys, pvals, st); break;
+    case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st); break;
+    default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st); break;
   }
 #if ART_FAST_SPLIT
-  const uint32_t nb_max = (uint32_t)((max_pairs + 63) / 64);
-  const size_t items = (size_t)nb_max * kVisRanges;
+  const uint32_t nb_max = (uint32_t)(pb.vp.echo_cap / 64 + (mcap + 63) / 64);
+  const size_t items = (size_t)nb_max * vis_ranges(sc);
   if (items) {
     if (sorted) {
+      hipLaunchKernelGGL(pair_hist_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.hist, pb.nblk,
+                         pb.nbins);
       size_t tb = pb.temp_bytes;
-      (void)hipcub::DeviceRadixSort::SortPairs(pb.temp, tb, pb.keys, pb.keys_s, pb.vals, pb.order, (int)max_pairs, 0, 16, st);
+      (void)hipcub::DeviceScan::ExclusiveSum(pb.temp, tb, pb.hist, pb.start, pb.nbins * pb.nblk, st);
+      hipLaunchKernelGGL(pair_scatter_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.start,
+                         pb.order, pb.nblk, pb.nbins);
     }
+    const uint32_t* order = sorted ? (const uint32_t*)pb.order : nullptr;
     if (fp.vis_bvh && sc.bvh_levels > 0)  // ART_CTX_VIS_BVH (measured 1.7x slower than vis_kernel on config 2)
       hipLaunchKernelGGL(vis_bvh_kernel, dim3((unsigned)((nb_max + kVisBvhWaves - 1) / kVisBvhWaves)), dim3(64 * kVisBvhWaves),
-                         (size_t)bvh_lds_nodes(sc) * sizeof(CullRec), st, sc, pb.pairs, pair_count, nb_max,
-                         sorted ? (const uint32_t*)pb.order : nullptr, fp.exec);
+                         (size_t)bvh_lds_nodes(sc) * sizeof(CullRec), st, sc, pb.vp, pair_count, nb_max, order, fp.exec);
     else
-      hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.pairs, pair_count, nb_max,
-                         sorted ? (const uint32_t*)pb.order : nullptr, fp.exec);
-    hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.pairs, pair_count, block,
+      hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
+                         fp.exec);
+    hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                        muffle_acc);
   }
 #endif
