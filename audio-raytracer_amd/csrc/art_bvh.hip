@@ -98,6 +98,35 @@ __global__ void gather_kernel(const int* __restrict__ perm, int ns, int na, int 
   }
 }
 
+// Refit of the sorted copies after colliders moved (same counts): every sorted record keeps its
+// position and is re-read from its original index (held in the record's pad field).
+__global__ void refit_gather_kernel(int ns, int na, int no, const SphereRec* __restrict__ sph,
+                                    const AabbRec* __restrict__ aabb, const ObbRec* __restrict__ obb,
+                                    const CullRec* __restrict__ cull, SphereRec* __restrict__ sph_s,
+                                    AabbRec* __restrict__ aabb_s, ObbRec* __restrict__ obb_s, CullRec* __restrict__ cull_s) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ns + na + no) return;
+  if (j < ns) {
+    const int g = sph_s[j].pad0;
+    SphereRec r = sph[g];
+    r.pad0 = g;
+    sph_s[j] = r;
+    cull_s[j] = cull[g];
+  } else if (j < ns + na) {
+    const int i = __float_as_int(aabb_s[j - ns].pad);
+    AabbRec r = aabb[i];
+    r.pad = __int_as_float(i);
+    aabb_s[j - ns] = r;
+    cull_s[j] = cull[ns + i];
+  } else {
+    const int i = __float_as_int(obb_s[j - ns - na].pad0);
+    ObbRec r = obb[i];
+    r.pad0 = __int_as_float(i);
+    obb_s[j - ns - na] = r;
+    cull_s[j] = cull[ns + na + i];
+  }
+}
+
 // One wave per chunk of 64 sorted colliders of one type: union of the members' bounds, largest
 // margin scale and factor.
 __global__ __launch_bounds__(64) void chunk_bounds_kernel(const CullRec* __restrict__ cull_s, int ns, int na, int no,
@@ -226,6 +255,8 @@ __device__ __forceinline__ CullRec cull_empty() {
 
 // Leaf j = sorted colliders [kBvhLeaf j, kBvhLeaf (j + 1)) (empty past the last); writes the
 // leaf references.
+// REFIT: the leaf order is kept (ref holds it) and only bounds and slots are recomputed.
+template <bool REFIT>
 __global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __restrict__ perm, int ns, int na, int n,
                                 const SphereRec* __restrict__ sph, const AabbRec* __restrict__ aabb,
                                 const ObbRec* __restrict__ obb, CullRec* __restrict__ leaves, int nleaf,
@@ -242,7 +273,13 @@ __global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __r
     float4 a = make_float4(0, 0, 0, 0), b = a, c = a, d = a;
     int code = -1;
     if (k < n) {
-      const int g = perm[k];
+      int g;
+      if (REFIT) {
+        const uint32_t r = ref[k], t = r >> 30, i = r & 0x3fffffffu;
+        g = (int)i + (t == 0 ? 0 : (t == 1 ? ns : ns + na));
+      } else {
+        g = perm[k];
+      }
       cull_union(u, cull[g]);
       if (g < ns) {
         ref[k] = (uint32_t)g;
@@ -298,10 +335,30 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, sb.keys, sb.keys_s, sb.vals, sb.perm, n, 0, 30, st) != hipSuccess)
     return -1;
   const int nleaf = total - leaf0;
-  hipLaunchKernelGGL(bvh_leaf_kernel, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, sb.perm, sc.ns, sc.na, n,
+  hipLaunchKernelGGL(bvh_leaf_kernel<false>, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, sb.perm, sc.ns, sc.na, n,
                      sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
   if (L > 1) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, sb.bvh, L);
   sc.bvh = sb.bvh; sc.bvh_ref = sb.bvh_ref; sc.bvh_leaf = sb.bvh_leaf; sc.bvh_levels = L; sc.bvh_leaf0 = leaf0;
+  return 0;
+}
+
+// Colliders moved but their counts did not: keep every order (per-type sorted copies, BVH leaf
+// order) and recompute records and bounds in place (4 kernels instead of the 11 of a rebuild).
+// Bounds stay exact unions, so the culls stay exact; only their tightness drifts until the next
+// rebuild (a count change, or art_scene_bind).
+int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
+  const int n = sc.ns + sc.na + sc.no;
+  if (n == 0 || sc.cull_s == nullptr) return launch_sort_scene(sc, sb, st);
+  hipLaunchKernelGGL(refit_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.ns, sc.na, sc.no, sc.sph, sc.aabb,
+                     sc.obb, sc.cull, sb.sph_s, sb.aabb_s, sb.obb_s, sb.cull_s);
+  const int nch = (sc.ns + 63) / 64 + (sc.na + 63) / 64 + (sc.no + 63) / 64;
+  hipLaunchKernelGGL(chunk_bounds_kernel, dim3(nch), dim3(64), 0, st, sb.cull_s, sc.ns, sc.na, sc.no, sb.chunks);
+  if (sc.bvh_levels > 0) {
+    const int leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1;  // 4^(L-1) leaves
+    hipLaunchKernelGGL(bvh_leaf_kernel<true>, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, (const int*)nullptr,
+                       sc.ns, sc.na, n, sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
+    if (sc.bvh_levels > 1) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, sb.bvh, sc.bvh_levels);
+  }
   return 0;
 }
 

@@ -118,6 +118,12 @@ struct Device {
   int fan_begin = 0, fan_count = 0;
   DevScene sc{};
   SortBufs sb{};  // buffers of the spatially sorted scene copy (art_bvh.hip), set by upload_scene
+  // resident scenes: the sorted copies / BVH in dv.soa were built for store generation sorted_gen
+  // (~0: none) with these counts; later frames reuse them (refit when the store changed)
+  uint64_t sorted_gen = ~0ull;
+  const void* sorted_soa = nullptr;
+  int sorted_n[3] = {-1, -1, -1};
+  DevScene sorted_sc{};
   bool bound = false;
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
   std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
@@ -150,6 +156,7 @@ struct art_ctx {
   } kinds[3];
   int synced[3] = {0, 0, 0};
   bool store_synced = false;
+  uint64_t sync_gen = 0;         // bumped by every art_colliders_sync that changed a record
   // audio_target_id of every synced record and their histogram (index = id + 32768), kept
   // incrementally from the dirty records (permeation loss test counts of counting frames)
   std::vector<int16_t> synced_tid[3];
@@ -415,8 +422,24 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sc.sph_s = nullptr; sc.aabb_s = nullptr; sc.obb_s = nullptr; sc.cull_s = nullptr; sc.chunks = nullptr; sc.nchunks = 0;
   sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
   dv.sb = sb;
-  if (fast_uses_sorted_scene() && launch_sort_scene(sc, sb, dv.stream) != 0)
-    return fail(c, ART_E_DEVICE, "collider sort failed");
+  if (fast_uses_sorted_scene()) {
+    const bool reuse = f.resident && dv.sorted_gen != ~0ull && dv.sorted_soa == dv.soa.p && dv.sorted_n[0] == f.ns &&
+                       dv.sorted_n[1] == f.na && dv.sorted_n[2] == f.no;
+    if (reuse) {  // same resident colliders (or only moved ones): keep the orders, refit if needed
+      const DevScene& o = dv.sorted_sc;
+      sc.sph_s = o.sph_s; sc.aabb_s = o.aabb_s; sc.obb_s = o.obb_s; sc.cull_s = o.cull_s; sc.chunks = o.chunks;
+      sc.nchunks = o.nchunks; sc.bvh = o.bvh; sc.bvh_ref = o.bvh_ref; sc.bvh_leaf = o.bvh_leaf;
+      sc.bvh_levels = o.bvh_levels; sc.bvh_leaf0 = o.bvh_leaf0;
+      if (dv.sorted_gen != c->sync_gen && launch_refit_scene(sc, sb, dv.stream) != 0)
+        return fail(c, ART_E_DEVICE, "collider refit failed");
+    } else if (launch_sort_scene(sc, sb, dv.stream) != 0) {
+      return fail(c, ART_E_DEVICE, "collider sort failed");
+    }
+    dv.sorted_gen = f.resident ? c->sync_gen : ~0ull;
+    dv.sorted_soa = dv.soa.p;
+    dv.sorted_n[0] = f.ns; dv.sorted_n[1] = f.na; dv.sorted_n[2] = f.no;
+    dv.sorted_sc = sc;
+  }
   HIP_TRY(c, hipGetLastError());
   dv.bound = true;
   return ART_OK;
@@ -1075,6 +1098,7 @@ ART_API int art_colliders_sync(art_ctx* c) {
     off_rec[k] = bytes; bytes = align_up(bytes + lists[k].size() * kRecSize[k], 16);
   }
   const int nd = (int)(lists[0].size() + lists[1].size() + lists[2].size());
+  if (nd || counts_changed) ++c->sync_gen;  // resident frames refit / rebuild their sorted copies
   for (Device& dv : c->devs) {  // the previous sync's copy may still read the pinned staging
     if (dv.st_pending) {
       HIP_TRY(c, hipSetDevice(dv.id));
@@ -1155,9 +1179,10 @@ ART_API int art_colliders_sync(art_ctx* c) {
         dv.sc.aabb = t.aabb; dv.sc.aabbc = t.aabbc; dv.sc.na = t.na;
         dv.sc.obb = t.obb; dv.sc.obbc = t.obbc; dv.sc.no = t.no;
         dv.sc.cull = t.cull;
-        // moved colliders move in the sorted copy too: sort again (device only, no H2D)
+        // moved colliders: refit the sorted copies and the BVH in place (device only, no H2D)
         if (fast_uses_sorted_scene() && nd) {
-          if (launch_sort_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider sort failed");
+          if (launch_refit_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider refit failed");
+          if (dv.sorted_gen != ~0ull) dv.sorted_gen = c->sync_gen;
           HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));  // device-path launches wait for the sort too
         }
       }

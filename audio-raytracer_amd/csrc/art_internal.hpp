@@ -116,6 +116,9 @@ int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
 size_t bvh_node_count(int n);
 size_t bvh_slot_count(int n);
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
+// Colliders moved, counts unchanged: recompute the sorted copies' records, chunk bounds and the
+// BVH's bounds and leaf slots in place, keeping every order.
+int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
 
 // Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
 struct FanLayout {

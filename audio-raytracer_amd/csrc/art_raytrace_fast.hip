@@ -1439,15 +1439,14 @@ __global__ __launch_bounds__(256) void vis_finalize(VisPairs vp, const uint32_t*
   const bool vis = valid && flag == 0u;
   const bool muf = (val & kPairMuffle) != 0;
   if (vis && !muf) reinterpret_cast<uint16_t*>(block)[dest] = (uint16_t)(val & 0xffffu);  // :142-144
-  // muffle counts (:171): one atomic per wave when the wave shares its counter
-  const unsigned long long mv = __ballot(vis && muf);
-  if (mv) {
+  // muffle counts (:171): one atomic per distinct counter of the wave (its pairs come from one or
+  // two (fan, target) groups of the emission order)
+  unsigned long long mv = __ballot(vis && muf);
+  while (mv) {
     const uint32_t d0 = __builtin_amdgcn_readlane(dest, __builtin_ctzll(mv));
-    if (__all(!(vis && muf) || dest == d0)) {
-      if (lane == 0) atomicAdd(&muffle_acc[d0], (uint32_t)__popcll(mv));
-    } else if (vis && muf) {
-      atomicAdd(&muffle_acc[dest], 1u);
-    }
+    const unsigned long long eq = __ballot(vis && muf && dest == d0);
+    if (lane == 0) atomicAdd(&muffle_acc[d0], (uint32_t)__popcll(eq));
+    mv &= ~eq;
   }
 }
 
