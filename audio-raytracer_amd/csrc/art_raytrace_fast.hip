@@ -484,7 +484,8 @@ __device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bo
           r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qd.x; r.lmxz = qd.y;
           h = obb_test<false>(s, r, stored_q(r), d); ++nt2;
         }
-        if (h && (d < best || (d == best && cc < code))) { best = d; code = cc; }
+        // a distance of exactly FLT_MAX never wins (the reference starts at float.MaxValue, strict <)
+        if (h && d < FLT_MAX && (d < best || (d == best && cc < code))) { best = d; code = cc; }
       }
       g = sp ? (int)stk[(sp - 1) * 64 + lane] : -1;
       sp = sp ? sp - 1 : 0;
@@ -502,6 +503,131 @@ __device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bo
       exec_add(ex, kExecCullCone, wave_sum_u32(ndiag) + ((unsigned long long)mx << 32));
     }
 #endif
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Quad-per-ray BVH traversal (nearest_bvh_quad): the K = 4 waves of a workgroup hold the same 64
+// ray states (lane = ray, as the K-way split does); in the nearest-hit phase wave w traverses rays
+// 16w .. 16w + 15 with 4 lanes per ray: lane q of a quad tests child q of an inner node or slot q
+// of a leaf, the quad exchanges the four results through DPP quad permutes and every lane applies
+// the same near-first ordering, so the ray's stack and current node stay identical in the quad.
+// Four times the waves of one-lane-per-ray traversal (latency hiding at config 2's 2048 groups),
+// and the inner-node / leaf steps are one test per lane instead of four.
+// ------------------------------------------------------------------------------------------
+template <int SEL>
+__device__ __forceinline__ int quad_bcast(int v) {
+  return __builtin_amdgcn_mov_dpp(v, SEL | (SEL << 2) | (SEL << 4) | (SEL << 6), 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ int quad_perm(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false); }
+constexpr int kQuadXor1 = 1 | (0 << 2) | (3 << 4) | (2 << 6), kQuadXor2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);
+
+// Ray r of the group (this wave's lanes 4 (r - 16 w) .. + 3) from lane r's state; writes
+// s_best[r] / s_code[r] (the q = 0 lane). stk = [64 rays][kBvhStack] u16.
+__device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& own, bool own_alive, int w, int lane,
+                                                 uint16_t* stk, float* s_best, int* s_code, unsigned long long* ex) {
+  const int qd = lane & 3, rr = 16 * w + (lane >> 2);
+  Seg s;
+  s.o = mk3(__shfl(own.o.x, rr, 64), __shfl(own.o.y, rr, 64), __shfl(own.o.z, rr, 64));
+  s.d = mk3(__shfl(own.d.x, rr, 64), __shfl(own.d.y, rr, 64), __shfl(own.d.z, rr, 64));
+  s.inv = mk3(__shfl(own.inv.x, rr, 64), __shfl(own.inv.y, rr, 64), __shfl(own.inv.z, rr, 64));
+  s.a2 = __shfl(own.a2, rr, 64);
+  s.a4 = __shfl(own.a4, rr, 64);
+  const bool alive = __shfl((int)own_alive, rr, 64) != 0;
+  float best = FLT_MAX;
+  int code = kNoHit;
+  unsigned nt0 = 0, nt1 = 0, nt2 = 0, nnode = 0;
+  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
+  const bool force = !(isfinite(om) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
+                     (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
+  const int leaf0 = sc.bvh_leaf0;
+  uint16_t* my = stk + rr * kBvhStack;
+  int g = alive ? 0 : -1, sp = 0;
+  while (__any(g >= 0)) {
+    while (g >= 0 && g < leaf0) {  // quad-uniform: the 4 lanes of a ray stay together
+      const int c0 = 4 * g + 1;
+      if (qd == 0) ++nnode;
+      const CullRec r = sc.bvh[c0 + qd];
+      const float m = r.factor * (r.scale + om);
+      float tn, tf;
+      const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m,
+                                 r.hix + m, r.hiy + m, r.hiz + m, tn, tf);
+      const float en = fmaxf(tn, 0.0f);
+      const bool live = r.lox <= r.hix;
+      const float ek = (live && (force || (h && en <= best))) ? (force ? 0.0f : en) : INFINITY;
+      const int eb = __float_as_int(ek);
+      float e[4] = {__int_as_float(quad_bcast<0>(eb)), __int_as_float(quad_bcast<1>(eb)),
+                    __int_as_float(quad_bcast<2>(eb)), __int_as_float(quad_bcast<3>(eb))};
+      int c[4] = {0, 1, 2, 3};
+      auto cswap = [&](int a, int b) {
+        if (e[b] < e[a]) { const float te = e[a]; e[a] = e[b]; e[b] = te; const int tc = c[a]; c[a] = c[b]; c[b] = tc; }
+      };
+      cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
+      if (e[0] < INFINITY) {
+#pragma unroll
+        for (int k = 3; k >= 1; --k)
+          if (e[k] < INFINITY) {
+            if (qd == 0) my[sp] = (uint16_t)(c0 + c[k]);
+            ++sp;
+          }
+        g = c0 + c[0];
+      } else {
+        g = sp ? (int)my[sp - 1] : -1;
+        sp = sp ? sp - 1 : 0;
+      }
+    }
+    if (g >= leaf0) {
+      const float4* sl = sc.bvh_leaf + (size_t)(g - leaf0) * (4 * kBvhLeaf) + 4 * qd;
+      const float4 qa = sl[0], qb = sl[1];
+      const int cc = __float_as_int(qb.w);
+      float d = INFINITY;
+      int dc = kNoHit;
+      if (cc >= 0) {
+        const int t = cc >> 28;
+        float dd = 0.0f;
+        bool h;
+        if (t == 0) {
+          SphereRec r;
+          r.cx = qa.x; r.cy = qa.y; r.cz = qa.z; r.r2 = qa.w;
+          h = sphere_hit_dist(s, r, dd); ++nt0;
+        } else if (t == 1) {
+          AabbRec r;
+          r.mnx = qa.x; r.mny = qa.y; r.mnz = qa.z; r.mxx = qa.w; r.mxy = qb.x; r.mxz = qb.y;
+          h = aabb_test<false>(s, r, dd); ++nt1;
+        } else {
+          const float4 qc = sl[2], qe = sl[3];
+          ObbRec r;
+          r.cx = qa.x; r.cy = qa.y; r.cz = qa.z;
+          r.qx = qa.w; r.qy = qb.x; r.qz = qb.y; r.qw = qb.z;
+          r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qe.x; r.lmxz = qe.y;
+          h = obb_test<false>(s, r, stored_q(r), dd); ++nt2;
+        }
+        // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue)
+        if (h && dd < FLT_MAX) { d = dd; dc = cc; }
+      }
+      // (distance, order) minimum over the quad's four slots
+      {
+        const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(d)));
+        const int oc = quad_perm<kQuadXor1>(dc);
+        if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
+      }
+      {
+        const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(d)));
+        const int oc = quad_perm<kQuadXor2>(dc);
+        if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
+      }
+      if (d < best || (d == best && dc < code)) { best = d; code = dc; }
+      g = sp ? (int)my[sp - 1] : -1;
+      sp = sp ? sp - 1 : 0;
+    }
+  }
+  if (qd == 0) { s_best[rr] = best; s_code[rr] = code; }
+  if (ex) {
+    exec_add(ex, kExecSphere, wave_sum_u32(nt0));
+    exec_add(ex, kExecAabb, wave_sum_u32(nt1));
+    exec_add(ex, kExecObb, wave_sum_u32(nt2));
+    exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nnode));
   }
 }
 
@@ -1478,7 +1604,7 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 
 // MULTI = false: frames with one hit per ray (H == 1, configs 2-4) compile without the later-bounce
 // nearest sweep and the reflection, which removes their registers from the kernel.
-template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD>
 __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
@@ -1490,7 +1616,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                uint16_t* __restrict__ pkeys) {
   // BVH: the K waves of a workgroup are independent (each pulls its own 64-ray groups and owns
   // their writes); they share the workgroup's LDS copy of the top BVH nodes.
-  constexpr bool IND = BVH;
+  // QUAD: the K = 4 waves hold the same 64 rays and split the nearest-hit traversal 16 rays each
+  // (nearest_bvh_quad); results meet in LDS as the K-way split's partials do.
+  constexpr bool IND = BVH && !QUAD;
   __shared__ float s_dist[K][64];
   __shared__ float s_best[K][64];  // running per-lane best of each wave (front-to-back pruning)
   (void)s_best;
@@ -1502,7 +1630,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   __shared__ uint32_t s_muf[kMaxTargets];
   __shared__ int s_ticket[IND ? K : 1];
   __shared__ int s_go[3];  // staged visibility only
-  __shared__ uint16_t s_stk[BVH ? kBvhStack * 64 * K : 1];  // per-lane BVH traversal stacks
+  __shared__ uint16_t s_stk[QUAD ? kBvhStack * 64 : (BVH ? kBvhStack * 64 * K : 1)];  // BVH traversal stacks
   (void)s_stk;
   (void)s_go; (void)s_pairof; (void)s_res; (void)s_head; (void)s_np;
 #ifdef ART_TEST_NO_OBB
@@ -1518,9 +1646,9 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   const int ngroups = fp.S * nrb;
   // BVH: the top bvh_lds_nodes(...) nodes in LDS (dynamic shared memory, BVH mode only)
   const CullRec* s_nodes = reinterpret_cast<const CullRec*>(s_seg);
-  const int nl = BVH ? bvh_lds_nodes(sc) : 0;
+  const int nl = IND ? bvh_lds_nodes(sc) : 0;
   (void)s_nodes; (void)nl;
-  if (BVH) {
+  if (IND) {
     CullRec* dst = reinterpret_cast<CullRec*>(s_seg);
     for (int i = threadIdx.x; i < nl; i += blockDim.x) dst[i] = sc.bvh[i];
     __syncthreads();
@@ -1530,12 +1658,16 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   // round of workgroups, and uneven visibility work balances itself).
   // BVH (independent waves): a static grid-stride assignment of groups to waves (a ticket per wave
   // would serialize on one counter: about 88 dequeues per microsecond).
-  int gnext = (int)blockIdx.x * K + w;
+  int gnext = IND ? (int)blockIdx.x * K + w : (int)blockIdx.x;
   for (;;) {
   int g;
   if (IND) {
     g = gnext;
     gnext += (int)gridDim.x * K;
+  } else if (QUAD) {  // static assignment, one group per workgroup
+    __syncthreads();  // the previous group's LDS reads are done
+    g = gnext;
+    gnext += (int)gridDim.x;
   } else {
     __syncthreads();  // the previous group's LDS reads are done
     if (threadIdx.x == 0) s_ticket[0] = (int)atomicAdd(&work[0], 1u);
@@ -1591,7 +1723,15 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     float best;
     int code;
 #if ART_FAST_CULL
-    if (BVH) {
+    if (BVH && QUAD) {
+#ifdef ART_DIAG_NO_NEAREST  // diagnostic build only: every live ray hits sphere 0 at distance 1
+      if (w == 0) { s_dist[0][lane] = alive ? 1.0f : FLT_MAX; s_code[0][lane] = alive ? 0 : kNoHit; }
+#else
+      nearest_bvh_quad(sc, s, alive, w, lane, s_stk, &s_dist[0][0], &s_code[0][0], fp.exec);
+#endif
+      best = FLT_MAX;
+      code = kNoHit;
+    } else if (BVH) {
 #ifdef ART_DIAG_NO_NEAREST  // diagnostic build only: every live ray hits sphere 0 at distance 1
       best = alive ? 1.0f : FLT_MAX; code = alive ? 0 : kNoHit;
 #else
@@ -1614,7 +1754,11 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #endif
     float bd = best;
     int bc = code;
-    if (!IND) {
+    if (QUAD) {
+      __syncthreads();
+      bd = s_dist[0][lane];
+      bc = s_code[0][lane];
+    } else if (!IND) {
       s_dist[w][lane] = best;
       s_code[w][lane] = code;
       __syncthreads();
@@ -1841,7 +1985,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   }
   // Every workgroup has drawn its final (out-of-range) ticket before it arrives here, so the last
   // arrival can rearm the counter for the next launch on this stream.
-  if (!IND && threadIdx.x == 0 && atomicAdd(&work[1], 1u) == gridDim.x - 1) {
+  if (!BVH && threadIdx.x == 0 && atomicAdd(&work[1], 1u) == gridDim.x - 1) {
     atomicExch(&work[0], 0u);
     atomicExch(&work[1], 0u);
 #ifdef ART_DIAG_CULL_STATS
@@ -1889,18 +2033,20 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
   return blocks;
 }
 
-template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD = false>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
                            uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
-  const size_t lds = BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T);
+  const size_t lds = QUAD ? 0 : (BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T));
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   // BVH: K independent waves per workgroup, one group each (grid-stride past 2^31 / K groups);
-  // otherwise a persistent grid of co-resident workgroups pulling groups from a ticket counter
-  const int nblk = BVH ? (int)std::min<long long>((groups + K - 1) / K, 1ll << 30)
-                       : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH>,
-                                                                          64 * K, lds));
-  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins,
+  // quad BVH: one group per workgroup; otherwise a persistent grid of co-resident workgroups
+  // pulling groups from a ticket counter
+  const int nblk = QUAD ? (int)std::min<long long>(groups, 1ll << 30)
+                 : BVH  ? (int)std::min<long long>((groups + K - 1) / K, 1ll << 30)
+                        : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD>,
+                                                                            64 * K, lds));
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins,
                      block, muffle_acc, ray_order, work, pairs, pair_count, pkeys);
 }
 
@@ -1928,16 +2074,37 @@ static_assert(!ART_FAST_BVH || ART_FAST_SPLIT, "the BVH path kernel emits visibi
 #define ART_FAST_BVH_WAVES 8  // independent waves per workgroup sharing the LDS node cache
 #endif
 
-// BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal.
+#ifndef ART_FAST_WPE_QUAD
+#define ART_FAST_WPE_QUAD 4
+#endif
+#ifndef ART_FAST_QUAD_GROUPS
+#define ART_FAST_QUAD_GROUPS 8192  // quad traversal up to this many 64-ray groups per launch (config 2/3/5:
+                                   // 2048 groups, quad 16 / 10 / 1 % faster; config 4: 16384, lanes 3 % faster)
+#endif
+static bool bvh_quad(const FrameParams& fp) {
+  return (long long)fp.S * ((fp.R + 63) / 64) <= (long long)ART_FAST_QUAD_GROUPS;
+}
+
+// BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal; or (quad)
+// 4 waves per group, 4 lanes per ray.
 static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                             uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
                             uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
 #define ART_LAUNCH(H_, M_) \
   launch_fast_kh<ART_FAST_BVH_WAVES, H_, 1, ART_FAST_WPE_BVH, M_, true>(sc, fp, L, origins, block, muffle_acc, ray_order, \
                                                                         work, pairs, pair_count, pkeys, st)
+#define ART_LAUNCH_Q(H_, M_) \
+  launch_fast_kh<4, H_, 1, ART_FAST_WPE_QUAD, M_, true, true>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, \
+                                                              pair_count, pkeys, st)
   const bool multi = fp.H > 1;
-  if (L.has_hits) { if (multi) ART_LAUNCH(true, true); else ART_LAUNCH(true, false); }
-  else { if (multi) ART_LAUNCH(false, true); else ART_LAUNCH(false, false); }
+  if (bvh_quad(fp)) {
+    if (L.has_hits) { if (multi) ART_LAUNCH_Q(true, true); else ART_LAUNCH_Q(true, false); }
+    else { if (multi) ART_LAUNCH_Q(false, true); else ART_LAUNCH_Q(false, false); }
+  } else {
+    if (L.has_hits) { if (multi) ART_LAUNCH(true, true); else ART_LAUNCH(true, false); }
+    else { if (multi) ART_LAUNCH(false, true); else ART_LAUNCH(false, false); }
+  }
+#undef ART_LAUNCH_Q
 #undef ART_LAUNCH
 }
 
