@@ -515,6 +515,9 @@ __device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bo
 // Four times the waves of one-lane-per-ray traversal (latency hiding at config 2's 2048 groups),
 // and the inner-node / leaf steps are one test per lane instead of four.
 // ------------------------------------------------------------------------------------------
+#ifndef ART_QUAD_FULL_SORT
+#define ART_QUAD_FULL_SORT 2  // 0: nearest child first, the rest in index order; 1: full near-first
+#endif                        // order; 2: full order for scenes with OBBs (config 3 -1 %, config 2 +5 %)
 template <int SEL>
 __device__ __forceinline__ int quad_bcast(int v) {
   return __builtin_amdgcn_mov_dpp(v, SEL | (SEL << 2) | (SEL << 4) | (SEL << 6), 0xf, 0xf, false);
@@ -543,6 +546,7 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
                      (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
   const int leaf0 = sc.bvh_leaf0;
   uint16_t* my = stk + rr * kBvhStack;
+  const bool full_sort = ART_QUAD_FULL_SORT == 1 || (ART_QUAD_FULL_SORT == 2 && sc.no > 0);
   int g = alive ? 0 : -1, sp = 0;
   while (__any(g >= 0)) {
     while (g >= 0 && g < leaf0) {  // quad-uniform: the 4 lanes of a ray stay together
@@ -556,6 +560,7 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
       const float en = fmaxf(tn, 0.0f);
       const bool live = r.lox <= r.hix;
       const float ek = (live && (force || (h && en <= best))) ? (force ? 0.0f : en) : INFINITY;
+      if (full_sort) {  // far-to-near pushes (sorting network); pays for OBB scenes' long leaf tests
       const int eb = __float_as_int(ek);
       float e[4] = {__int_as_float(quad_bcast<0>(eb)), __int_as_float(quad_bcast<1>(eb)),
                     __int_as_float(quad_bcast<2>(eb)), __int_as_float(quad_bcast<3>(eb))};
@@ -575,6 +580,33 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
       } else {
         g = sp ? (int)my[sp - 1] : -1;
         sp = sp ? sp - 1 : 0;
+      }
+      } else {
+      // descend into the nearest child ((entry, index) minimum over the quad, two DPP steps); the
+      // other entered children go on the stack in index order, each lane writing its own
+      float mn = ek;
+      int mi = qd;
+      {
+        const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(mn)));
+        const int oi = quad_perm<kQuadXor1>(mi);
+        if (od < mn || (od == mn && oi < mi)) { mn = od; mi = oi; }
+      }
+      {
+        const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(mn)));
+        const int oi = quad_perm<kQuadXor2>(mi);
+        if (od < mn || (od == mn && oi < mi)) { mn = od; mi = oi; }
+      }
+      const int qshift = lane & ~3;
+      const bool push = ek < INFINITY && qd != mi;
+      const uint32_t pb = (uint32_t)(__ballot(push) >> qshift) & 0xFu;
+      if (mn < INFINITY) {
+        if (push) my[sp + __popc(pb & ((1u << qd) - 1u))] = (uint16_t)(c0 + qd);
+        sp += __popc(pb);
+        g = c0 + mi;
+      } else {
+        g = sp ? (int)my[sp - 1] : -1;
+        sp = sp ? sp - 1 : 0;
+      }
       }
     }
     if (g >= leaf0) {
@@ -1756,6 +1788,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     int bc = code;
     if (QUAD) {
       __syncthreads();
+      // one bounce: waves 1-3 were only needed for the traversal; wave 0 owns the rest
+      if (!MULTI && w != 0) break;
       bd = s_dist[0][lane];
       bc = s_code[0][lane];
     } else if (!IND) {
