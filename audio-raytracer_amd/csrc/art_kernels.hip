@@ -522,20 +522,37 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
 
   const uint16_t* echo = reinterpret_cast<const uint16_t*>(fb + L.echo_off);
   const int n = fp.R * fp.H;
+  // The echo sum (:42-47) must add in index order. Zeros only count as returned, but adding a
+  // zero leaves the running sum unchanged (it starts at +0 and a round-to-nearest sum of non-zero
+  // terms is never -0), so every element is added: the wave converts a chunk to floats in LDS
+  // (coalesced loads, parallel conversion) and lane 0 accumulates it from 16-B LDS reads, with
+  // no cross-lane step per element.
+  constexpr int kChunkF = 4096;
+  __shared__ float4 s_f4[kChunkF / 4];
+  float* s_f = reinterpret_cast<float*>(s_f4);
   float total = 0.0f;
   uint32_t zeros = 0;
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + lane;
-    const bool in = i < n;
-    const float e = in ? f16tof32(echo[i]) : 0.0f;
-    zeros += __popcll(__ballot(in && e == 0.0f));
-    unsigned long long m = __ballot(in && e != 0.0f);
-    while (m) {
-      int j = __builtin_ctzll(m);
-      m &= m - 1;
-      total += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, e), j));
+  for (int base = 0; base < n; base += kChunkF) {
+    const int m = min(kChunkF, n - base);
+    for (int i0 = 0; i0 < m; i0 += 64) {
+      const int i = i0 + lane;
+      const bool in = i < m;
+      const float e = in ? f16tof32(echo[base + i]) : 0.0f;
+      if (in) s_f[i] = e;
+      zeros += __popcll(__ballot(in && e == 0.0f));
     }
+    __syncthreads();
+    if (lane == 0) {
+      int i = 0;
+      for (; i + 4 <= m; i += 4) {
+        const float4 v = s_f4[i >> 2];
+        total += v.x; total += v.y; total += v.z; total += v.w;
+      }
+      for (; i < m; ++i) total += s_f[i];
+    }
+    __syncthreads();
   }
+  total = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, total), 0));
   // echoRayReturnedHits is a float incremented by 1 (exact below 2^24).
   const float returned = (float)zeros;
   const float avg = total / (float)n;

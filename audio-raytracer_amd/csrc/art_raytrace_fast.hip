@@ -1179,24 +1179,29 @@ __device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet&
 // scene of art_bvh.hip): chunks [c_lo, c_hi) of the sorted order are tested as a whole first
 // (lane = chunk, union bounds), then the members of the candidate chunks. Any-hit is an OR over
 // the colliders, so the order is free. Returns the lane's verdict (true = blocked).
+// The box of a wave's segments [o, o + maxd d] (valid lanes) and the margin term max |o|_1 + maxd.
+__device__ __forceinline__ WaveBox make_wave_box(const Seg& s, float maxd, bool valid) {
+  WaveBox wb;
+  const vec3 e = s.o + s.d * maxd;
+  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+  wb.lx = wave_min(valid ? fminf(s.o.x, e.x) : INFINITY);
+  wb.ly = wave_min(valid ? fminf(s.o.y, e.y) : INFINITY);
+  wb.lz = wave_min(valid ? fminf(s.o.z, e.z) : INFINITY);
+  wb.hx = wave_max(valid ? fmaxf(s.o.x, e.x) : -INFINITY);
+  wb.hy = wave_max(valid ? fmaxf(s.o.y, e.y) : -INFINITY);
+  wb.hz = wave_max(valid ? fmaxf(s.o.z, e.z) : -INFINITY);
+  wb.om = wave_max(valid ? om : 0.0f);
+  return wb;
+}
+
+// wbp: a precomputed box of (a superset of) the wave's segments, else computed here.
 __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid, int lane,
                                            unsigned long long* ex, bool done_in = false, int c_lo = 0, int c_hi = 1 << 30,
-                                           const VisCone* vc = nullptr, bool two = false) {
+                                           const VisCone* vc = nullptr, bool two = false, const WaveBox* wbp = nullptr) {
   const ChunkMap cm = {(sc.ns + kChunk - 1) / kChunk, (sc.na + kChunk - 1) / kChunk, (sc.no + kChunk - 1) / kChunk};
   const int nchunks = min(cm.total(), c_hi);
   if (c_lo >= nchunks) return false;
-  WaveBox wb;
-  {
-    const vec3 e = s.o + s.d * maxd;
-    const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
-    wb.lx = wave_min(valid ? fminf(s.o.x, e.x) : INFINITY);
-    wb.ly = wave_min(valid ? fminf(s.o.y, e.y) : INFINITY);
-    wb.lz = wave_min(valid ? fminf(s.o.z, e.z) : INFINITY);
-    wb.hx = wave_max(valid ? fmaxf(s.o.x, e.x) : -INFINITY);
-    wb.hy = wave_max(valid ? fmaxf(s.o.y, e.y) : -INFINITY);
-    wb.hz = wave_max(valid ? fmaxf(s.o.z, e.z) : -INFINITY);
-    wb.om = wave_max(valid ? om : 0.0f);
-  }
+  const WaveBox wb = wbp ? *wbp : make_wave_box(s, maxd, valid);
   bool blocked = false;
   const bool done = !valid || done_in;
   if (__all(done)) return false;
@@ -1374,6 +1379,9 @@ __host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) { return 
 #ifndef ART_VIS_SORT
 #define ART_VIS_SORT 1  // visibility batches in (target, direction from the target) order (vis_sort_key)
 #endif
+#ifndef ART_VIS_DESC
+#define ART_VIS_DESC 0  // 1: batch box + cone computed once per batch (vis_batch_kernel): config 2 -3 us in vis_kernel, +12 us kernel
+#endif
 #ifndef ART_VIS_TWO_LEVEL
 #define ART_VIS_TWO_LEVEL 1  // vis_kernel walks the sorted scene's chunk bounds first (art_bvh.hip)
 #endif
@@ -1422,6 +1430,38 @@ __device__ __forceinline__ bool batch_pair(const VisPairs& vp, const uint32_t* c
   return true;
 }
 
+// Broad-phase descriptor of one 64-pair batch, computed once (vis_batch_kernel) for all its chunk
+// ranges: the segments' box and margin term, and the apex cone (cos2 <= 0: no cone).
+struct alignas(16) BatchDesc {
+  float lx, ly, lz, om;
+  float hx, hy, hz, extra;
+  float ax, ay, az, cos2;
+  float nx, ny, nz, sin_t;
+};
+
+__global__ __launch_bounds__(256) void vis_batch_kernel(VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
+                                                        const uint32_t* __restrict__ order, BatchDesc* __restrict__ desc) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t b = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t pi, n_in;
+  if (b >= nb_max || !batch_pair(vp, count, order, b, lane, pi, n_in)) return;
+  const bool valid = (uint32_t)lane < n_in;
+  Seg s;
+  float maxd;
+  int owner;
+  load_pair_seg(vp, pi, s, maxd, owner);
+  const WaveBox wb = make_wave_box(s, maxd, valid);
+  const VisCone vc = make_vis_cone(s, maxd, valid, wb.om);
+  if (lane == 0) {
+    BatchDesc d;
+    d.lx = wb.lx; d.ly = wb.ly; d.lz = wb.lz; d.om = wb.om;
+    d.hx = wb.hx; d.hy = wb.hy; d.hz = wb.hz; d.extra = vc.extra;
+    d.ax = vc.ax; d.ay = vc.ay; d.az = vc.az; d.cos2 = vc.on ? vc.cos2 : -1.0f;
+    d.nx = vc.nx; d.ny = vc.ny; d.nz = vc.nz; d.sin_t = vc.sin_t;
+    desc[b] = d;
+  }
+}
+
 // Work item i of vis_kernel = (chunk range r, batch b), range-major: r = i / nb_max, b = i % nb_max.
 // A batch's later ranges usually start after its earlier ones finished and skip the pairs those
 // already blocked (a stale read only costs work). Verdicts meet in VisPairs::flag through relaxed
@@ -1429,7 +1469,7 @@ __device__ __forceinline__ bool batch_pair(const VisPairs& vp, const uint32_t* c
 // vis_finalize writes the outputs after the kernel boundary.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
-                const uint32_t* __restrict__ order, unsigned long long* ex) {
+                const uint32_t* __restrict__ order, const BatchDesc* __restrict__ desc, unsigned long long* ex) {
   const int lane = threadIdx.x & 63;
   const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t r = item / nb_max, b = item - r * nb_max;
@@ -1455,9 +1495,20 @@ void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, ui
   const bool two = sc.chunks != nullptr && (ART_VIS_TWO_LEVEL || (ART_FAST_TWO_LEVEL && sc.nchunks > 64));
   const int c_lo = (int)(((long long)nch * r) / nranges), c_hi = (int)(((long long)nch * (r + 1)) / nranges);
 #if ART_VIS_CONE
-  const float om = wave_max(valid ? fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd : 0.0f);
-  const VisCone vc = make_vis_cone(s, maxd, valid, om);
-  const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, &vc, two);
+  bool blocked;
+  if (desc) {  // the batch's box and cone, computed once for its ranges (scalar loads)
+    const BatchDesc d = ldc(desc, (int)b);
+    WaveBox wb;
+    wb.lx = d.lx; wb.ly = d.ly; wb.lz = d.lz; wb.om = d.om; wb.hx = d.hx; wb.hy = d.hy; wb.hz = d.hz;
+    VisCone vc;
+    vc.ax = d.ax; vc.ay = d.ay; vc.az = d.az; vc.nx = d.nx; vc.ny = d.ny; vc.nz = d.nz;
+    vc.cos2 = d.cos2; vc.sin_t = d.sin_t; vc.extra = d.extra; vc.on = d.cos2 > 0.0f;
+    blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, &vc, two, &wb);
+  } else {
+    const float om = wave_max(valid ? fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd : 0.0f);
+    const VisCone vc = make_vis_cone(s, maxd, valid, om);
+    blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, &vc, two);
+  }
 #else
   const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, false, c_lo, c_hi, nullptr, two);
 #endif
@@ -2148,11 +2199,22 @@ bool fast_uses_sorted_scene() {
   return ART_FAST_TWO_LEVEL || ART_FAST_SORTED_NEAREST || (ART_FAST_SPLIT && ART_VIS_TWO_LEVEL) || ART_FAST_BVH;
 }
 
-// Counting sort of the muffle pairs by key (kSortBins buckets; the order inside a bucket is free:
-// the any-hit verdicts do not depend on it). Block j of kSortBlock pairs: LDS histogram -> column j
-// of hist[bin][block]; an exclusive scan over the matrix in (bin, block) order gives each block its
-// first position per bucket; the scatter hands out positions with LDS atomics.
+// Counting sort of the muffle pairs by key (T << kSortDirBits buckets; the order inside a bucket
+// is free: the any-hit verdicts do not depend on it). Block j of kSortBlock pairs: LDS histogram
+// -> row j of hist[block][bucket]; a column prefix per bucket and the buckets' totals; each
+// scatter block scans the totals and hands out positions with LDS atomics.
 constexpr int kSortThreads = 256, kSortBlock = 16 * kSortThreads;
+
+// The 16 keys of one thread with two 16-B loads (one memory latency). i0 is a multiple of 16 below
+// the key count and the key array is 256-B aligned and padded, so a read past the last key stays
+// in the buffer; those keys are ignored.
+__device__ __forceinline__ void load_keys16(const uint16_t* keys, uint32_t i0, uint16_t* kk) {
+  const uint4* p = reinterpret_cast<const uint4*>(keys + i0);
+  const uint4 a = p[0], b = p[1];
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { kk[2 * j] = (uint16_t)(w[j] & 0xffffu); kk[2 * j + 1] = (uint16_t)(w[j] >> 16); }
+}
 
 __global__ __launch_bounds__(kSortThreads) void pair_hist_kernel(const uint16_t* __restrict__ keys,
                                                                  const uint32_t* __restrict__ count,
@@ -2164,28 +2226,89 @@ __global__ __launch_bounds__(kSortThreads) void pair_hist_kernel(const uint16_t*
   // wave's rays are coherent, so per-key atomics would serialize on a few bins)
   const uint32_t n = ldc(count, 1), i0 = blockIdx.x * (uint32_t)kSortBlock + threadIdx.x * 16u;
   const uint32_t e = min(n, i0 + 16u);
+  uint16_t kk[16];
+  if (i0 < n) load_keys16(keys, i0, kk);
   uint32_t run = 0, rk = 0;
-  for (uint32_t i = i0; i < e; ++i) {
-    const uint32_t k = keys[i];
+#pragma unroll
+  for (uint32_t j = 0; j < 16u; ++j) {
+    if (i0 + j >= e) break;
+    const uint32_t k = kk[j];
     if (run && k != rk) { atomicAdd(&h[rk], run); run = 0; }
     rk = k;
     ++run;
   }
   if (run) atomicAdd(&h[rk], run);
   __syncthreads();
-  for (int i = threadIdx.x; i < nbins; i += kSortThreads) hist[(size_t)i * nblk + blockIdx.x] = h[i];
+  for (int i = threadIdx.x; i < nbins; i += kSortThreads) hist[(size_t)blockIdx.x * nbins + i] = h[i];  // row = block
 }
 
+// Column prefix: thread = bucket; hist[block][bucket] becomes the count of the bucket's keys in
+// earlier blocks, and tot[bucket] the bucket's total (rows are read and written coalesced).
+__global__ __launch_bounds__(64) void pair_colscan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ prefix,
+                                                          uint32_t* __restrict__ tot, int nblk, int nbins) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nbins) return;
+  uint32_t run = 0;
+  int b = 0;
+  for (; b + 8 <= nblk; b += 8) {  // 8 independent loads in flight per step
+    uint32_t c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = hist[(size_t)(b + j) * nbins + k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { prefix[(size_t)(b + j) * nbins + k] = run; run += c[j]; }
+  }
+  for (; b < nblk; ++b) {
+    const uint32_t c = hist[(size_t)b * nbins + k];
+    prefix[(size_t)b * nbins + k] = run;
+    run += c;
+  }
+  tot[k] = run;
+}
+
+// Each block scans the bucket totals itself (nbins <= kSortBins, 32 per thread) and adds its row
+// of column prefixes: cur[bucket] = first position of this block's keys of that bucket.
 __global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16_t* __restrict__ keys,
                                                                     const uint32_t* __restrict__ count,
-                                                                    const uint32_t* __restrict__ start,
+                                                                    const uint32_t* __restrict__ prefix,
+                                                                    const uint32_t* __restrict__ tot,
                                                                     uint32_t* __restrict__ order, int nblk, int nbins) {
   __shared__ uint32_t cur[kSortBins];
-  for (int i = threadIdx.x; i < nbins; i += kSortThreads) cur[i] = start[(size_t)i * nblk + blockIdx.x];
+  __shared__ uint32_t s_part[kSortThreads];
+  constexpr int kPer = kSortBins / kSortThreads;
+  const int t = threadIdx.x;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = t * kPer + j;
+    v[j] = k < nbins ? tot[k] : 0u;
+    sum += v[j];
+  }
+  s_part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < kSortThreads; off <<= 1) {  // inclusive scan of the per-thread sums
+    const uint32_t x = t >= off ? s_part[t - off] : 0u;
+    __syncthreads();
+    s_part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = s_part[t] - sum;  // exclusive
+  const uint32_t* row = prefix + (size_t)blockIdx.x * nbins;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = t * kPer + j;
+    if (k < nbins) cur[k] = run + row[k];
+    run += v[j];
+  }
   __syncthreads();
   const uint32_t n = ldc(count, 1), i0 = blockIdx.x * (uint32_t)kSortBlock + threadIdx.x * 16u;
   const uint32_t e = min(n, i0 + 16u);
-  for (uint32_t i = i0; i < e; ++i) order[atomicAdd(&cur[keys[i]], 1u)] = i;
+  uint16_t kk[16];
+  if (i0 < n) load_keys16(keys, i0, kk);
+#pragma unroll
+  for (uint32_t j = 0; j < 16u; ++j) {
+    if (i0 + j >= e) break;
+    order[atomicAdd(&cur[kk[j]], 1u)] = i0 + j;
+  }
 }
 
 // Pair buffer: VisPairs (seg | out | flag) | muffle keys u16 | sorted order u32 | hist, scanned
@@ -2193,9 +2316,9 @@ __global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16
 struct PairBufs {
   VisPairs vp;
   uint16_t* keys;
-  uint32_t *order, *hist, *start;
-  void* temp;
-  size_t temp_bytes, total;
+  uint32_t *order, *hist, *prefix, *tot;
+  BatchDesc* desc;  // [batches], when the batch descriptors are precomputed
+  size_t total;
   int nblk, nbins;
 };
 
@@ -2214,24 +2337,16 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   b.vp.out = reinterpret_cast<uint2*>(take(max_pairs * 8));
   b.vp.flag = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
   b.vp.echo_cap = (uint32_t)ecap;
+  b.desc = ART_VIS_DESC ? reinterpret_cast<BatchDesc*>(take((ecap / 64 + (mcap + 63) / 64) * sizeof(BatchDesc))) : nullptr;
   if (ART_VIS_SORT && mcap) {
     b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
     b.nbins = fp.T << kSortDirBits;  // keys (target << kSortDirBits | cell) < T << kSortDirBits
     const size_t cells = (size_t)b.nbins * b.nblk;
-    b.keys = reinterpret_cast<uint16_t*>(take(mcap * 2));
+    b.keys = reinterpret_cast<uint16_t*>(take(mcap * 2 + 64));  // + padding for load_keys16 past the end
     b.order = reinterpret_cast<uint32_t*>(take(mcap * 4));
     b.hist = reinterpret_cast<uint32_t*>(take(cells * 4));
-    b.start = reinterpret_cast<uint32_t*>(take(cells * 4));
-    static thread_local size_t last_n = 0, last_tb = 0;  // the size query is per item count
-    if (last_n != cells) {
-      size_t tb = 0;
-      if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells) != hipSuccess)
-        tb = 0;
-      last_n = cells;
-      last_tb = tb;
-    }
-    b.temp_bytes = last_tb;
-    b.temp = take(last_tb);
+    b.prefix = reinterpret_cast<uint32_t*>(take(cells * 4));
+    b.tot = reinterpret_cast<uint32_t*>(take((size_t)b.nbins * 4));
   }
   b.total = off;
   return b;
@@ -2245,7 +2360,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   if (fp.S == 0) return;
   const PairBufs pb = pair_bufs(ART_FAST_SPLIT ? pair_buf : nullptr, fp);
   const size_t mcap = muffle_cap_of(fp), max_pairs = (size_t)pb.vp.echo_cap + mcap;
-  const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && mcap && pb.temp_bytes && max_pairs < (1u << 31);
+  const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && mcap && pb.nbins <= kSortBins && max_pairs < (1u << 31);
   uint16_t* pkeys = sorted ? pb.keys : nullptr;
   if (ART_FAST_BVH && sc.bvh_levels > 0) {
     launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st);
@@ -2260,18 +2375,21 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (sorted) {
       hipLaunchKernelGGL(pair_hist_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.hist, pb.nblk,
                          pb.nbins);
-      size_t tb = pb.temp_bytes;
-      (void)hipcub::DeviceScan::ExclusiveSum(pb.temp, tb, pb.hist, pb.start, pb.nbins * pb.nblk, st);
-      hipLaunchKernelGGL(pair_scatter_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.start,
+      hipLaunchKernelGGL(pair_colscan_kernel, dim3((pb.nbins + 63) / 64), dim3(64), 0, st, pb.hist, pb.prefix, pb.tot, pb.nblk,
+                         pb.nbins);
+      hipLaunchKernelGGL(pair_scatter_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.prefix, pb.tot,
                          pb.order, pb.nblk, pb.nbins);
     }
     const uint32_t* order = sorted ? (const uint32_t*)pb.order : nullptr;
+    const bool use_desc = pb.desc && ART_VIS_CONE && vis_ranges(sc) > 1 && !(fp.vis_bvh && sc.bvh_levels > 0);
+    if (use_desc)
+      hipLaunchKernelGGL(vis_batch_kernel, dim3((nb_max + 3) / 4), dim3(256), 0, st, pb.vp, pair_count, nb_max, order, pb.desc);
     if (fp.vis_bvh && sc.bvh_levels > 0)  // ART_CTX_VIS_BVH (measured 1.7x slower than vis_kernel on config 2)
       hipLaunchKernelGGL(vis_bvh_kernel, dim3((unsigned)((nb_max + kVisBvhWaves - 1) / kVisBvhWaves)), dim3(64 * kVisBvhWaves),
                          (size_t)bvh_lds_nodes(sc) * sizeof(CullRec), st, sc, pb.vp, pair_count, nb_max, order, fp.exec);
     else
       hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
-                         fp.exec);
+                         use_desc ? (const BatchDesc*)pb.desc : nullptr, fp.exec);
     hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                        muffle_acc);
   }
