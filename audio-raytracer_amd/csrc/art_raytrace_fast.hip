@@ -1379,6 +1379,9 @@ __host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) { return 
 #ifndef ART_VIS_SORT
 #define ART_VIS_SORT 1  // visibility batches in (target, direction from the target) order (vis_sort_key)
 #endif
+#ifndef ART_VIS_ECHO_QUAD
+#define ART_VIS_ECHO_QUAD 1  // echo pairs by quad-per-segment BVH traversal (vis_echo_quad_kernel)
+#endif
 #ifndef ART_VIS_DESC
 #define ART_VIS_DESC 0  // 1: batch box + cone computed once per batch (vis_batch_kernel): config 2 -3 us in vis_kernel, +12 us kernel
 #endif
@@ -1467,15 +1470,23 @@ __global__ __launch_bounds__(256) void vis_batch_kernel(VisPairs vp, const uint3
 // already blocked (a stale read only costs work). Verdicts meet in VisPairs::flag through relaxed
 // device-scope atomicOr (no fences: an agent-scope release writes back the XCD's L2);
 // vis_finalize writes the outputs after the kernel boundary.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
-void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
-                const uint32_t* __restrict__ order, const BatchDesc* __restrict__ desc, unsigned long long* ex) {
+__device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
+                                               uint32_t nb_max, const uint32_t* order, const BatchDesc* desc,
+                                               unsigned long long* ex, uint32_t b_first, uint32_t blk) {
   const int lane = threadIdx.x & 63;
-  const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t r = item / nb_max, b = item - r * nb_max;
+  // items cover batches [b_first, nb_max) (b_first > 0: the echo batches run in vis_echo_quad_kernel)
+  const uint32_t nbv = nb_max - b_first;
+  const uint32_t item = blk * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t r = item / nbv, b = b_first + (item - r * nbv);
   const int nranges = vis_ranges(sc);
   uint32_t pi, n_in;
   if (r >= (uint32_t)nranges || !batch_pair(vp, count, order, b, lane, pi, n_in)) return;
+#ifdef ART_DIAG_VIS_ONLY_ECHO  // diagnostic builds only: time one region of the pairs
+  if (b * 64u >= vp.echo_cap) return;
+#endif
+#ifdef ART_DIAG_VIS_ONLY_MUFFLE
+  if (b * 64u < vp.echo_cap) return;
+#endif
   uint32_t* flag = vp.flag + pi;
   // pairs an earlier range already blocked are skipped (not loaded, and out of the wave's box)
 #if ART_VIS_PLAIN_FLAG
@@ -1631,6 +1642,115 @@ __global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc,
     exec_add(ex, kExecObb, wave_sum_u32(nt[2]));
     exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nt[3]));
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Echo visibility by quad-per-segment BVH traversal (ART_VIS_ECHO_QUAD). An echo batch is one
+// wave's rays of one fan traced back to the fan origin: 64 segments fanning over an eighth of the
+// sphere, whose box and cone admit ~10 % of the colliders, so the chunk sweep spends most of its
+// time there. Per segment the BVH visits only the nodes along it. 4 lanes per segment (lane q:
+// child q / leaf slot q; the quad agrees through ballots), first blocker ends the segment. Same
+// exactness argument as anyhit_bvh.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void vis_echo_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
+                                                   unsigned long long* ex, uint32_t blk, uint16_t* s_stk) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
+  const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64
+  const uint32_t p = blk * 64u + (uint32_t)slot;               // echo pair index
+  const uint32_t ne = ldc(count, 0);
+  if ((uint32_t)__builtin_amdgcn_readfirstlane(blk * 64u + w * 16u) >= ne) return;
+  const bool valid = p < ne;
+  Seg s;
+  float maxd = 0.0f;
+  int owner = kNoOwner;
+  s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
+  s.a2 = s.a4 = 0.0f;
+  if (valid) load_pair_seg(vp, p, s, maxd, owner);
+  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+  const bool force = !(isfinite(om) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
+                     (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
+  const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
+  uint16_t* my = s_stk + slot * kBvhStack;
+  unsigned nt0 = 0, nt1 = 0, nt2 = 0, nnode = 0;
+  bool blocked = false;
+  int g = valid ? 0 : -1, sp = 0;
+  while (__any(g >= 0)) {
+    while (g >= 0 && g < leaf0) {  // quad-uniform
+      const int c0 = 4 * g + 1;
+      if (qd == 0) ++nnode;
+      const CullRec r = sc.bvh[c0 + qd];
+      const float m = r.factor * (r.scale + om);
+      float tn, tf;
+      const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m,
+                                 r.hix + m, r.hiy + m, r.hiz + m, tn, tf);
+      const bool enter = r.lox <= r.hix && (force || (h && tn <= maxd));
+      const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
+      if (eb) {
+        const int first = __builtin_ctz(eb);
+        const uint32_t rest = eb & (eb - 1u);
+        if (enter && qd != first) my[sp + __popc(rest & ((1u << qd) - 1u))] = (uint16_t)(c0 + qd);
+        sp += __popc(rest);
+        g = c0 + first;
+      } else {
+        g = sp ? (int)my[sp - 1] : -1;
+        sp = sp ? sp - 1 : 0;
+      }
+    }
+    if (g >= leaf0) {
+      const float4* sl = sc.bvh_leaf + (size_t)(g - leaf0) * (4 * kBvhLeaf) + 4 * qd;
+      const float4 qa = sl[0], qb = sl[1];
+      const int cc = __float_as_int(qb.w);
+      bool blk = false;
+      if (cc >= 0) {
+        const int t = cc >> 28;
+        float d = 0.0f;
+        bool hh;
+        int tid;
+        if (t == 0) {
+          SphereRec rr;
+          rr.cx = qa.x; rr.cy = qa.y; rr.cz = qa.z; rr.r2 = qa.w;
+          hh = sphere_hit_dist(s, rr, d); tid = __float_as_int(qb.z); ++nt0;
+        } else if (t == 1) {
+          AabbRec rr;
+          rr.mnx = qa.x; rr.mny = qa.y; rr.mnz = qa.z; rr.mxx = qa.w; rr.mxy = qb.x; rr.mxz = qb.y;
+          hh = aabb_test<false>(s, rr, d); tid = __float_as_int(qb.z); ++nt1;
+        } else {
+          const float4 qc = sl[2], qe = sl[3];
+          ObbRec rr;
+          rr.cx = qa.x; rr.cy = qa.y; rr.cz = qa.z;
+          rr.qx = qa.w; rr.qy = qb.x; rr.qz = qb.y; rr.qw = qb.z;
+          rr.lmnx = qc.x; rr.lmny = qc.y; rr.lmnz = qc.z; rr.lmxx = qc.w; rr.lmxy = qe.x; rr.lmxz = qe.y;
+          hh = obb_test<false>(s, rr, stored_q(rr), d); tid = __float_as_int(qe.z); ++nt2;
+        }
+        blk = hh && d < maxd && tid != owner;  // :373-394
+      }
+      if ((uint32_t)(__ballot(blk) >> qshift) & 0xFu) {
+        blocked = true;
+        g = -1;
+      } else {
+        g = sp ? (int)my[sp - 1] : -1;
+        sp = sp ? sp - 1 : 0;
+      }
+    }
+  }
+  if (valid && blocked && qd == 0) vp.flag[p] = 1u;
+  if (ex) {
+    exec_add(ex, kExecSphere, wave_sum_u32(nt0));
+    exec_add(ex, kExecAabb, wave_sum_u32(nt1));
+    exec_add(ex, kExecObb, wave_sum_u32(nt2));
+    exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nnode));
+  }
+}
+
+// One launch for both visibility halves, so they overlap on the chip: blocks [0, n_echo) trace
+// the echo batches by quad BVH traversal (longer jobs first), the others run the sweep's items.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
+void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
+                const uint32_t* __restrict__ order, const BatchDesc* __restrict__ desc, unsigned long long* ex,
+                uint32_t n_echo) {
+  __shared__ uint16_t s_stk[64 * kBvhStack];
+  if (blockIdx.x < n_echo) vis_echo_quad_body(sc, vp, count, ex, blockIdx.x, s_stk);
+  else vis_sweep_body(sc, vp, count, nb_max, order, desc, ex, n_echo, blockIdx.x - n_echo);
 }
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
@@ -2387,9 +2507,15 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (fp.vis_bvh && sc.bvh_levels > 0)  // ART_CTX_VIS_BVH (measured 1.7x slower than vis_kernel on config 2)
       hipLaunchKernelGGL(vis_bvh_kernel, dim3((unsigned)((nb_max + kVisBvhWaves - 1) / kVisBvhWaves)), dim3(64 * kVisBvhWaves),
                          (size_t)bvh_lds_nodes(sc) * sizeof(CullRec), st, sc, pb.vp, pair_count, nb_max, order, fp.exec);
-    else
-      hipLaunchKernelGGL(vis_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
-                         use_desc ? (const BatchDesc*)pb.desc : nullptr, fp.exec);
+    else {
+      // echo batches by quad BVH traversal (when the scene has a BVH), the rest by the sweep
+      const uint32_t eb = (ART_VIS_ECHO_QUAD && sc.bvh_levels > 0) ? pb.vp.echo_cap / 64 : 0u;
+      const size_t vitems = (size_t)(nb_max - eb) * vis_ranges(sc);
+      const size_t blocks = eb + (vitems + 3) / 4;
+      if (blocks)
+        hipLaunchKernelGGL(vis_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
+                           use_desc ? (const BatchDesc*)pb.desc : nullptr, fp.exec, eb);
+    }
     hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                        muffle_acc);
   }
