@@ -515,6 +515,9 @@ __device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bo
 // Four times the waves of one-lane-per-ray traversal (latency hiding at config 2's 2048 groups),
 // and the inner-node / leaf steps are one test per lane instead of four.
 // ------------------------------------------------------------------------------------------
+#ifndef ART_QUAD_SPECULATIVE
+#define ART_QUAD_SPECULATIVE 1
+#endif
 #ifndef ART_QUAD_FULL_SORT
 #define ART_QUAD_FULL_SORT 2  // 0: nearest child first, the rest in index order; 1: full near-first
 #endif                        // order; 2: full order for scenes with OBBs (config 3 -1 %, config 2 +5 %)
@@ -548,112 +551,130 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
   uint16_t* my = stk + rr * kBvhStack;
   const bool full_sort = ART_QUAD_FULL_SORT == 1 || (ART_QUAD_FULL_SORT == 2 && sc.no > 0);
   int g = alive ? 0 : -1, sp = 0;
-  while (__any(g >= 0)) {
-    while (g >= 0 && g < leaf0) {  // quad-uniform: the 4 lanes of a ray stay together
+  auto pop = [&]() { g = sp ? (int)my[sp - 1] : -1; sp = sp ? sp - 1 : 0; };
+  auto inner_step = [&]() {
       const int c0 = 4 * g + 1;
-      if (qd == 0) ++nnode;
-      const CullRec r = sc.bvh[c0 + qd];
-      const float m = r.factor * (r.scale + om);
-      float tn, tf;
-      const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m,
-                                 r.hix + m, r.hiy + m, r.hiz + m, tn, tf);
-      const float en = fmaxf(tn, 0.0f);
-      const bool live = r.lox <= r.hix;
-      const float ek = (live && (force || (h && en <= best))) ? (force ? 0.0f : en) : INFINITY;
-      if (full_sort) {  // far-to-near pushes (sorting network); pays for OBB scenes' long leaf tests
-      const int eb = __float_as_int(ek);
-      float e[4] = {__int_as_float(quad_bcast<0>(eb)), __int_as_float(quad_bcast<1>(eb)),
-                    __int_as_float(quad_bcast<2>(eb)), __int_as_float(quad_bcast<3>(eb))};
-      int c[4] = {0, 1, 2, 3};
-      auto cswap = [&](int a, int b) {
-        if (e[b] < e[a]) { const float te = e[a]; e[a] = e[b]; e[b] = te; const int tc = c[a]; c[a] = c[b]; c[b] = tc; }
-      };
-      cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
-      if (e[0] < INFINITY) {
+    if (qd == 0) ++nnode;
+    const CullRec r = sc.bvh[c0 + qd];
+    const float m = r.factor * (r.scale + om);
+    float tn, tf;
+    const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m,
+                               r.hix + m, r.hiy + m, r.hiz + m, tn, tf);
+    const float en = fmaxf(tn, 0.0f);
+    const bool live = r.lox <= r.hix;
+    const float ek = (live && (force || (h && en <= best))) ? (force ? 0.0f : en) : INFINITY;
+    if (full_sort) {  // far-to-near pushes (sorting network); pays for OBB scenes' long leaf tests
+    const int eb = __float_as_int(ek);
+    float e[4] = {__int_as_float(quad_bcast<0>(eb)), __int_as_float(quad_bcast<1>(eb)),
+                  __int_as_float(quad_bcast<2>(eb)), __int_as_float(quad_bcast<3>(eb))};
+    int c[4] = {0, 1, 2, 3};
+    auto cswap = [&](int a, int b) {
+      if (e[b] < e[a]) { const float te = e[a]; e[a] = e[b]; e[b] = te; const int tc = c[a]; c[a] = c[b]; c[b] = tc; }
+    };
+    cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
+    if (e[0] < INFINITY) {
 #pragma unroll
-        for (int k = 3; k >= 1; --k)
-          if (e[k] < INFINITY) {
-            if (qd == 0) my[sp] = (uint16_t)(c0 + c[k]);
-            ++sp;
-          }
-        g = c0 + c[0];
-      } else {
-        g = sp ? (int)my[sp - 1] : -1;
-        sp = sp ? sp - 1 : 0;
-      }
-      } else {
-      // descend into the nearest child ((entry, index) minimum over the quad, two DPP steps); the
-      // other entered children go on the stack in index order, each lane writing its own
-      float mn = ek;
-      int mi = qd;
-      {
-        const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(mn)));
-        const int oi = quad_perm<kQuadXor1>(mi);
-        if (od < mn || (od == mn && oi < mi)) { mn = od; mi = oi; }
-      }
-      {
-        const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(mn)));
-        const int oi = quad_perm<kQuadXor2>(mi);
-        if (od < mn || (od == mn && oi < mi)) { mn = od; mi = oi; }
-      }
-      const int qshift = lane & ~3;
-      const bool push = ek < INFINITY && qd != mi;
-      const uint32_t pb = (uint32_t)(__ballot(push) >> qshift) & 0xFu;
-      if (mn < INFINITY) {
-        if (push) my[sp + __popc(pb & ((1u << qd) - 1u))] = (uint16_t)(c0 + qd);
-        sp += __popc(pb);
-        g = c0 + mi;
-      } else {
-        g = sp ? (int)my[sp - 1] : -1;
-        sp = sp ? sp - 1 : 0;
-      }
-      }
-    }
-    if (g >= leaf0) {
-      const float4* sl = sc.bvh_leaf + (size_t)(g - leaf0) * (4 * kBvhLeaf) + 4 * qd;
-      const float4 qa = sl[0], qb = sl[1];
-      const int cc = __float_as_int(qb.w);
-      float d = INFINITY;
-      int dc = kNoHit;
-      if (cc >= 0) {
-        const int t = cc >> 28;
-        float dd = 0.0f;
-        bool h;
-        if (t == 0) {
-          SphereRec r;
-          r.cx = qa.x; r.cy = qa.y; r.cz = qa.z; r.r2 = qa.w;
-          h = sphere_hit_dist(s, r, dd); ++nt0;
-        } else if (t == 1) {
-          AabbRec r;
-          r.mnx = qa.x; r.mny = qa.y; r.mnz = qa.z; r.mxx = qa.w; r.mxy = qb.x; r.mxz = qb.y;
-          h = aabb_test<false>(s, r, dd); ++nt1;
-        } else {
-          const float4 qc = sl[2], qe = sl[3];
-          ObbRec r;
-          r.cx = qa.x; r.cy = qa.y; r.cz = qa.z;
-          r.qx = qa.w; r.qy = qb.x; r.qz = qb.y; r.qw = qb.z;
-          r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qe.x; r.lmxz = qe.y;
-          h = obb_test<false>(s, r, stored_q(r), dd); ++nt2;
+      for (int k = 3; k >= 1; --k)
+        if (e[k] < INFINITY) {
+          if (qd == 0) my[sp] = (uint16_t)(c0 + c[k]);
+          ++sp;
         }
-        // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue)
-        if (h && dd < FLT_MAX) { d = dd; dc = cc; }
-      }
-      // (distance, order) minimum over the quad's four slots
-      {
-        const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(d)));
-        const int oc = quad_perm<kQuadXor1>(dc);
-        if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
-      }
-      {
-        const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(d)));
-        const int oc = quad_perm<kQuadXor2>(dc);
-        if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
-      }
-      if (d < best || (d == best && dc < code)) { best = d; code = dc; }
+      g = c0 + c[0];
+    } else {
       g = sp ? (int)my[sp - 1] : -1;
       sp = sp ? sp - 1 : 0;
     }
+    } else {
+    // descend into the nearest child ((entry, index) minimum over the quad, two DPP steps); the
+    // other entered children go on the stack in index order, each lane writing its own
+    float mn = ek;
+    int mi = qd;
+    {
+      const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(mn)));
+      const int oi = quad_perm<kQuadXor1>(mi);
+      if (od < mn || (od == mn && oi < mi)) { mn = od; mi = oi; }
+    }
+    {
+      const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(mn)));
+      const int oi = quad_perm<kQuadXor2>(mi);
+      if (od < mn || (od == mn && oi < mi)) { mn = od; mi = oi; }
+    }
+    const int qshift = lane & ~3;
+    const bool push = ek < INFINITY && qd != mi;
+    const uint32_t pb = (uint32_t)(__ballot(push) >> qshift) & 0xFu;
+    if (mn < INFINITY) {
+      if (push) my[sp + __popc(pb & ((1u << qd) - 1u))] = (uint16_t)(c0 + qd);
+      sp += __popc(pb);
+      g = c0 + mi;
+    } else {
+      g = sp ? (int)my[sp - 1] : -1;
+      sp = sp ? sp - 1 : 0;
+    }
+    }
+  };
+  auto leaf_step = [&](int leaf) {
+      const float4* sl = sc.bvh_leaf + (size_t)(leaf - leaf0) * (4 * kBvhLeaf) + 4 * qd;
+    const float4 qa = sl[0], qb = sl[1];
+    const int cc = __float_as_int(qb.w);
+    float d = INFINITY;
+    int dc = kNoHit;
+    if (cc >= 0) {
+      const int t = cc >> 28;
+      float dd = 0.0f;
+      bool h;
+      if (t == 0) {
+        SphereRec r;
+        r.cx = qa.x; r.cy = qa.y; r.cz = qa.z; r.r2 = qa.w;
+        h = sphere_hit_dist(s, r, dd); ++nt0;
+      } else if (t == 1) {
+        AabbRec r;
+        r.mnx = qa.x; r.mny = qa.y; r.mnz = qa.z; r.mxx = qa.w; r.mxy = qb.x; r.mxz = qb.y;
+        h = aabb_test<false>(s, r, dd); ++nt1;
+      } else {
+        const float4 qc = sl[2], qe = sl[3];
+        ObbRec r;
+        r.cx = qa.x; r.cy = qa.y; r.cz = qa.z;
+        r.qx = qa.w; r.qy = qb.x; r.qz = qb.y; r.qw = qb.z;
+        r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qe.x; r.lmxz = qe.y;
+        h = obb_test<false>(s, r, stored_q(r), dd); ++nt2;
+      }
+      // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue)
+      if (h && dd < FLT_MAX) { d = dd; dc = cc; }
+    }
+    // (distance, order) minimum over the quad's four slots
+    {
+      const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(d)));
+      const int oc = quad_perm<kQuadXor1>(dc);
+      if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
+    }
+    {
+      const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(d)));
+      const int oc = quad_perm<kQuadXor2>(dc);
+      if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
+    }
+    if (d < best || (d == best && dc < code)) { best = d; code = dc; }
+  };
+#if ART_QUAD_SPECULATIVE
+  // Speculative while-while (Aila & Laine): a quad that reaches a leaf parks it and keeps
+  // descending; the wave tests leaves once every quad with work holds one, so both kinds of
+  // step run with most quads busy. The order in which leaves are tested does not change the
+  // (distance, order) minimum.
+  int pend = -1;
+  while (__any(g >= 0 || pend >= 0)) {
+    for (;;) {
+      if (g >= leaf0 && pend < 0) { pend = g; pop(); }
+      const bool inner = g >= 0 && g < leaf0;
+      if (!__any(inner) || !__any(pend < 0 && g >= 0)) break;
+      if (inner) inner_step();
+    }
+    if (pend >= 0) { leaf_step(pend); pend = -1; }
   }
+#else
+  while (__any(g >= 0)) {
+    while (g >= 0 && g < leaf0) inner_step();  // quad-uniform: the 4 lanes of a ray stay together
+    if (g >= leaf0) { leaf_step(g); pop(); }
+  }
+#endif
   if (qd == 0) { s_best[rr] = best; s_code[rr] = code; }
   if (ex) {
     exec_add(ex, kExecSphere, wave_sum_u32(nt0));
@@ -1382,6 +1403,9 @@ __host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) { return 
 #ifndef ART_VIS_ECHO_QUAD
 #define ART_VIS_ECHO_QUAD 1  // echo pairs by quad-per-segment BVH traversal (vis_echo_quad_kernel)
 #endif
+#ifndef ART_VIS_ALL_QUAD
+#define ART_VIS_ALL_QUAD 0  // 1: the muffle batches by quad traversal too
+#endif
 #ifndef ART_VIS_DESC
 #define ART_VIS_DESC 0  // 1: batch box + cone computed once per batch (vis_batch_kernel): config 2 -3 us in vis_kernel, +12 us kernel
 #endif
@@ -1652,14 +1676,14 @@ __global__ __launch_bounds__(64 * kVisBvhWaves) void vis_bvh_kernel(DevScene sc,
 // child q / leaf slot q; the quad agrees through ballots), first blocker ends the segment. Same
 // exactness argument as anyhit_bvh.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void vis_echo_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                                   unsigned long long* ex, uint32_t blk, uint16_t* s_stk) {
+__device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
+                                              const uint32_t* order, unsigned long long* ex, uint32_t blk, uint16_t* s_stk) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
-  const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64
-  const uint32_t p = blk * 64u + (uint32_t)slot;               // echo pair index
-  const uint32_t ne = ldc(count, 0);
-  if ((uint32_t)__builtin_amdgcn_readfirstlane(blk * 64u + w * 16u) >= ne) return;
-  const bool valid = p < ne;
+  const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64-pair batch
+  uint32_t p, n_in;
+  if (!batch_pair(vp, count, order, blk, slot, p, n_in)) return;
+  if ((uint32_t)(w * 16) >= n_in) return;                      // this wave's 16 segments are past the batch's end
+  const bool valid = (uint32_t)slot < n_in;
   Seg s;
   float maxd = 0.0f;
   int owner = kNoOwner;
@@ -1749,7 +1773,7 @@ void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, ui
                 const uint32_t* __restrict__ order, const BatchDesc* __restrict__ desc, unsigned long long* ex,
                 uint32_t n_echo) {
   __shared__ uint16_t s_stk[64 * kBvhStack];
-  if (blockIdx.x < n_echo) vis_echo_quad_body(sc, vp, count, ex, blockIdx.x, s_stk);
+  if (blockIdx.x < n_echo) vis_quad_body(sc, vp, count, order, ex, blockIdx.x, s_stk);
   else vis_sweep_body(sc, vp, count, nb_max, order, desc, ex, n_echo, blockIdx.x - n_echo);
 }
 
@@ -2027,10 +2051,14 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
         // echo pairs to the echo region, muffle pairs to the muffle region (one reservation each)
         const uint32_t ne = (uint32_t)__popcll(mq[0]), nm = np - ne;
         uint32_t eb = 0, mb = 0;
+#ifdef ART_DIAG_NO_PAIR_ATOMICS  // diagnostic build only (H = 1 timing): fixed per-group positions
+        eb = (uint32_t)g * 64u; mb = (uint32_t)g * 64u * (uint32_t)T;
+#else
         if (lane == 0) {
           if (ne) eb = atomicAdd(&pair_count[0], ne);
           if (nm) mb = atomicAdd(&pair_count[1], nm);
         }
+#endif
         eb = __builtin_amdgcn_readfirstlane(__shfl(eb, 0, 64));
         mb = __builtin_amdgcn_readfirstlane(__shfl(mb, 0, 64));
         uint32_t pos = mb;  // muffle position (region-relative)
@@ -2509,7 +2537,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                          (size_t)bvh_lds_nodes(sc) * sizeof(CullRec), st, sc, pb.vp, pair_count, nb_max, order, fp.exec);
     else {
       // echo batches by quad BVH traversal (when the scene has a BVH), the rest by the sweep
-      const uint32_t eb = (ART_VIS_ECHO_QUAD && sc.bvh_levels > 0) ? pb.vp.echo_cap / 64 : 0u;
+      const uint32_t eb = (ART_VIS_ECHO_QUAD && sc.bvh_levels > 0) ? (ART_VIS_ALL_QUAD ? nb_max : pb.vp.echo_cap / 64) : 0u;
       const size_t vitems = (size_t)(nb_max - eb) * vis_ranges(sc);
       const size_t blocks = eb + (vitems + 3) / 4;
       if (blocks)
