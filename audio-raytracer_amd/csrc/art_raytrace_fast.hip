@@ -1387,16 +1387,23 @@ __device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Se
 #ifndef ART_VIS_PLAIN_FLAG
 #define ART_VIS_PLAIN_FLAG 0
 #endif
-// Chunk ranges per 64-pair batch (work items of vis_kernel), by scene kind: OBB tests are long,
-// so OBB scenes balance better over 8 ranges (config 3: 1.46 vs 1.54 ms at 4); otherwise each
-// range repeats the batch's setup, and 4 measured best (config 2 vis_kernel 296 vs 315 us).
+// Chunk ranges per 64-pair batch (work items of the muffle sweep), by scene kind: each range
+// repeats the batch's setup, while OBB tests are long and balance better over more items.
+// Measured (raytrace stage): no OBBs 2 ranges (config 2: 218 vs 231 us at 4, 274 at 1); OBB
+// majority 8 (config 3: 0.98 vs 1.01 ms at 4); some OBBs 4 (config 4: 5.73 vs 5.84 ms at 8,
+// config 5: 2.69 vs 2.81).
 #ifndef ART_VIS_RANGES_OBB
 #define ART_VIS_RANGES_OBB 8
 #endif
-#ifndef ART_VIS_RANGES
-#define ART_VIS_RANGES 4
+#ifndef ART_VIS_RANGES_MIXED
+#define ART_VIS_RANGES_MIXED 4
 #endif
-__host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) { return sc.no > 0 ? ART_VIS_RANGES_OBB : ART_VIS_RANGES; }
+#ifndef ART_VIS_RANGES
+#define ART_VIS_RANGES 2
+#endif
+__host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) {
+  return 2 * sc.no > sc.ns + sc.na + sc.no ? ART_VIS_RANGES_OBB : (sc.no > 0 ? ART_VIS_RANGES_MIXED : ART_VIS_RANGES);
+}
 #ifndef ART_VIS_SORT
 #define ART_VIS_SORT 1  // visibility batches in (target, direction from the target) order (vis_sort_key)
 #endif
