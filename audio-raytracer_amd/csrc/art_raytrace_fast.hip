@@ -529,26 +529,18 @@ template <int CTRL>
 __device__ __forceinline__ int quad_perm(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false); }
 constexpr int kQuadXor1 = 1 | (0 << 2) | (3 << 4) | (2 << 6), kQuadXor2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);
 
-// Ray r of the group (this wave's lanes 4 (r - 16 w) .. + 3) from lane r's state; writes
-// s_best[r] / s_code[r] (the q = 0 lane). stk = [64 rays][kBvhStack] u16.
-__device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& own, bool own_alive, int w, int lane,
-                                                 uint16_t* stk, float* s_best, int* s_code, unsigned long long* ex) {
-  const int qd = lane & 3, rr = 16 * w + (lane >> 2);
-  Seg s;
-  s.o = mk3(__shfl(own.o.x, rr, 64), __shfl(own.o.y, rr, 64), __shfl(own.o.z, rr, 64));
-  s.d = mk3(__shfl(own.d.x, rr, 64), __shfl(own.d.y, rr, 64), __shfl(own.d.z, rr, 64));
-  s.inv = mk3(__shfl(own.inv.x, rr, 64), __shfl(own.inv.y, rr, 64), __shfl(own.inv.z, rr, 64));
-  s.a2 = __shfl(own.a2, rr, 64);
-  s.a4 = __shfl(own.a4, rr, 64);
-  const bool alive = __shfl((int)own_alive, rr, 64) != 0;
-  float best = FLT_MAX;
-  int code = kNoHit;
+// Nearest hit of the quad's ray s (identical in the 4 lanes; `my` = the ray's kBvhStack u16
+// stack): (distance, order) minimum in best / code of every lane of the quad.
+__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg& s, bool alive, int lane, uint16_t* my,
+                                                  float& best, int& code, unsigned long long* ex) {
+  const int qd = lane & 3;
+  best = FLT_MAX;
+  code = kNoHit;
   unsigned nt0 = 0, nt1 = 0, nt2 = 0, nnode = 0;
   const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
   const bool force = !(isfinite(om) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
                      (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
   const int leaf0 = sc.bvh_leaf0;
-  uint16_t* my = stk + rr * kBvhStack;
   const bool full_sort = ART_QUAD_FULL_SORT == 1 || (ART_QUAD_FULL_SORT == 2 && sc.no > 0);
   int g = alive ? 0 : -1, sp = 0;
   auto pop = [&]() { g = sp ? (int)my[sp - 1] : -1; sp = sp ? sp - 1 : 0; };
@@ -675,13 +667,56 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
     if (g >= leaf0) { leaf_step(g); pop(); }
   }
 #endif
-  if (qd == 0) { s_best[rr] = best; s_code[rr] = code; }
   if (ex) {
     exec_add(ex, kExecSphere, wave_sum_u32(nt0));
     exec_add(ex, kExecAabb, wave_sum_u32(nt1));
     exec_add(ex, kExecObb, wave_sum_u32(nt2));
     exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nnode));
   }
+}
+
+// Ray r of the group (this wave's lanes 4 (r - 16 w) .. + 3) from lane r's state; writes
+// s_best[r] / s_code[r] (the q = 0 lane). stk = [64 rays][kBvhStack] u16.
+__device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& own, bool own_alive, int w, int lane,
+                                                 uint16_t* stk, float* s_best, int* s_code, unsigned long long* ex) {
+  const int rr = 16 * w + (lane >> 2);
+  Seg s;
+  s.o = mk3(__shfl(own.o.x, rr, 64), __shfl(own.o.y, rr, 64), __shfl(own.o.z, rr, 64));
+  s.d = mk3(__shfl(own.d.x, rr, 64), __shfl(own.d.y, rr, 64), __shfl(own.d.z, rr, 64));
+  s.inv = mk3(__shfl(own.inv.x, rr, 64), __shfl(own.inv.y, rr, 64), __shfl(own.inv.z, rr, 64));
+  s.a2 = __shfl(own.a2, rr, 64);
+  s.a4 = __shfl(own.a4, rr, 64);
+  const bool alive = __shfl((int)own_alive, rr, 64) != 0;
+  float best;
+  int code;
+  quad_nearest_core(sc, s, alive, lane, stk + rr * kBvhStack, best, code, ex);
+  if ((lane & 3) == 0) { s_best[rr] = best; s_code[rr] = code; }
+}
+
+// First-segment nearest hits in a launch of their own (ART_FAST_PRE_NEAREST): one 64-ray group per
+// workgroup, wave w traverses rays 16w .. 16w + 15 with 4 lanes each (quad_nearest_core). Without
+// the path kernel's emission state live across the traversal, the registers allow more waves per
+// SIMD. hits[g * 64 + r] = (distance bits, code) of the group's ray slot r.
+#ifndef ART_FAST_WPE_PRE
+#define ART_FAST_WPE_PRE 8
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WPE_PRE))) void nearest_first_kernel(
+    DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
+    int2* __restrict__ hits) {
+  __shared__ uint16_t s_stk[kBvhStack * 64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nrb = (fp.R + 63) >> 6;
+  const int g = blockIdx.x;
+  const int fan = g / nrb;
+  const int rr = 16 * w + (lane >> 2);
+  const int slot = (g - fan * nrb) * 64 + rr;
+  const bool valid = slot < fp.R;
+  const int ray = valid ? ray_order[slot] : 0;
+  const Seg s = make_seg(load3(origins, fan), load_dir(sc.dirs, ray));
+  float best;
+  int code;
+  quad_nearest_core(sc, s, valid, lane, s_stk + rr * kBvhStack, best, code, fp.exec);
+  if ((lane & 3) == 0) hits[(size_t)g * 64 + rr] = make_int2(__float_as_int(best), code);
 }
 
 // brute-force nearest sweep of this wave's ranges (nearest_chunk): every collider of the range
@@ -1838,7 +1873,10 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 
 // MULTI = false: frames with one hit per ray (H == 1, configs 2-4) compile without the later-bounce
 // nearest sweep and the reflection, which removes their registers from the kernel.
-template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD>
+#ifndef ART_FAST_AGG_RESERVE
+#define ART_FAST_AGG_RESERVE 1
+#endif
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD, bool PRE>
 __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
@@ -1847,12 +1885,22 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                uint32_t* __restrict__ work,
                                                                VisPairs vp,
                                                                uint32_t* __restrict__ pair_count,
-                                                               uint16_t* __restrict__ pkeys) {
+                                                               uint16_t* __restrict__ pkeys,
+                                                               const int2* __restrict__ pre_hits) {
+  // PRE (independent waves): the first segment's nearest hits come from nearest_first_kernel.
   // BVH: the K waves of a workgroup are independent (each pulls its own 64-ray groups and owns
   // their writes); they share the workgroup's LDS copy of the top BVH nodes.
   // QUAD: the K = 4 waves hold the same 64 rays and split the nearest-hit traversal 16 rays each
   // (nearest_bvh_quad); results meet in LDS as the K-way split's partials do.
   constexpr bool IND = BVH && !QUAD;
+  // AGG: the K waves of a workgroup reserve their pair positions with one atomic per counter for
+  // the whole workgroup (one wave per group: 4096 same-line atomics serialize to ~46 us at config
+  // 2); the waves step through their groups together (block-uniform loop and bounce count).
+  constexpr bool AGG = PRE && !MULTI && ART_FAST_AGG_RESERVE;
+  __shared__ uint32_t s_agg[AGG ? 2 : 1][AGG ? K : 1][2];
+  __shared__ uint32_t s_aggb[2][2];
+  (void)s_agg; (void)s_aggb;
+  int it = 0;  // block-uniform group iteration (AGG buffers alternate by its parity)
   __shared__ float s_dist[K][64];
   __shared__ float s_best[K][64];  // running per-lane best of each wave (front-to-back pruning)
   (void)s_best;
@@ -1880,9 +1928,10 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   const int ngroups = fp.S * nrb;
   // BVH: the top bvh_lds_nodes(...) nodes in LDS (dynamic shared memory, BVH mode only)
   const CullRec* s_nodes = reinterpret_cast<const CullRec*>(s_seg);
-  const int nl = IND ? bvh_lds_nodes(sc) : 0;
-  (void)s_nodes; (void)nl;
-  if (IND) {
+  constexpr bool NODES = IND && (!PRE || MULTI);  // later bounces traverse per lane
+  const int nl = NODES ? bvh_lds_nodes(sc) : 0;
+  (void)s_nodes; (void)nl; (void)pre_hits;
+  if (NODES) {
     CullRec* dst = reinterpret_cast<CullRec*>(s_seg);
     for (int i = threadIdx.x; i < nl; i += blockDim.x) dst[i] = sc.bvh[i];
     __syncthreads();
@@ -1898,6 +1947,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   if (IND) {
     g = gnext;
     gnext += (int)gridDim.x * K;
+    ++it;
   } else if (QUAD) {  // static assignment, one group per workgroup
     __syncthreads();  // the previous group's LDS reads are done
     g = gnext;
@@ -1908,9 +1958,10 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     __syncthreads();
     g = __builtin_amdgcn_readfirstlane(s_ticket[0]);
   }
-  if (g >= ngroups) break;
-  const int fan = g / nrb;
-  const int slot = (g - fan * nrb) * 64 + lane;
+  if (AGG ? g - w >= ngroups : g >= ngroups) break;
+  const bool gvalid = !AGG || g < ngroups;  // AGG: a wave past the end takes part with no rays
+  const int fan = gvalid ? g / nrb : 0;
+  const int slot = gvalid ? (g - fan * nrb) * 64 + lane : fp.R;
   const bool valid = slot < fp.R;
   const int ray = valid ? ray_order[slot] : 0;
   const int T = fp.T, H = MULTI ? fp.H : 1;
@@ -1952,7 +2003,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   bool alive = valid;
 
   int bounce = 0;  // wave-uniform (lanes that stopped keep their own `hits`)
-  while (__any(alive)) {  // identical in every wave of the block -> uniform barriers
+  while (AGG ? bounce == 0 : __any(alive)) {  // identical in every wave of the block -> uniform barriers
     const Seg s = make_seg(o, d);
     float best;
     int code;
@@ -1969,7 +2020,16 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #ifdef ART_DIAG_NO_NEAREST  // diagnostic build only: every live ray hits sphere 0 at distance 1
       best = alive ? 1.0f : FLT_MAX; code = alive ? 0 : kNoHit;
 #else
-      nearest_bvh(sc, s, alive, s_nodes, nl, s_stk + w * (kBvhStack * 64), lane, best, code, fp.exec);
+      if (PRE && bounce == 0) {
+        const int2 h = gvalid ? pre_hits[(size_t)g * 64 + lane] : make_int2(__float_as_int(FLT_MAX), kNoHit);
+        best = __int_as_float(h.x);
+        code = h.y;
+      } else if (!PRE || MULTI) {
+        nearest_bvh(sc, s, alive, s_nodes, nl, s_stk + w * (kBvhStack * 64), lane, best, code, fp.exec);
+      } else {  // not reached: PRE one-hit frames have one segment
+        best = FLT_MAX;
+        code = kNoHit;
+      }
 #endif
     } else if (!MULTI || bounce == 0) {  // first segment: every ray of the fan starts at O
       const WaveCone wc = make_cone(O, d, alive);
@@ -2054,14 +2114,29 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #ifdef ART_DIAG_NO_EMIT  // diagnostic build only: time the path without the pair emission
       np = 0;
 #endif
+      // echo pairs to the echo region, muffle pairs to the muffle region (one reservation each)
+      const uint32_t ne = (uint32_t)__popcll(mq[0]), nm = np - ne;
+      uint32_t eb = 0, mb = 0;
+      if (AGG) {  // every wave of the workgroup is here (block-uniform loop, one bounce)
+        const int par = it & 1;
+        if (lane == 0) { s_agg[par][w][0] = ne; s_agg[par][w][1] = nm; }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+          uint32_t t = 0;
+#pragma unroll
+          for (int k = 0; k < K; ++k) t += s_agg[par][k][threadIdx.x];
+          s_aggb[par][threadIdx.x] = t ? atomicAdd(&pair_count[threadIdx.x], t) : 0u;
+        }
+        __syncthreads();
+        eb = s_aggb[par][0];
+        mb = s_aggb[par][1];
+        for (int k = 0; k < w; ++k) { eb += s_agg[par][k][0]; mb += s_agg[par][k][1]; }
+      }
       if (np) {
-        // echo pairs to the echo region, muffle pairs to the muffle region (one reservation each)
-        const uint32_t ne = (uint32_t)__popcll(mq[0]), nm = np - ne;
-        uint32_t eb = 0, mb = 0;
 #ifdef ART_DIAG_NO_PAIR_ATOMICS  // diagnostic build only (H = 1 timing): fixed per-group positions
         eb = (uint32_t)g * 64u; mb = (uint32_t)g * 64u * (uint32_t)T;
 #else
-        if (lane == 0) {
+        if (!AGG && lane == 0) {
           if (ne) eb = atomicAdd(&pair_count[0], ne);
           if (nm) mb = atomicAdd(&pair_count[1], nm);
         }
@@ -2273,21 +2348,22 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
   return blocks;
 }
 
-template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD = false>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD = false, bool PRE = false>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
-                           uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
-  const size_t lds = QUAD ? 0 : (BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T));
+                           uint32_t* pair_count, uint16_t* pkeys, hipStream_t st, const int2* pre = nullptr) {
+  const size_t lds = QUAD || (PRE && !MULTI) ? 0
+                     : (BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T));
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   // BVH: K independent waves per workgroup, one group each (grid-stride past 2^31 / K groups);
   // quad BVH: one group per workgroup; otherwise a persistent grid of co-resident workgroups
   // pulling groups from a ticket counter
   const int nblk = QUAD ? (int)std::min<long long>(groups, 1ll << 30)
                  : BVH  ? (int)std::min<long long>((groups + K - 1) / K, 1ll << 30)
-                        : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD>,
+                        : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD, PRE>,
                                                                             64 * K, lds));
-  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L, origins,
-                     block, muffle_acc, ray_order, work, pairs, pair_count, pkeys);
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD, PRE>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L,
+                     origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, pre);
 }
 
 template <int K>
@@ -2324,12 +2400,29 @@ static_assert(!ART_FAST_BVH || ART_FAST_SPLIT, "the BVH path kernel emits visibi
 static bool bvh_quad(const FrameParams& fp) {
   return (long long)fp.S * ((fp.R + 63) / 64) <= (long long)ART_FAST_QUAD_GROUPS;
 }
+#ifndef ART_FAST_PRE_NEAREST
+#define ART_FAST_PRE_NEAREST 1  // 1: one-hit frames take the first segment from nearest_first_kernel;
+#endif                          // 2: multi-hit frames too (later bounces per lane)
 
 // BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal; or (quad)
-// 4 waves per group, 4 lanes per ray.
+// 4 waves per group, 4 lanes per ray; or (pre) the quad first-segment launch, then the path
+// kernel's independent waves from its hits.
 static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                             uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
-                            uint32_t* pair_count, uint16_t* pkeys, hipStream_t st) {
+                            uint32_t* pair_count, uint16_t* pkeys, int2* pre, hipStream_t st) {
+#define ART_LAUNCH_P(H_, M_) \
+  launch_fast_kh<ART_FAST_BVH_WAVES, H_, 1, ART_FAST_WPE_BVH, M_, true, false, true>(sc, fp, L, origins, block, muffle_acc, \
+                                                                                     ray_order, work, pairs, pair_count, pkeys, \
+                                                                                     st, pre)
+  const bool multi_ = fp.H > 1;
+  if (pre && bvh_quad(fp) && (!multi_ || ART_FAST_PRE_NEAREST > 1)) {
+    const long long groups = (long long)fp.S * ((fp.R + 63) / 64);  // <= ART_FAST_QUAD_GROUPS
+    hipLaunchKernelGGL(nearest_first_kernel, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
+    if (L.has_hits) { if (multi_) ART_LAUNCH_P(true, true); else ART_LAUNCH_P(true, false); }
+    else { if (multi_) ART_LAUNCH_P(false, true); else ART_LAUNCH_P(false, false); }
+    return;
+  }
+#undef ART_LAUNCH_P
 #define ART_LAUNCH(H_, M_) \
   launch_fast_kh<ART_FAST_BVH_WAVES, H_, 1, ART_FAST_WPE_BVH, M_, true>(sc, fp, L, origins, block, muffle_acc, ray_order, \
                                                                         work, pairs, pair_count, pkeys, st)
@@ -2473,6 +2566,7 @@ struct PairBufs {
   uint16_t* keys;
   uint32_t *order, *hist, *prefix, *tot;
   BatchDesc* desc;  // [batches], when the batch descriptors are precomputed
+  int2* pre;        // [groups * 64] first-segment nearest hits (ART_FAST_PRE_NEAREST)
   size_t total;
   int nblk, nbins;
 };
@@ -2493,6 +2587,8 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   b.vp.flag = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
   b.vp.echo_cap = (uint32_t)ecap;
   b.desc = ART_VIS_DESC ? reinterpret_cast<BatchDesc*>(take((ecap / 64 + (mcap + 63) / 64) * sizeof(BatchDesc))) : nullptr;
+  if (ART_FAST_PRE_NEAREST && bvh_quad(fp))
+    b.pre = reinterpret_cast<int2*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * sizeof(int2)));
   if (ART_VIS_SORT && mcap) {
     b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
     b.nbins = fp.T << kSortDirBits;  // keys (target << kSortDirBits | cell) < T << kSortDirBits
@@ -2518,7 +2614,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && mcap && pb.nbins <= kSortBins && max_pairs < (1u << 31);
   uint16_t* pkeys = sorted ? pb.keys : nullptr;
   if (ART_FAST_BVH && sc.bvh_levels > 0) {
-    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st);
+    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, pb.pre, st);
   } else switch (fast_split(fp.S, fp.R)) {
     case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st); break;
     default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st); break;
