@@ -1896,7 +1896,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   // AGG: the K waves of a workgroup reserve their pair positions with one atomic per counter for
   // the whole workgroup (one wave per group: 4096 same-line atomics serialize to ~46 us at config
   // 2); the waves step through their groups together (block-uniform loop and bounce count).
-  constexpr bool AGG = PRE && !MULTI && ART_FAST_AGG_RESERVE;
+  constexpr bool AGG = IND && !MULTI && ART_FAST_AGG_RESERVE;
   __shared__ uint32_t s_agg[AGG ? 2 : 1][AGG ? K : 1][2];
   __shared__ uint32_t s_aggb[2][2];
   (void)s_agg; (void)s_aggb;
@@ -2401,8 +2401,12 @@ static bool bvh_quad(const FrameParams& fp) {
   return (long long)fp.S * ((fp.R + 63) / 64) <= (long long)ART_FAST_QUAD_GROUPS;
 }
 #ifndef ART_FAST_PRE_NEAREST
-#define ART_FAST_PRE_NEAREST 1  // 1: one-hit frames take the first segment from nearest_first_kernel;
-#endif                          // 2: multi-hit frames too (later bounces per lane)
+#define ART_FAST_PRE_NEAREST 1  // 1: one-hit frames take the first segment from nearest_first_kernel
+#endif                          // (any size: config 4 5.58 -> 4.74 ms); 2: multi-hit quad frames too
+static bool bvh_pre(const FrameParams& fp) {
+  const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
+  return ART_FAST_PRE_NEAREST && groups < (1ll << 30) && (fp.H == 1 || (ART_FAST_PRE_NEAREST > 1 && bvh_quad(fp)));
+}
 
 // BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal; or (quad)
 // 4 waves per group, 4 lanes per ray; or (pre) the quad first-segment launch, then the path
@@ -2415,8 +2419,8 @@ static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const Fan
                                                                                      ray_order, work, pairs, pair_count, pkeys, \
                                                                                      st, pre)
   const bool multi_ = fp.H > 1;
-  if (pre && bvh_quad(fp) && (!multi_ || ART_FAST_PRE_NEAREST > 1)) {
-    const long long groups = (long long)fp.S * ((fp.R + 63) / 64);  // <= ART_FAST_QUAD_GROUPS
+  if (pre && bvh_pre(fp)) {
+    const long long groups = (long long)fp.S * ((fp.R + 63) / 64);  // < 2^30
     hipLaunchKernelGGL(nearest_first_kernel, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
     if (L.has_hits) { if (multi_) ART_LAUNCH_P(true, true); else ART_LAUNCH_P(true, false); }
     else { if (multi_) ART_LAUNCH_P(false, true); else ART_LAUNCH_P(false, false); }
@@ -2587,7 +2591,7 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   b.vp.flag = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
   b.vp.echo_cap = (uint32_t)ecap;
   b.desc = ART_VIS_DESC ? reinterpret_cast<BatchDesc*>(take((ecap / 64 + (mcap + 63) / 64) * sizeof(BatchDesc))) : nullptr;
-  if (ART_FAST_PRE_NEAREST && bvh_quad(fp))
+  if (bvh_pre(fp))
     b.pre = reinterpret_cast<int2*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * sizeof(int2)));
   if (ART_VIS_SORT && mcap) {
     b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);

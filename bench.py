@@ -479,7 +479,7 @@ def main():
                    "parallelism": f"fan-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
         "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "raytrace stage: raytrace_fast_kernel + vis_kernel + vis_finalize", "kernel_ms": rt_ms,
+                     "kernel": "raytrace stage: nearest_first_kernel + raytrace_fast_kernel + pair sort + vis_kernel + vis_finalize", "kernel_ms": rt_ms,
                      "note": "FP32 VALU roof (no MFMA-shaped work). achieved = the reference algorithm's tests x ops per "
                              "test (SURVEY.md 8(d)) per launch / kernel time: brute-force-equivalent, since the kernel's "
                              "exact broad phase skips tests that cannot hit. 'executed' is the work the kernel did.",
