@@ -531,6 +531,7 @@ constexpr int kQuadXor1 = 1 | (0 << 2) | (3 << 4) | (2 << 6), kQuadXor2 = 2 | (3
 
 // Nearest hit of the quad's ray s (identical in the 4 lanes; `my` = the ray's kBvhStack u16
 // stack): (distance, order) minimum in best / code of every lane of the quad.
+template <bool EX>
 __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg& s, bool alive, int lane, uint16_t* my,
                                                   float& best, int& code, unsigned long long* ex) {
   const int qd = lane & 3;
@@ -546,7 +547,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
   auto pop = [&]() { g = sp ? (int)my[sp - 1] : -1; sp = sp ? sp - 1 : 0; };
   auto inner_step = [&]() {
       const int c0 = 4 * g + 1;
-    if (qd == 0) ++nnode;
+    if (EX && qd == 0) ++nnode;
     const CullRec r = sc.bvh[c0 + qd];
     const float m = r.factor * (r.scale + om);
     float tn, tf;
@@ -617,18 +618,18 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
       if (t == 0) {
         SphereRec r;
         r.cx = qa.x; r.cy = qa.y; r.cz = qa.z; r.r2 = qa.w;
-        h = sphere_hit_dist(s, r, dd); ++nt0;
+        h = sphere_hit_dist(s, r, dd); if (EX) ++nt0;
       } else if (t == 1) {
         AabbRec r;
         r.mnx = qa.x; r.mny = qa.y; r.mnz = qa.z; r.mxx = qa.w; r.mxy = qb.x; r.mxz = qb.y;
-        h = aabb_test<false>(s, r, dd); ++nt1;
+        h = aabb_test<false>(s, r, dd); if (EX) ++nt1;
       } else {
         const float4 qc = sl[2], qe = sl[3];
         ObbRec r;
         r.cx = qa.x; r.cy = qa.y; r.cz = qa.z;
         r.qx = qa.w; r.qy = qb.x; r.qz = qb.y; r.qw = qb.z;
         r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qe.x; r.lmxz = qe.y;
-        h = obb_test<false>(s, r, stored_q(r), dd); ++nt2;
+        h = obb_test<false>(s, r, stored_q(r), dd); if (EX) ++nt2;
       }
       // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue)
       if (h && dd < FLT_MAX) { d = dd; dc = cc; }
@@ -689,7 +690,7 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
   const bool alive = __shfl((int)own_alive, rr, 64) != 0;
   float best;
   int code;
-  quad_nearest_core(sc, s, alive, lane, stk + rr * kBvhStack, best, code, ex);
+  quad_nearest_core<true>(sc, s, alive, lane, stk + rr * kBvhStack, best, code, ex);
   if ((lane & 3) == 0) { s_best[rr] = best; s_code[rr] = code; }
 }
 
@@ -700,6 +701,7 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
 #ifndef ART_FAST_WPE_PRE
 #define ART_FAST_WPE_PRE 8
 #endif
+template <bool EX>  // EX: count the executed tests (fp.exec)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WPE_PRE))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits) {
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WP
   const Seg s = make_seg(load3(origins, fan), load_dir(sc.dirs, ray));
   float best;
   int code;
-  quad_nearest_core(sc, s, valid, lane, s_stk + rr * kBvhStack, best, code, fp.exec);
+  quad_nearest_core<EX>(sc, s, valid, lane, s_stk + rr * kBvhStack, best, code, EX ? fp.exec : nullptr);
   if ((lane & 3) == 0) hits[(size_t)g * 64 + rr] = make_int2(__float_as_int(best), code);
 }
 
@@ -2421,7 +2423,10 @@ static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const Fan
   const bool multi_ = fp.H > 1;
   if (pre && bvh_pre(fp)) {
     const long long groups = (long long)fp.S * ((fp.R + 63) / 64);  // < 2^30
-    hipLaunchKernelGGL(nearest_first_kernel, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
+    if (fp.exec)
+      hipLaunchKernelGGL(nearest_first_kernel<true>, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
+    else
+      hipLaunchKernelGGL(nearest_first_kernel<false>, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
     if (L.has_hits) { if (multi_) ART_LAUNCH_P(true, true); else ART_LAUNCH_P(true, false); }
     else { if (multi_) ART_LAUNCH_P(false, true); else ART_LAUNCH_P(false, false); }
     return;
