@@ -704,7 +704,7 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
 template <bool EX>  // EX: count the executed tests (fp.exec)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WPE_PRE))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
-    int2* __restrict__ hits) {
+    int2* __restrict__ hits, const float4* __restrict__ state, int step) {
   __shared__ uint16_t s_stk[kBvhStack * 64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
@@ -714,10 +714,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WP
   const int slot = (g - fan * nrb) * 64 + rr;
   const bool valid = slot < fp.R;
   const int ray = valid ? ray_order[slot] : 0;
-  const Seg s = make_seg(load3(origins, fan), load_dir(sc.dirs, ray));
+  Seg s;
+  bool alive = valid;
+  if (step == 0) {
+    s = make_seg(load3(origins, fan), load_dir(sc.dirs, ray));
+  } else {  // later bounce of a multi-hit frame: the path kernel's ray state
+    const size_t i = (size_t)g * 64 + rr;
+    const float4 a = state[2 * i], b = state[2 * i + 1];
+    s = make_seg(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
+    alive = valid && ((__float_as_int(b.w) >> 8) & 1) != 0;
+  }
   float best;
   int code;
-  quad_nearest_core<EX>(sc, s, valid, lane, s_stk + rr * kBvhStack, best, code, EX ? fp.exec : nullptr);
+  quad_nearest_core<EX>(sc, s, alive, lane, s_stk + rr * kBvhStack, best, code, EX ? fp.exec : nullptr);
   if ((lane & 3) == 0) hits[(size_t)g * 64 + rr] = make_int2(__float_as_int(best), code);
 }
 
@@ -1878,7 +1887,7 @@ __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) 
 #ifndef ART_FAST_AGG_RESERVE
 #define ART_FAST_AGG_RESERVE 1
 #endif
-template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD, bool PRE>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD, bool PRE, bool STEP>
 __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) void raytrace_fast_kernel(DevScene sc, FrameParams fp, FanLayout L,
                                                                const float* __restrict__ origins,
                                                                uint8_t* __restrict__ block,
@@ -1888,7 +1897,10 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
                                                                VisPairs vp,
                                                                uint32_t* __restrict__ pair_count,
                                                                uint16_t* __restrict__ pkeys,
-                                                               const int2* __restrict__ pre_hits) {
+                                                               const int2* __restrict__ pre_hits,
+                                                               float4* __restrict__ state, int step) {
+  // STEP (multi-hit frames, PRE): one bounce per launch; the ray state (o, life | d, hits, alive)
+  // carries over in `state` between the launches of the frame.
   // PRE (independent waves): the first segment's nearest hits come from nearest_first_kernel.
   // BVH: the K waves of a workgroup are independent (each pulls its own 64-ray groups and owns
   // their writes); they share the workgroup's LDS copy of the top BVH nodes.
@@ -1898,7 +1910,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   // AGG: the K waves of a workgroup reserve their pair positions with one atomic per counter for
   // the whole workgroup (one wave per group: 4096 same-line atomics serialize to ~46 us at config
   // 2); the waves step through their groups together (block-uniform loop and bounce count).
-  constexpr bool AGG = IND && !MULTI && ART_FAST_AGG_RESERVE;
+  constexpr bool AGG = IND && (!MULTI || STEP) && ART_FAST_AGG_RESERVE;
+  constexpr bool ONCE = AGG || STEP;  // one bounce per group (block-uniform)
   __shared__ uint32_t s_agg[AGG ? 2 : 1][AGG ? K : 1][2];
   __shared__ uint32_t s_aggb[2][2];
   (void)s_agg; (void)s_aggb;
@@ -1930,7 +1943,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   const int ngroups = fp.S * nrb;
   // BVH: the top bvh_lds_nodes(...) nodes in LDS (dynamic shared memory, BVH mode only)
   const CullRec* s_nodes = reinterpret_cast<const CullRec*>(s_seg);
-  constexpr bool NODES = IND && (!PRE || MULTI);  // later bounces traverse per lane
+  constexpr bool NODES = IND && (!PRE || (MULTI && !STEP));  // later bounces traverse per lane
+  (void)state; (void)step;
   const int nl = NODES ? bvh_lds_nodes(sc) : 0;
   (void)s_nodes; (void)nl; (void)pre_hits;
   if (NODES) {
@@ -1986,7 +2000,7 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
       bool any_reset;
       const int keep = batch_slot_state(fp, j, my_batch, any_reset);
       if (!keep) frozen |= 1u << k;
-      if (lead && !single_slot && (!keep || any_reset)) {  // TC == 1: every slot is written once below
+      if (lead && !single_slot && (!keep || any_reset) && (!STEP || step == 0)) {  // TC == 1: every slot is written once below
         echo[j] = 0;
         if (HITS) hpo[j] = z;
       }
@@ -2003,9 +2017,21 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   float life = fp.max_life;
   int hits = 0;
   bool alive = valid;
+  const size_t sidx = (size_t)g * 64 + lane;  // ray slot of the state / pre-hit arrays
+  if (STEP && step > 0 && valid) {
+    const float4 a = state[2 * sidx], b = state[2 * sidx + 1];
+    o = mk3(a.x, a.y, a.z);
+    life = a.w;
+    d = mk3(b.x, b.y, b.z);
+    hits = __float_as_int(b.w) & 0xff;
+    alive = ((__float_as_int(b.w) >> 8) & 1) != 0;
+  }
+  const bool alive0 = alive;
+  (void)alive0;
 
-  int bounce = 0;  // wave-uniform (lanes that stopped keep their own `hits`)
-  while (AGG ? bounce == 0 : __any(alive)) {  // identical in every wave of the block -> uniform barriers
+  const int b0 = STEP ? step : 0;
+  int bounce = b0;  // wave-uniform (lanes that stopped keep their own `hits`)
+  while (ONCE ? bounce == b0 : __any(alive)) {  // identical in every wave of the block -> uniform barriers
     const Seg s = make_seg(o, d);
     float best;
     int code;
@@ -2022,8 +2048,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #ifdef ART_DIAG_NO_NEAREST  // diagnostic build only: every live ray hits sphere 0 at distance 1
       best = alive ? 1.0f : FLT_MAX; code = alive ? 0 : kNoHit;
 #else
-      if (PRE && bounce == 0) {
-        const int2 h = gvalid ? pre_hits[(size_t)g * 64 + lane] : make_int2(__float_as_int(FLT_MAX), kNoHit);
+      if (PRE && (STEP || bounce == 0)) {
+        const int2 h = gvalid ? pre_hits[sidx] : make_int2(__float_as_int(FLT_MAX), kNoHit);
         best = __int_as_float(h.x);
         code = h.y;
       } else if (!PRE || MULTI) {
@@ -2283,7 +2309,11 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     }
     ++bounce;
   }
-  if (valid && lead) {
+  if (STEP && valid) {  // the next launch's ray state (a ray that stopped records alive = 0)
+    state[2 * sidx] = make_float4(o.x, o.y, o.z, life);
+    state[2 * sidx + 1] = make_float4(d.x, d.y, d.z, __int_as_float(hits | (alive ? 256 : 0)));
+  }
+  if (valid && lead && (!STEP || (alive0 && !alive))) {  // STEP: in the launch where the ray stops
     if (single_slot) {  // slots past the last hit keep the reset value 0 (:72-80)
       const art_half3 z = {0, 0, 0};
       for (int k = hits; k < H; ++k) {
@@ -2350,11 +2380,12 @@ static int resident_blocks(Kern kern, int threads, size_t lds) {
   return blocks;
 }
 
-template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD = false, bool PRE = false>
+template <int K, bool HITS, int U, int WPE, bool MULTI, bool BVH, bool QUAD = false, bool PRE = false, bool STEP = false>
 static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                            uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
-                           uint32_t* pair_count, uint16_t* pkeys, hipStream_t st, const int2* pre = nullptr) {
-  const size_t lds = QUAD || (PRE && !MULTI) ? 0
+                           uint32_t* pair_count, uint16_t* pkeys, hipStream_t st, const int2* pre = nullptr,
+                           float4* state = nullptr, int step = 0) {
+  const size_t lds = QUAD || (PRE && (!MULTI || STEP)) ? 0
                      : (BVH ? (size_t)bvh_lds_nodes(sc) * sizeof(CullRec) : fast_lds_bytes(sc, fp.T));
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   // BVH: K independent waves per workgroup, one group each (grid-stride past 2^31 / K groups);
@@ -2362,10 +2393,10 @@ static void launch_fast_kh(const DevScene& sc, const FrameParams& fp, const FanL
   // pulling groups from a ticket counter
   const int nblk = QUAD ? (int)std::min<long long>(groups, 1ll << 30)
                  : BVH  ? (int)std::min<long long>((groups + K - 1) / K, 1ll << 30)
-                        : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD, PRE>,
+                        : (int)std::min<long long>(groups, resident_blocks(raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD, PRE, STEP>,
                                                                             64 * K, lds));
-  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD, PRE>), dim3(nblk), dim3(64 * K), lds, st, sc, fp, L,
-                     origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, pre);
+  hipLaunchKernelGGL((raytrace_fast_kernel<K, HITS, U, WPE, MULTI, BVH, QUAD, PRE, STEP>), dim3(nblk), dim3(64 * K), lds, st, sc, fp,
+                     L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, pre, state, step);
 }
 
 template <int K>
@@ -2405,9 +2436,14 @@ static bool bvh_quad(const FrameParams& fp) {
 #ifndef ART_FAST_PRE_NEAREST
 #define ART_FAST_PRE_NEAREST 1  // 1: one-hit frames take the first segment from nearest_first_kernel
 #endif                          // (any size: config 4 5.58 -> 4.74 ms); 2: multi-hit quad frames too
+#ifndef ART_FAST_STEP_MULTI
+#define ART_FAST_STEP_MULTI 1  // multi-hit frames: one first-segment + path launch pair per bounce
+#endif
+static bool bvh_step(const FrameParams& fp) { return ART_FAST_PRE_NEAREST && ART_FAST_STEP_MULTI && fp.H > 1; }
 static bool bvh_pre(const FrameParams& fp) {
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
-  return ART_FAST_PRE_NEAREST && groups < (1ll << 30) && (fp.H == 1 || (ART_FAST_PRE_NEAREST > 1 && bvh_quad(fp)));
+  return ART_FAST_PRE_NEAREST && groups < (1ll << 30) &&
+         (fp.H == 1 || bvh_step(fp) || (ART_FAST_PRE_NEAREST > 1 && bvh_quad(fp)));
 }
 
 // BVH path kernel: one wave per 64-ray group (no collider split), per-lane traversal; or (quad)
@@ -2415,7 +2451,7 @@ static bool bvh_pre(const FrameParams& fp) {
 // kernel's independent waves from its hits.
 static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                             uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, const VisPairs& pairs,
-                            uint32_t* pair_count, uint16_t* pkeys, int2* pre, hipStream_t st) {
+                            uint32_t* pair_count, uint16_t* pkeys, int2* pre, float4* state, hipStream_t st) {
 #define ART_LAUNCH_P(H_, M_) \
   launch_fast_kh<ART_FAST_BVH_WAVES, H_, 1, ART_FAST_WPE_BVH, M_, true, false, true>(sc, fp, L, origins, block, muffle_acc, \
                                                                                      ray_order, work, pairs, pair_count, pkeys, \
@@ -2423,10 +2459,27 @@ static void launch_fast_bvh(const DevScene& sc, const FrameParams& fp, const Fan
   const bool multi_ = fp.H > 1;
   if (pre && bvh_pre(fp)) {
     const long long groups = (long long)fp.S * ((fp.R + 63) / 64);  // < 2^30
-    if (fp.exec)
-      hipLaunchKernelGGL(nearest_first_kernel<true>, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
-    else
-      hipLaunchKernelGGL(nearest_first_kernel<false>, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre);
+    auto first = [&](int step) {
+      if (fp.exec)
+        hipLaunchKernelGGL(nearest_first_kernel<true>, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre,
+                           state, step);
+      else
+        hipLaunchKernelGGL(nearest_first_kernel<false>, dim3((unsigned)groups), dim3(256), 0, st, sc, fp, origins, ray_order, pre,
+                           state, step);
+    };
+    if (state && bvh_step(fp)) {  // one launch pair per bounce; all rays stop by bounce H - 1
+      for (int k = 0; k < fp.H; ++k) {
+        first(k);
+        if (L.has_hits)
+          launch_fast_kh<ART_FAST_BVH_WAVES, true, 1, ART_FAST_WPE_BVH, true, true, false, true, true>(
+              sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, st, pre, state, k);
+        else
+          launch_fast_kh<ART_FAST_BVH_WAVES, false, 1, ART_FAST_WPE_BVH, true, true, false, true, true>(
+              sc, fp, L, origins, block, muffle_acc, ray_order, work, pairs, pair_count, pkeys, st, pre, state, k);
+      }
+      return;
+    }
+    first(0);
     if (L.has_hits) { if (multi_) ART_LAUNCH_P(true, true); else ART_LAUNCH_P(true, false); }
     else { if (multi_) ART_LAUNCH_P(false, true); else ART_LAUNCH_P(false, false); }
     return;
@@ -2576,6 +2629,7 @@ struct PairBufs {
   uint32_t *order, *hist, *prefix, *tot;
   BatchDesc* desc;  // [batches], when the batch descriptors are precomputed
   int2* pre;        // [groups * 64] first-segment nearest hits (ART_FAST_PRE_NEAREST)
+  float4* state;    // [groups * 64][2] ray state between the bounce launches (multi-hit frames)
   size_t total;
   int nblk, nbins;
 };
@@ -2598,6 +2652,8 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   b.desc = ART_VIS_DESC ? reinterpret_cast<BatchDesc*>(take((ecap / 64 + (mcap + 63) / 64) * sizeof(BatchDesc))) : nullptr;
   if (bvh_pre(fp))
     b.pre = reinterpret_cast<int2*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * sizeof(int2)));
+  if (bvh_pre(fp) && bvh_step(fp))
+    b.state = reinterpret_cast<float4*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * 2 * sizeof(float4)));
   if (ART_VIS_SORT && mcap) {
     b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
     b.nbins = fp.T << kSortDirBits;  // keys (target << kSortDirBits | cell) < T << kSortDirBits
@@ -2623,7 +2679,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const bool sorted = ART_FAST_SPLIT && ART_VIS_SORT && mcap && pb.nbins <= kSortBins && max_pairs < (1u << 31);
   uint16_t* pkeys = sorted ? pb.keys : nullptr;
   if (ART_FAST_BVH && sc.bvh_levels > 0) {
-    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, pb.pre, st);
+    launch_fast_bvh(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, pb.pre, pb.state, st);
   } else switch (fast_split(fp.S, fp.R)) {
     case 4: launch_fast_k<4>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st); break;
     default: launch_fast_k<8>(sc, fp, L, origins, block, muffle_acc, ray_order, work, pb.vp, pair_count, pkeys, st); break;
