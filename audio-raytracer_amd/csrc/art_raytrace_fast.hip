@@ -519,8 +519,9 @@ __device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bo
 #define ART_QUAD_SPECULATIVE 1
 #endif
 #ifndef ART_QUAD_FULL_SORT
-#define ART_QUAD_FULL_SORT 2  // 0: nearest child first, the rest in index order; 1: full near-first
-#endif                        // order; 2: full order for scenes with OBBs (config 3 -1 %, config 2 +5 %)
+#define ART_QUAD_FULL_SORT 1  // 0: nearest child first, the rest in index order; 1: full near-first
+#endif                        // order (own first-segment launch: config 3 / 5 -1 %, config 2 even);
+                              // 2: full order for scenes with OBBs only
 template <int SEL>
 __device__ __forceinline__ int quad_bcast(int v) {
   return __builtin_amdgcn_mov_dpp(v, SEL | (SEL << 2) | (SEL << 4) | (SEL << 6), 0xf, 0xf, false);
