@@ -124,6 +124,15 @@ struct Device {
   const void* sorted_soa = nullptr;
   int sorted_n[3] = {-1, -1, -1};
   DevScene sorted_sc{};
+  // host-API frames: the inputs of the last full upload (bytes, layout key, buffers) and the scene
+  // built from them; a frame whose packed inputs are byte-identical skips the H2D copy, the record
+  // decode and the BVH build (the Unity caller passes unchanged collider arrays every frame)
+  std::vector<uint8_t> last_raw;
+  int last_key[10] = {};
+  const void* last_raw_p = nullptr;
+  const void* last_soa_p = nullptr;
+  bool raw_valid = false;
+  DevScene last_sc{};
   bool bound = false;
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
   std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
@@ -382,6 +391,14 @@ void pack_inputs(const art_frame_desc* d, const Frame& f, uint8_t* h) {
 int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   HIP_TRY(c, hipSetDevice(dv.id));
   if (!dv.raw.reserve(f.raw_bytes) || !dv.soa.reserve(f.soa_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
+  const int key[10] = {f.ns, f.na, f.no, f.T, f.R, f.TC, f.H, f.fp.vol_n, f.fp.muf_n, (int)f.raw_bytes};
+  if (!f.resident && dv.raw_valid && dv.last_raw_p == dv.raw.p && dv.last_soa_p == dv.soa.p &&
+      memcmp(dv.last_key, key, sizeof key) == 0 && memcmp(dv.last_raw.data(), h_in, f.raw_bytes) == 0) {
+    dv.sc = dv.last_sc;  // device records, sorted copies and BVH are those of these same inputs
+    dv.bound = true;
+    return ART_OK;
+  }
+  dv.raw_valid = false;
   HIP_TRY(c, hipMemcpyAsync(dv.raw.p, h_in, f.raw_bytes, hipMemcpyHostToDevice, dv.stream));
   uint8_t* raw = static_cast<uint8_t*>(dv.raw.p);
   uint8_t* soa = static_cast<uint8_t*>(dv.soa.p);
@@ -441,6 +458,14 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     dv.sorted_sc = sc;
   }
   HIP_TRY(c, hipGetLastError());
+  if (!f.resident) {
+    dv.last_raw.assign(h_in, h_in + f.raw_bytes);
+    memcpy(dv.last_key, key, sizeof key);
+    dv.last_raw_p = dv.raw.p;
+    dv.last_soa_p = dv.soa.p;
+    dv.last_sc = sc;
+    dv.raw_valid = true;
+  }
   dv.bound = true;
   return ART_OK;
 }

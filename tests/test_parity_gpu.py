@@ -260,3 +260,39 @@ def test_golden_on_gpu(ctx, name):
     ctx.set_flags(0)
     assert all(cnt_out.equal(expected).values())
     assert ctx.last_test_counts() == counts
+
+
+@pytest.mark.gpu
+def test_inputs_change_between_frames(ctx):
+    """art_schedule reuses the device scene (records, sorted copies, BVH) when the packed inputs are
+    byte-identical to the last frame's; any change — every sphere moved, one radius changed,
+    the targets moved — must rebuild it. Each frame is checked against the oracle."""
+    scene, org, params = art.synth(art.CONFIGS[2], S=8, R=128, C_scale=0.25)
+    base_c = scene.spheres["center"].copy()
+    base_r = scene.spheres["radius"].copy()
+    base_t = scene.targets.copy()
+
+    def check():
+        o_gpu = art.FanOutputs(8, scene.R, params.max_hits_per_ray, scene.T, params.thread_count)
+        o_ref = o_gpu.copy()
+        oracle.run_frame(art.Frame(scene, params, org, o_ref), threads=16)
+        ctx.set_flags(0)
+        ctx.run(art.Frame(scene, params, org, o_gpu))
+        eq = o_gpu.equal(o_ref)
+        assert all(eq.values()), f"{eq}\n{_diff_report(o_gpu, o_ref)}"
+        return o_gpu
+
+    a = check()
+    check()                                           # identical inputs: cached scene
+    scene.spheres["center"][:] = base_c[::-1]         # every sphere moved
+    b = check()
+    scene.spheres["radius"][:] = base_r
+    scene.spheres["center"][:] = base_c
+    scene.spheres["radius"][3] = scene.spheres["radius"][3] ^ 0x0400  # one radius changed
+    check()
+    scene.spheres["radius"][:] = base_r
+    scene.targets[:] = base_t[::-1]                   # only the targets moved
+    check()
+    scene.targets[:] = base_t
+    c = check()                                       # back to the first frame's inputs
+    assert all(c.equal(a).values()) and not all(b.equal(a).values())
