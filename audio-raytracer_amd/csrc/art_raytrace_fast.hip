@@ -1262,6 +1262,9 @@ __device__ __forceinline__ WaveBox make_wave_box(const Seg& s, float maxd, bool 
   return wb;
 }
 
+#ifndef ART_VIS_OBB_PRE
+#define ART_VIS_OBB_PRE 1
+#endif
 // wbp: a precomputed box of (a superset of) the wave's segments, else computed here.
 __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid, int lane,
                                            unsigned long long* ex, bool done_in = false, int c_lo = 0, int c_hi = 1 << 30,
@@ -1301,11 +1304,36 @@ __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, flo
         float d;
         return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
       }, nt[1]);
-    } else {
+    } else if (!ART_VIS_OBB_PRE) {
       blocked = test_candidates<1>(obb, b, cs, blocked, done, [&](const ObbRec& r) {
         float d;
         return obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
       }, nt[2]);
+    } else {
+      // OBB candidates (118-op exact test): first each lane's slab test against the collider's own
+      // widened bounds (the per-lane BVH node test of anyhit_bvh: a blocker's segment enters them
+      // before maxd); the exact test runs only where a live lane passes
+      const CullRec* cb = (obb == sc.obb_s ? sc.cull_s : sc.cull) + sc.ns + sc.na;
+      const float oml = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+      const bool force = !(isfinite(oml) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
+                         (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
+      while (cs.left > 0) {
+        const int i = wave_uniform(b + cs.pop());
+        const CullRec c = ldc(cb, i);
+        const float m = c.factor * (c.scale + oml);
+        float tn, tf;
+        const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, c.lox - m, c.loy - m, c.loz - m,
+                                   c.hix + m, c.hiy + m, c.hiz + m, tn, tf);
+        const bool near = force || (h && tn <= maxd);
+        if (!__any(near && !blocked && !done)) continue;
+        const ObbRec r = ldc(obb, i);
+        ++nt[2];
+        if (near && !blocked) {
+          float d;
+          blocked = obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
+        }
+        if (__all(blocked || done)) break;
+      }
     }
   };
   if (!two) {
