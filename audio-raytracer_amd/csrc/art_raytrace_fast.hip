@@ -1262,6 +1262,9 @@ __device__ __forceinline__ WaveBox make_wave_box(const Seg& s, float maxd, bool 
   return wb;
 }
 
+#ifndef ART_VIS_ALL_PRE
+#define ART_VIS_ALL_PRE 0
+#endif
 #ifndef ART_VIS_OBB_PRE
 #define ART_VIS_OBB_PRE 1
 #endif
@@ -1294,7 +1297,31 @@ __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, flo
   };
   // exact tests of one chunk's candidates (records `sph`/`aabb`/`obb`: reference or sorted order)
   auto test_chunk = [&](int type, int b, CandSet& cs, const SphereRec* sph, const AabbRec* aabb, const ObbRec* obb) {
-    if (type == 0) {
+    if (ART_VIS_ALL_PRE && type < 2) {  // the same prefilter for spheres and boxes
+      const CullRec* cb = (sph == sc.sph_s ? sc.cull_s : sc.cull) + (type == 0 ? 0 : sc.ns);
+      const float oml = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+      const bool force = !(isfinite(oml) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z)) ||
+                         (s.d.x == 0.0f && s.d.y == 0.0f && s.d.z == 0.0f);
+      while (cs.left > 0) {
+        const int i = wave_uniform(b + cs.pop());
+        const CullRec c = ldc(cb, i);
+        const float m = c.factor * (c.scale + oml);
+        float tn, tf;
+        const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, c.lox - m, c.loy - m, c.loz - m,
+                                   c.hix + m, c.hiy + m, c.hiz + m, tn, tf);
+        const bool near = force || (h && tn <= maxd);
+        if (!__any(near && !blocked && !done)) continue;
+        ++nt[type];
+        if (type == 0) {
+          const SphereRec r = ldc(sph, i);
+          if (near && !blocked) { float d; blocked = sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner; }
+        } else {
+          const AabbRec r = ldc(aabb, i);
+          if (near && !blocked) { float d; blocked = aabb_test<false>(s, r, d) && d < maxd && r.tid != owner; }
+        }
+        if (__all(blocked || done)) break;
+      }
+    } else if (type == 0) {
       blocked = test_candidates<kCullU>(sph, b, cs, blocked, done, [&](const SphereRec& r) {
         float d;
         return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
