@@ -518,6 +518,9 @@ __device__ __forceinline__ void nearest_bvh(const DevScene& sc, const Seg& s, bo
 #ifndef ART_QUAD_SPECULATIVE
 #define ART_QUAD_SPECULATIVE 1
 #endif
+#ifndef ART_QUAD_SELECT_PUSH
+#define ART_QUAD_SELECT_PUSH 0  // 1: stack pushes / pops as selects (measured 1-2 % slower)
+#endif
 #ifndef ART_QUAD_FULL_SORT
 #define ART_QUAD_FULL_SORT 1  // 0: nearest child first, the rest in index order; 1: full near-first
 #endif                        // order (own first-segment launch: config 3 / 5 -1 %, config 2 even);
@@ -566,6 +569,16 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
       if (e[b] < e[a]) { const float te = e[a]; e[a] = e[b]; e[b] = te; const int tc = c[a]; c[a] = c[b]; c[b] = tc; }
     };
     cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
+#if ART_QUAD_SELECT_PUSH
+    // branch-free: the entered children are the sorted prefix e[0 .. nv); lane q in 1 .. nv - 1
+    // pushes child q (far first: c[nv - 1] lowest), the quad descends into c[0] or pops
+    const int nv = (e[0] < INFINITY) + (e[1] < INFINITY) + (e[2] < INFINITY) + (e[3] < INFINITY);
+    const int ck = qd == 1 ? c[1] : (qd == 2 ? c[2] : c[3]);
+    const int top = (int)my[sp ? sp - 1 : 0];
+    if (qd >= 1 && qd < nv) my[sp + nv - 1 - qd] = (uint16_t)(c0 + ck);
+    g = nv > 0 ? c0 + c[0] : (sp ? top : -1);
+    sp = nv > 0 ? sp + nv - 1 : (sp ? sp - 1 : 0);
+#else
     if (e[0] < INFINITY) {
 #pragma unroll
       for (int k = 3; k >= 1; --k)
@@ -578,6 +591,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
       g = sp ? (int)my[sp - 1] : -1;
       sp = sp ? sp - 1 : 0;
     }
+#endif
     } else {
     // descend into the nearest child ((entry, index) minimum over the quad, two DPP steps); the
     // other entered children go on the stack in index order, each lane writing its own
@@ -656,7 +670,17 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
   int pend = -1;
   while (__any(g >= 0 || pend >= 0)) {
     for (;;) {
+#if ART_QUAD_SELECT_PUSH
+      {
+        const bool park = g >= leaf0 && pend < 0;
+        const int top = (int)my[sp ? sp - 1 : 0];
+        pend = park ? g : pend;
+        g = park ? (sp ? top : -1) : g;
+        sp = park ? (sp ? sp - 1 : 0) : sp;
+      }
+#else
       if (g >= leaf0 && pend < 0) { pend = g; pop(); }
+#endif
       const bool inner = g >= 0 && g < leaf0;
       if (!__any(inner) || !__any(pend < 0 && g >= 0)) break;
       if (inner) inner_step();
