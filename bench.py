@@ -456,7 +456,7 @@ def main():
 
     value = tests_all * a.steps / dt
     res = {
-        "metric": "ray-collider tests/sec + p50 per-frame batch ms, 256src x 512ray x 4096col",
+        "metric": "ray-collider tests/sec + p50 per-frame batch ms, 256src\u00d7512ray\u00d74096col",  # BASELINE.json "metric"
         "value": value,
         "unit": "ray-collider tests/s",
         "n_gpus": world,
