@@ -723,13 +723,17 @@ __device__ __forceinline__ void nearest_bvh_quad(const DevScene& sc, const Seg& 
 // workgroup, wave w traverses rays 16w .. 16w + 15 with 4 lanes each (quad_nearest_core). Without
 // the path kernel's emission state live across the traversal, the registers allow more waves per
 // SIMD. hits[g * 64 + r] = (distance bits, code) of the group's ray slot r.
+#ifndef ART_FAST_COMPACT
+#define ART_FAST_COMPACT 1  // multi-hit frames: later bounces traverse only the live rays
+#endif
+constexpr int kLiveCounters = 32;  // per-bounce list counters (H <= 32)
 #ifndef ART_FAST_WPE_PRE
 #define ART_FAST_WPE_PRE 8
 #endif
 template <bool EX>  // EX: count the executed tests (fp.exec)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WPE_PRE))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
-    int2* __restrict__ hits, const float4* __restrict__ state, int step) {
+    int2* __restrict__ hits, float4* __restrict__ state, int step) {
   __shared__ uint16_t s_stk[kBvhStack * 64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
@@ -741,6 +745,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FAST_WP
   const int ray = valid ? ray_order[slot] : 0;
   Seg s;
   bool alive = valid;
+  if (ART_FAST_COMPACT && state && step > 0) {  // the previous bounce's list of live ray slots
+    const int ngroups = fp.S * nrb;
+    const uint32_t* live = reinterpret_cast<const uint32_t*>(state + 2 * (size_t)ngroups * 64);
+    const uint32_t cnt = live[(size_t)ngroups * 64 + step];
+    if ((uint32_t)g * 64u >= cnt) return;  // the whole workgroup: past the list
+    const uint32_t e = (uint32_t)g * 64u + (uint32_t)rr;
+    const bool ok = e < cnt;
+    const uint32_t i = ok ? live[e] : 0u;
+    const float4 a = state[2 * (size_t)i], b = state[2 * (size_t)i + 1];
+    s = make_seg(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
+    alive = ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
+    float best;
+    int code;
+    quad_nearest_core<EX>(sc, s, alive, lane, s_stk + rr * kBvhStack, best, code, EX ? fp.exec : nullptr);
+    if ((lane & 3) == 0 && ok) hits[i] = make_int2(__float_as_int(best), code);
+    return;
+  }
+  if (ART_FAST_COMPACT && state && step == 0 && blockIdx.x == 0 && threadIdx.x < kLiveCounters)
+    (reinterpret_cast<uint32_t*>(state + 2 * (size_t)fp.S * nrb * 64) + (size_t)fp.S * nrb * 64)[threadIdx.x] = 0u;
   if (step == 0) {
     s = make_seg(load3(origins, fan), load_dir(sc.dirs, ray));
   } else {  // later bounce of a multi-hit frame: the path kernel's ray state
@@ -1994,6 +2017,8 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
   constexpr bool ONCE = AGG || STEP;  // one bounce per group (block-uniform)
   __shared__ uint32_t s_agg[AGG ? 2 : 1][AGG ? K : 1][2];
   __shared__ uint32_t s_aggb[2][2];
+  __shared__ uint32_t s_live[AGG && STEP ? 2 : 1][AGG && STEP ? K : 1], s_liveb[2];
+  (void)s_live; (void)s_liveb;
   (void)s_agg; (void)s_aggb;
   int it = 0;  // block-uniform group iteration (AGG buffers alternate by its parity)
   __shared__ float s_dist[K][64];
@@ -2393,6 +2418,31 @@ __global__ __launch_bounds__(64 * K) __attribute__((amdgpu_waves_per_eu(WPE))) v
     state[2 * sidx] = make_float4(o.x, o.y, o.z, life);
     state[2 * sidx + 1] = make_float4(d.x, d.y, d.z, __int_as_float(hits | (alive ? 256 : 0)));
   }
+  if (STEP && ART_FAST_COMPACT) {  // the rays still alive: the next bounce's traversal list
+    uint32_t* live = reinterpret_cast<uint32_t*>(state + 2 * (size_t)ngroups * 64);
+    uint32_t* live_n = live + (size_t)ngroups * 64;
+    const bool app = valid && alive && step + 1 < fp.H;
+    const unsigned long long m = __ballot(app);
+    uint32_t base = 0;
+    if (AGG) {  // every wave of the workgroup is here (one bounce per launch)
+      const int par = it & 1;
+      if (lane == 0) s_live[par][w] = (uint32_t)__popcll(m);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) t += s_live[par][k];
+        s_liveb[par] = t ? atomicAdd(&live_n[step + 1], t) : 0u;
+      }
+      __syncthreads();
+      base = s_liveb[par];
+      for (int k = 0; k < w; ++k) base += s_live[par][k];
+    } else {
+      if (lane == 0 && m) base = atomicAdd(&live_n[step + 1], (uint32_t)__popcll(m));
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+    }
+    if (app) live[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)sidx;
+  }
   if (valid && lead && (!STEP || (alive0 && !alive))) {  // STEP: in the launch where the ray stops
     if (single_slot) {  // slots past the last hit keep the reset value 0 (:72-80)
       const art_half3 z = {0, 0, 0};
@@ -2519,7 +2569,9 @@ static bool bvh_quad(const FrameParams& fp) {
 #ifndef ART_FAST_STEP_MULTI
 #define ART_FAST_STEP_MULTI 1  // multi-hit frames: one first-segment + path launch pair per bounce
 #endif
-static bool bvh_step(const FrameParams& fp) { return ART_FAST_PRE_NEAREST && ART_FAST_STEP_MULTI && fp.H > 1; }
+static bool bvh_step(const FrameParams& fp) {
+  return ART_FAST_PRE_NEAREST && ART_FAST_STEP_MULTI && fp.H > 1 && fp.H <= kLiveCounters;
+}
 static bool bvh_pre(const FrameParams& fp) {
   const long long groups = (long long)fp.S * ((fp.R + 63) / 64);
   return ART_FAST_PRE_NEAREST && groups < (1ll << 30) &&
@@ -2733,7 +2785,8 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   if (bvh_pre(fp))
     b.pre = reinterpret_cast<int2*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * sizeof(int2)));
   if (bvh_pre(fp) && bvh_step(fp))
-    b.state = reinterpret_cast<float4*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * 2 * sizeof(float4)));
+    b.state = reinterpret_cast<float4*>(take((size_t)fp.S * ((fp.R + 63) / 64) * 64 * (2 * sizeof(float4) + 4) +
+                                             kLiveCounters * 4));  // + live list and counters
   if (ART_VIS_SORT && mcap) {
     b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
     b.nbins = fp.T << kSortDirBits;  // keys (target << kSortDirBits | cell) < T << kSortDirBits
