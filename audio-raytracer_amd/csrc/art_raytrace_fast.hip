@@ -1530,8 +1530,8 @@ __device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Se
   owner = __float_as_int(q1.w);
 }
 
-#ifndef ART_VIS_WPE
-#define ART_VIS_WPE 6
+#ifndef ART_VIS_WPE  // 8 waves per SIMD once the test counters compile out (vis_kernel<false>): config 2
+#define ART_VIS_WPE 8  // vis 228 -> 215 us, config 5 -2 %, config 3 even (a few spills, measured faster)
 #endif
 #ifndef ART_VIS_PLAIN_FLAG
 #define ART_VIS_PLAIN_FLAG 0
@@ -1924,13 +1924,16 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 
 // One launch for both visibility halves, so they overlap on the chip: blocks [0, n_echo) trace
 // the echo batches by quad BVH traversal (longer jobs first), the others run the sweep's items.
+// EX: count the executed tests (fp.exec); without it the counters compile out.
+template <bool EX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
                 const uint32_t* __restrict__ order, const BatchDesc* __restrict__ desc, unsigned long long* ex,
                 uint32_t n_echo) {
   __shared__ uint16_t s_stk[64 * kBvhStack];
-  if (blockIdx.x < n_echo) vis_quad_body(sc, vp, count, order, ex, blockIdx.x, s_stk);
-  else vis_sweep_body(sc, vp, count, nb_max, order, desc, ex, n_echo, blockIdx.x - n_echo);
+  unsigned long long* e = EX ? ex : nullptr;
+  if (blockIdx.x < n_echo) vis_quad_body(sc, vp, count, order, e, blockIdx.x, s_stk);
+  else vis_sweep_body(sc, vp, count, nb_max, order, desc, e, n_echo, blockIdx.x - n_echo);
 }
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
@@ -2842,8 +2845,12 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
       const size_t vitems = (size_t)(nb_max - eb) * vis_ranges(sc);
       const size_t blocks = eb + (vitems + 3) / 4;
       if (blocks)
-        hipLaunchKernelGGL(vis_kernel, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
-                           use_desc ? (const BatchDesc*)pb.desc : nullptr, fp.exec, eb);
+        if (fp.exec)
+          hipLaunchKernelGGL(vis_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
+                             use_desc ? (const BatchDesc*)pb.desc : nullptr, fp.exec, eb);
+        else
+          hipLaunchKernelGGL(vis_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
+                             use_desc ? (const BatchDesc*)pb.desc : nullptr, nullptr, eb);
     }
     hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                        muffle_acc);
