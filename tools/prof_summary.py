@@ -68,8 +68,8 @@ def main():
             w.writerows(rows)
 
     # HBM traffic of the timed raytrace stage per frame (sum over its kernels of the mean per launch)
-    # (nearest_first_kernel<true> is the one test-counting launch of a run, not a timed frame)
-    stage = [k for k in per if k.startswith(STAGE) and not k.startswith("nearest_first_kernel<true>")]
+    # (the <true> instantiations are the one test-counting launch of a run, not timed frames)
+    stage = [k for k in per if k.startswith(STAGE) and not k.startswith(("nearest_first_kernel<true>", "vis_kernel<true>"))]
     if stage:
         def mean(k, c):
             v = per[k].get(c, [])
