@@ -1932,8 +1932,9 @@ void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, ui
                 uint32_t n_echo) {
   __shared__ uint16_t s_stk[64 * kBvhStack];
   unsigned long long* e = EX ? ex : nullptr;
+  const BatchDesc* dsc = ART_VIS_DESC ? desc : nullptr;  // off: the descriptor branch compiles out
   if (blockIdx.x < n_echo) vis_quad_body(sc, vp, count, order, e, blockIdx.x, s_stk);
-  else vis_sweep_body(sc, vp, count, nb_max, order, desc, e, n_echo, blockIdx.x - n_echo);
+  else vis_sweep_body(sc, vp, count, nb_max, order, dsc, e, n_echo, blockIdx.x - n_echo);
 }
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
