@@ -1652,7 +1652,8 @@ __global__ __launch_bounds__(256) void vis_batch_kernel(VisPairs vp, const uint3
 // vis_finalize writes the outputs after the kernel boundary.
 __device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
                                                uint32_t nb_max, const uint32_t* order, const BatchDesc* desc,
-                                               unsigned long long* ex, uint32_t b_first, uint32_t blk) {
+                                               unsigned long long* ex, uint32_t b_first, uint32_t blk,
+                                               bool force_two = false) {
   const int lane = threadIdx.x & 63;
   // items cover batches [b_first, nb_max) (b_first > 0: the echo batches run in vis_echo_quad_kernel)
   const uint32_t nbv = nb_max - b_first;
@@ -1683,7 +1684,8 @@ __device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPair
   s.a2 = s.a4 = 0.0f;
   if (valid) load_pair_seg(vp, pi, s, maxd, owner);
   const int nch = (sc.ns + kChunk - 1) / kChunk + (sc.na + kChunk - 1) / kChunk + (sc.no + kChunk - 1) / kChunk;
-  const bool two = sc.chunks != nullptr && (ART_VIS_TWO_LEVEL || (ART_FAST_TWO_LEVEL && sc.nchunks > 64));
+  // force_two (compile-time true in vis_kernel<., true>): the scene has the sorted chunks
+  const bool two = force_two || (sc.chunks != nullptr && (ART_VIS_TWO_LEVEL || (ART_FAST_TWO_LEVEL && sc.nchunks > 64)));
   const int c_lo = (int)(((long long)nch * r) / nranges), c_hi = (int)(((long long)nch * (r + 1)) / nranges);
 #if ART_VIS_CONE
   bool blocked;
@@ -1925,7 +1927,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 // One launch for both visibility halves, so they overlap on the chip: blocks [0, n_echo) trace
 // the echo batches by quad BVH traversal (longer jobs first), the others run the sweep's items.
 // EX: count the executed tests (fp.exec); without it the counters compile out.
-template <bool EX>
+template <bool EX, bool TWO>  // TWO: two-level sweep known on the host (the flat sweep compiles out)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_VIS_WPE)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
                 const uint32_t* __restrict__ order, const BatchDesc* __restrict__ desc, unsigned long long* ex,
@@ -1934,7 +1936,7 @@ void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, ui
   unsigned long long* e = EX ? ex : nullptr;
   const BatchDesc* dsc = ART_VIS_DESC ? desc : nullptr;  // off: the descriptor branch compiles out
   if (blockIdx.x < n_echo) vis_quad_body(sc, vp, count, order, e, blockIdx.x, s_stk);
-  else vis_sweep_body(sc, vp, count, nb_max, order, dsc, e, n_echo, blockIdx.x - n_echo);
+  else vis_sweep_body(sc, vp, count, nb_max, order, dsc, e, n_echo, blockIdx.x - n_echo, TWO);
 }
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
@@ -2845,13 +2847,19 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
       const uint32_t eb = (ART_VIS_ECHO_QUAD && sc.bvh_levels > 0) ? (ART_VIS_ALL_QUAD ? nb_max : pb.vp.echo_cap / 64) : 0u;
       const size_t vitems = (size_t)(nb_max - eb) * vis_ranges(sc);
       const size_t blocks = eb + (vitems + 3) / 4;
-      if (blocks)
+      const BatchDesc* dsc = use_desc ? (const BatchDesc*)pb.desc : nullptr;
+      if (blocks) {
+        const bool two = sc.chunks != nullptr && ART_VIS_TWO_LEVEL;
         if (fp.exec)
-          hipLaunchKernelGGL(vis_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
-                             use_desc ? (const BatchDesc*)pb.desc : nullptr, fp.exec, eb);
+          hipLaunchKernelGGL((vis_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max,
+                             order, dsc, fp.exec, eb);
+        else if (two)
+          hipLaunchKernelGGL((vis_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max,
+                             order, dsc, nullptr, eb);
         else
-          hipLaunchKernelGGL(vis_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max, order,
-                             use_desc ? (const BatchDesc*)pb.desc : nullptr, nullptr, eb);
+          hipLaunchKernelGGL((vis_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max,
+                             order, dsc, nullptr, eb);
+      }
     }
     hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                        muffle_acc);
