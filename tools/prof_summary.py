@@ -69,7 +69,7 @@ def main():
 
     # HBM traffic of the timed raytrace stage per frame (sum over its kernels of the mean per launch)
     # (the <true> instantiations are the one test-counting launch of a run, not timed frames)
-    stage = [k for k in per if k.startswith(STAGE) and not k.startswith(("nearest_first_kernel<true>", "vis_kernel<true>"))]
+    stage = [k for k in per if k.startswith(STAGE) and not k.startswith(("nearest_first_kernel<true", "vis_kernel<true"))]
     if stage:
         def mean(k, c):
             v = per[k].get(c, [])
