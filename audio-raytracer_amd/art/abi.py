@@ -203,6 +203,7 @@ SIGNATURES = {
     "art_colliders_sync": (I32, [VP]),
     "art_colliders_last_sync": (I32, [VP, C.POINTER(art_collider_sync_stats)]),
     "art_device_count": (I32, []),
+    "art_create_on": (I32, [C.POINTER(I32), I32, C.POINTER(VP)]),
     # art_synth.h
     "art_synth_scene": (I32, [C.POINTER(art_synth_config), VP, VP, VP, VP, VP, VP]),
     "art_fibonacci_directions": (None, [I32, VP]),

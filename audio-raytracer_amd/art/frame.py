@@ -212,10 +212,16 @@ class JobHandle:
 class Context:
     """An art_ctx: one HIP stream per selected device. Raises ArtError(ART_E_DEVICE) without a GPU."""
 
-    def __init__(self, device_mask: int = 0, flags: int = 0):
+    def __init__(self, device_mask: int = 0, flags: int = 0, devices: list[int] | None = None):
+        """device_mask: bit i selects HIP device i (art_create); devices: an explicit device list,
+        ids may repeat (art_create_on: shards on separate streams of one device)."""
         self.lib = abi.load_library()
         p = C.c_void_p()
-        rc = self.lib.art_create(device_mask, C.byref(p))
+        if devices is not None:
+            ids = (C.c_int32 * len(devices))(*devices)
+            rc = self.lib.art_create_on(ids, len(devices), C.byref(p))
+        else:
+            rc = self.lib.art_create(device_mask, C.byref(p))
         if rc:
             raise ArtError(rc, "art_create failed (no HIP device?) — the product path has no CPU fallback")
         self.ptr = p

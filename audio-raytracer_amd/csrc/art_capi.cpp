@@ -112,6 +112,8 @@ struct Device {
   bool st_fresh = true;         // capacity (re)allocated: every record must be uploaded
   hipEvent_t st_done = nullptr; // recorded after the last sync's upload + decode (dv.stream)
   bool st_pending = false;      // st_done recorded and the host staging may still be read
+  hipEvent_t launch_done = nullptr;  // after the last art_launch_device frame (caller's stream)
+  bool launch_pending = false;       // a sync must wait for it before rewriting records / BVH
   uint64_t exec_launches = 0;
   DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
   int wf_blocks = 0;
@@ -606,14 +608,24 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         fpx.exec = static_cast<unsigned long long*>(dv.exec.p);
         dv.exec_launches++;
       }
+      // The pair arrays index pairs with 32-bit slots (sorted below 2^31) and the echo outputs with
+      // 32-bit half offsets into the block: larger frames run as consecutive fan chunks on the
+      // stream (the pair buffer and counter are reused, the muffle accumulators offset per chunk).
+      const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.L.stride);
       FrameParams fps = fpx;
-      fps.S = fan_count;
+      fps.S = std::min(fan_count, chunk);
       if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
       DevScene scx = dv.sc;
       if (c->flags & ART_CTX_NO_BVH) scx.bvh_levels = 0;  // cone / K-way split path
       fpx.vis_bvh = (c->flags & ART_CTX_VIS_BVH) ? 1 : 0;
-      launch_raytrace_fast(scx, fpx, f.L, d_origins, d_block, acc, order, static_cast<uint32_t*>(dv.work.p), dv.pairs.p,
-                           pair_count, st);
+      for (int b0 = 0; b0 < fan_count; b0 += chunk) {
+        FrameParams fpc = fpx;
+        fpc.S = std::min(chunk, fan_count - b0);
+        if (b0) HIP_TRY(c, hipMemsetAsync(pair_count, 0, 16, st));
+        launch_raytrace_fast(scx, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
+                             acc + (size_t)b0 * f.TC * f.T, order, static_cast<uint32_t*>(dv.work.p), dv.pairs.p, pair_count,
+                             st);
+      }
     } else if (f.T <= 31) {
       int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);
       if (rc) return rc;
@@ -665,6 +677,33 @@ bool fan_wants_hits(const art_fan* fans, int n) {
   return false;
 }
 
+// One device's share of an art_schedule frame: scene upload, origins and in/out slot arrays H2D,
+// kernels, result blocks D2H, completion event (all async on dv.stream).
+int enqueue_device_frame(art_ctx* c, Device& dv, const Frame& f, const uint8_t* hin, const float* horg, uint8_t* hb,
+                         bool need_echo, bool count) {
+  const FanLayout& L = f.L;
+  int rc = upload_scene(c, dv, f, hin);
+  if (rc) return rc;
+  if (dv.fan_count == 0) { HIP_TRY(c, hipEventRecord(dv.done, dv.stream)); return ART_OK; }
+  const size_t bbytes = (size_t)dv.fan_count * L.stride;
+  if (!dv.origins.reserve((size_t)dv.fan_count * 12) || !dv.block.reserve(bbytes))
+    return fail(c, ART_E_NOMEM, "device allocation failed");
+  HIP_TRY(c, hipMemcpyAsync(dv.origins.p, horg + 3 * dv.fan_begin, (size_t)dv.fan_count * 12, hipMemcpyHostToDevice, dv.stream));
+  uint8_t* hbs = hb + (size_t)dv.fan_begin * L.stride;
+  if (need_echo || L.has_hits) {
+    HIP_TRY(c, hipMemcpyAsync(dv.block.p, hbs, bbytes, hipMemcpyHostToDevice, dv.stream));
+  } else {  // only the muffle + permeation slot arrays (adjacent in the record)
+    HIP_TRY(c, hipMemcpy2DAsync(static_cast<uint8_t*>(dv.block.p) + L.muffle_off, L.stride, hbs + L.muffle_off, L.stride,
+                                L.echo_off - L.muffle_off, dv.fan_count, hipMemcpyHostToDevice, dv.stream));
+  }
+  rc = enqueue_kernels(c, dv, f, static_cast<const float*>(dv.origins.p), dv.fan_count, static_cast<uint8_t*>(dv.block.p),
+                       dv.stream, count);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(hbs, dv.block.p, bbytes, hipMemcpyDeviceToHost, dv.stream));
+  HIP_TRY(c, hipEventRecord(dv.done, dv.stream));
+  return ART_OK;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -680,28 +719,43 @@ ART_API int art_device_count(void) {
   return n;
 }
 
-ART_API int art_create(uint32_t device_mask, art_ctx** out) {
+static int create_on(const int32_t* ids, int32_t count, art_ctx** out) {
   if (!out) return ART_E_INVALID;
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ART_E_DEVICE;
+  if (count <= 0 || count > 64 || !ids) return ART_E_INVALID;
   art_ctx* c = new (std::nothrow) art_ctx();
   if (!c) return ART_E_NOMEM;
-  if (device_mask == 0) device_mask = 1;
-  for (int i = 0; i < 32; ++i) {
-    if (!(device_mask & (1u << i))) continue;
-    if (i >= n) { delete c; return ART_E_DEVICE; }
+  for (int32_t k = 0; k < count; ++k) {
+    const int i = ids[k];
     Device dv;
     dv.id = i;
-    if (hipSetDevice(i) != hipSuccess || hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking) != hipSuccess ||
+    if (i < 0 || i >= n || hipSetDevice(i) != hipSuccess || hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&dv.done, hipEventDisableTiming) != hipSuccess) {
-      delete c;
+      if (dv.stream) (void)hipStreamDestroy(dv.stream);
+      c->devs.push_back(dv);
+      art_destroy(c);
       return ART_E_DEVICE;
     }
     c->devs.push_back(dv);
   }
   *out = c;
   return ART_OK;
+}
+
+ART_API int art_create(uint32_t device_mask, art_ctx** out) {
+  if (!out) return ART_E_INVALID;
+  if (device_mask == 0) device_mask = 1;
+  int32_t ids[32];
+  int32_t k = 0;
+  for (int i = 0; i < 32; ++i)
+    if (device_mask & (1u << i)) ids[k++] = i;
+  return create_on(ids, k, out);
+}
+
+ART_API int art_create_on(const int32_t* device_ids, int32_t count, art_ctx** out) {
+  return create_on(device_ids, count, out);
 }
 
 ART_API void art_destroy(art_ctx* c) {
@@ -713,6 +767,7 @@ ART_API void art_destroy(art_ctx* c) {
     dv.work.release(); dv.exec.release(); dv.pairs.release(); dv.dsp.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
     if (dv.st_done) (void)hipEventDestroy(dv.st_done);
+    if (dv.launch_done) (void)hipEventDestroy(dv.launch_done);
     dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
@@ -801,26 +856,18 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
     dv.fan_begin = (int)((long long)fan_count * k / nd);
     dv.fan_count = (int)((long long)fan_count * (k + 1) / nd) - dv.fan_begin;
   }
+  // Enqueue per device. An error on device k leaves devices [0, k) (and k itself, partly) with
+  // async copies that still read or write the pinned staging: drain every stream before returning,
+  // so the next art_schedule can repack h_in / h_block safely.
   for (Device& dv : c->devs) {
-    rc = upload_scene(c, dv, f, hin);
-    if (rc) return rc;
-    if (dv.fan_count == 0) { HIP_TRY(c, hipEventRecord(dv.done, dv.stream)); continue; }
-    const size_t bbytes = (size_t)dv.fan_count * L.stride;
-    if (!dv.origins.reserve((size_t)dv.fan_count * 12) || !dv.block.reserve(bbytes))
-      return fail(c, ART_E_NOMEM, "device allocation failed");
-    HIP_TRY(c, hipMemcpyAsync(dv.origins.p, horg + 3 * dv.fan_begin, (size_t)dv.fan_count * 12, hipMemcpyHostToDevice, dv.stream));
-    uint8_t* hbs = hb + (size_t)dv.fan_begin * L.stride;
-    if (need_echo || L.has_hits) {
-      HIP_TRY(c, hipMemcpyAsync(dv.block.p, hbs, bbytes, hipMemcpyHostToDevice, dv.stream));
-    } else {  // only the muffle + permeation slot arrays (adjacent in the record)
-      HIP_TRY(c, hipMemcpy2DAsync(static_cast<uint8_t*>(dv.block.p) + L.muffle_off, L.stride, hbs + L.muffle_off, L.stride,
-                                  L.echo_off - L.muffle_off, dv.fan_count, hipMemcpyHostToDevice, dv.stream));
+    rc = enqueue_device_frame(c, dv, f, hin, horg, hb, need_echo, count);
+    if (rc) {
+      for (Device& e : c->devs) {
+        (void)hipSetDevice(e.id);
+        (void)hipStreamSynchronize(e.stream);
+      }
+      return rc;
     }
-    rc = enqueue_kernels(c, dv, f, static_cast<const float*>(dv.origins.p), dv.fan_count, static_cast<uint8_t*>(dv.block.p),
-                         dv.stream, count);
-    if (rc) return rc;
-    HIP_TRY(c, hipMemcpyAsync(hbs, dv.block.p, bbytes, hipMemcpyDeviceToHost, dv.stream));
-    HIP_TRY(c, hipEventRecord(dv.done, dv.stream));
   }
   c->fans.assign(fans, fans + fan_count);
   c->counted = count;
@@ -892,6 +939,8 @@ ART_API int art_last_test_counts(art_ctx* c, art_test_counts* out) {
 // ---------------------------------------------------------------------------- device-resident
 ART_API int art_scene_bind(art_ctx* c, const art_frame_desc* d) {
   if (!c) return ART_E_INVALID;
+  // the in-flight frame's art_complete reads c->fr and its H2D copy may still read c->h_in
+  if (c->inflight) return fail(c, ART_E_STATE, "art_scene_bind: a frame is in flight (bind after art_complete)");
   int rc = validate_desc(c, d);
   if (rc) return rc;
   rc = check_resident(c, d);
@@ -912,6 +961,7 @@ ART_API int art_scene_bind(art_ctx* c, const art_frame_desc* d) {
 static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, void* d_block, uint32_t out_flags,
                          void* stream, bool count, art_test_counts* out) {
   if (!c) return ART_E_INVALID;
+  if (c->inflight) return fail(c, ART_E_STATE, "a frame is in flight (launch after art_complete)");
   if (c->devs.empty() || !c->devs[0].bound) return fail(c, ART_E_STATE, "no scene bound (art_scene_bind)");
   if (fan_count < 0 || (fan_count > 0 && (!d_origins || !d_block))) return fail(c, ART_E_INVALID, "bad device buffers");
   Device& dv = c->devs[0];
@@ -929,6 +979,11 @@ static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, 
   if (f.resident && dv.st_done) HIP_TRY(c, hipStreamWaitEvent(st, dv.st_done, 0));
   int rc = enqueue_kernels(c, dv, f, d_origins, fan_count, static_cast<uint8_t*>(d_block), st, count);
   if (rc) return rc;
+  if (f.resident) {  // the next art_colliders_sync rewrites the records and refits in place: after this frame
+    if (!dv.launch_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.launch_done, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(dv.launch_done, st));
+    dv.launch_pending = true;
+  }
   if (count) return read_counts(c, dv, st, out, false);
   return ART_OK;
 }
@@ -1171,6 +1226,11 @@ ART_API int art_colliders_sync(art_ctx* c) {
     auto* oobb = reinterpret_cast<ObbRec*>(soa + s_obb);
     auto* oobbc = reinterpret_cast<ObbCold*>(soa + s_obbc);
     auto* cull = reinterpret_cast<CullRec*>(soa + s_cull);
+    // device-path frames on other streams still read the records / BVH being rewritten: wait for them
+    if (dv.launch_pending) {
+      HIP_TRY(c, hipStreamWaitEvent(dv.stream, dv.launch_done, 0));
+      dv.launch_pending = false;
+    }
     if (nd) {
       HIP_TRY(c, hipMemcpyAsync(up, h, bytes, hipMemcpyHostToDevice, dv.stream));
       launch_scatter_prep(reinterpret_cast<const int*>(up + off_idx[0]), reinterpret_cast<const art_sphere*>(up + off_rec[0]),

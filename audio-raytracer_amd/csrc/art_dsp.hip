@@ -315,13 +315,16 @@ int dsp_source_params(const art_spatializer_settings& st, const art_audio_source
   {  // BinauralDSP.cs:17-50, :65, :73
     const float* ld = src.local_dir;
     const float dist = src.listener_distance;
-    const float azimuth = std::atan2(ld[0], ld[2]) * kToDegrees;
+    // BinauralDSP.Process runs unbursted on the audio thread (no [BurstCompile] under Audio/), so
+    // Unity.Mathematics' atan2 / sin / cos are (float)System.Math.Atan2/Sin/Cos: double precision,
+    // rounded once to float.
+    const float azimuth = (float)std::atan2((double)ld[0], (double)ld[2]) * kToDegrees;
     float eps = st.pan_strength;
     if (st.distance_based_panning) eps *= usaturate(dist / st.max_pan_distance);
-    const float pan = std::sin(azimuth * kToRadians) * eps;
+    const float pan = (float)std::sin((double)(azimuth * kToRadians)) * eps;
     const float gl = std::sqrt(0.5f * (1.0f - pan));
     const float gr = std::sqrt(0.5f * (1.0f + pan));
-    const float front = umax(0.0f, std::cos(azimuth * kToRadians));
+    const float front = umax(0.0f, (float)std::cos((double)(azimuth * kToRadians)));
     float rear = ulerp(1.0f - st.rear_attenuation_strength, 1.0f, front);
     if (st.distance_based_rear_attenuation) {
       const float df = usaturate(1.0f - (dist / st.max_rear_attenuation_distance));

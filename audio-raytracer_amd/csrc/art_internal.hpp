@@ -162,6 +162,7 @@ void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout&
 // Bytes of the global visibility pair array the throughput kernel needs for this frame (0 when the
 // fused in-block visibility is built).
 size_t fast_pair_bytes(const FrameParams& fp);
+int fast_fans_per_launch(int R, int H, int T, uint32_t stride);
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,
                           uint32_t* pair_count, hipStream_t st);

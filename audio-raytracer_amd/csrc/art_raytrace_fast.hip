@@ -15,7 +15,8 @@
 // point into a small solid angle and their visibility sweeps end together; every output is
 // written at the ray's own index, so the order changes no result.
 // This kernel does not count tests; the test-count metric comes from raytrace_kernel<COUNT>.
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cstdlib>
 
 #include "art_device_fns.hpp"
 
@@ -2808,6 +2809,21 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
 }
 
 size_t fast_pair_bytes(const FrameParams& fp) { return ART_FAST_SPLIT ? pair_bufs(nullptr, fp).total : 0; }
+
+// Fans per launch_raytrace_fast call: pair slots (echo + muffle, R*H*(T+1) per fan) stay below
+// 2^31 (the sorted-visibility bound, u32 slots) and a fan's echo halves stay addressable with a
+// 32-bit half offset into the block (fan * stride / 2 < 2^32).
+int fast_fans_per_launch(int R, int H, int T, uint32_t stride) {
+  const unsigned long long per_fan = (unsigned long long)R * H * (T + 1) + 64;
+  const unsigned long long by_pairs = ((1ull << 31) - 64) / per_fan;
+  const unsigned long long by_block = ((1ull << 33) - 1) / (stride ? stride : 1) - 1;
+  unsigned long long n = std::min(std::min(by_pairs, by_block), (unsigned long long)(1 << 30));
+  if (const char* e = getenv("ART_FAST_CHUNK_FANS")) {  // test hook: force small chunks
+    const long long v = atoll(e);
+    if (v > 0) n = std::min(n, (unsigned long long)v);
+  }
+  return (int)std::max(1ull, n);
+}
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,

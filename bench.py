@@ -4,12 +4,15 @@
 Workload (N=1): BASELINE config 2 — 256 sources (fans) x 512 rays x 4096 colliders
 (2048 AABB + 2048 Sphere), T = 4 audio targets, maxBounces 0, stages raytrace + reduce.
 A "step" = one frame of the hot path over every fan of this rank, inputs resident in HBM,
-launched through the C ABI (art_launch_device) on torch's current HIP stream; with N > 1 each
-rank owns 256 fans (weak scaling) and the per-fan result blocks are all-gathered over RCCL.
+launched through the C ABI (art_launch_device) on torch's current HIP stream.
+Multi-GPU (one process per GPU, RCCL): config 2 runs weak (256 fans per rank); config 4 runs as
+BASELINE.json names it, strong: 1024 fans split contiguously over the G ranks (SURVEY.md §8 e);
+each step all-gathers the per-fan result blocks (art.dist.all_gather_fan_blocks).
 
-value = (tests executed by all ranks per frame, per the reference algorithm's counts) * K / max
-over ranks of the timed region. Test counts come from the counting variant of the kernels
-(art_count_device), which tests/test_parity_gpu.py checks against the oracle's counters.
+value = (tests the reference algorithm executes on all ranks' fans per frame) * K / max over ranks
+of the timed region: "equivalent ray-collider tests/s" — the kernels use an exact broad phase
+(BVH, culls) and execute far fewer tests (roofline.executed says how many). Test counts come from
+the counting kernel (art_count_device), which tests/test_parity_gpu.py checks against the oracle.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
 torch.distributed.run (one process per GPU, MASTER_ADDR=127.0.0.1).
@@ -38,13 +41,14 @@ CULL_OPS = {"cull_box": 14, "cull_cone": 35}
 OPS = {"rt_sphere": 26, "rt_aabb": 34, "rt_obb": 118, "perm_hit_sphere": 26, "perm_hit_aabb": 34, "perm_hit_obb": 134,
        "perm_loss_sphere": 18, "perm_loss_aabb": 33, "perm_loss_obb": 117}
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
+SINGLE_ISSUE_TLOPS = 39.3      # 256 CU x 64 lanes x 2.4 GHz, one non-FMA lane-op per cycle
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW" (spec)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--steps", type=int, default=0, help="timed steps (0 = enough for about 1.5 s)")
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", type=int, default=2)
     p.add_argument("--frames", type=int, default=50, help="host-API frames for the p50 frame latency")
@@ -53,7 +57,11 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--collider-scale", type=float, default=None,
                    help="scale the config's collider count (experiments only; the metric is quoted at 1)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU-baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum wall time of each CPU-baseline leg")
+    p.add_argument("--scaling", choices=("auto", "weak", "strong"), default="auto",
+                   help="N > 1: weak = cfg.S fans per rank; strong = cfg.S fans split over the ranks "
+                        "(auto: strong for config 4, as BASELINE.json names it, weak otherwise)")
+    p.add_argument("--no-dynamic", action="store_true", help="skip the dynamic-scene and rebuild measurements")
     p.add_argument("--path", choices=("raytrace", "dsp", "dirs"), default="raytrace",
                    help="raytrace: the headline metric; dsp: the per-sample spatializer DSP (SURVEY.md 8 f rank 1); "
                         "dirs: Fibonacci ray directions on the device (rank 3)")
@@ -65,25 +73,67 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(cfg, scene, params, org, fans, threads, min_seconds):
-    """The oracle (C restatement of the reference jobs) timed on this host's cores: whole frames
-    of `fans` fans, repeated until at least `min_seconds` of wall time (bounded sample)."""
+def host_cpu_info():
+    """The host cores this job may use: the affinity set, capped by the cgroup CPU quota (a GPU
+    box's share of a large machine: nproc shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    threads = min(aff, max(1, int(quota + 0.5))) if quota else aff
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota, "model": model,
+            "threads_used": threads}
+
+
+def cpu_leg(cfg, scene, params, org, threads, min_seconds):
+    """The oracle (C restatement of the reference jobs, oracle/art_oracle.c) timed on `threads`
+    host threads, one fan per task (TC = 1, as the shipped scene): batches of whole fans of this
+    config until at least `min_seconds` of wall time (a bounded sample; fans wrap around)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle  # CPU baseline leg only
 
-    sub = np.ascontiguousarray(org[:fans])
-    out = art.FanOutputs(fans, cfg.R, cfg.H, cfg.T, 1)
     oracle.load()
-    tests, frames = 0, 0
-    t0 = time.perf_counter()
-    while True:
-        _, counts = oracle.run(scene, params, sub, out, threads=threads)
+    S = org.shape[0]
+    tests, fans, dt, nxt, batch = 0, 0, 0.0, 0, max(1, min(threads, S))
+    while dt < min_seconds:
+        idx = (nxt + np.arange(batch)) % S
+        nxt = (nxt + batch) % S
+        out = art.FanOutputs(batch, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+        t0 = time.perf_counter()
+        _, counts = oracle.run(scene, params, np.ascontiguousarray(org[idx]), out, threads=threads)
+        dt += time.perf_counter() - t0
         tests += sum(counts.values())
-        frames += 1
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds or frames >= 100:
-            break
-    return tests / dt, dt, tests, frames
+        fans += batch
+        per_fan = dt / fans
+        want = int((min_seconds - dt) / per_fan) + 1
+        batch = max(1, min(S, -(-want // threads) * threads))
+    return {"value": tests / dt, "seconds": dt, "tests": tests, "fans": fans}
+
+
+def cpu_baseline(cfg, scene, params, org, min_seconds):
+    host = host_cpu_info()
+    n = host["threads_used"]
+    many = cpu_leg(cfg, scene, params, org, n, min_seconds)
+    one = cpu_leg(cfg, scene, params, org, 1, max(3.0, min_seconds / 2))
+    return {"value": many["value"], "unit": "ray-collider tests/s", "cores": n, "kind": "port",
+            "label": "reference algorithm (C restatement of the Burst jobs, oracle/art_oracle.c; Burst cannot run here)",
+            "sample": f"{many['fans']} fans of config {cfg.index} ({many['tests']} reference tests, {many['seconds']:.1f} s) "
+                      f"on {n} threads, one fan per task; gcc -O3 -march=x86-64-v3 -ffp-contract=off",
+            "one_thread": {"value": one["value"], "unit": "ray-collider tests/s",
+                           "sample": f"{one['fans']} fans ({one['tests']} tests, {one['seconds']:.1f} s) on 1 thread"},
+            "host": host}
 
 
 DSP_BYTES_PER_FRAME = 16     # one stereo frame read + written (8 B each way)
@@ -302,8 +352,113 @@ def main_dirs(a):
         "cpu_baseline": cpu}))
 
 
+def lib_sha256():
+    import hashlib
+    return hashlib.sha256(open(abi.LIB_PATH, "rb").read()).hexdigest()
+
+
+def read_traffic(cfg_index):
+    """HBM bytes per raytrace launch from the PMC pass (tools/pmc_traffic.sh, FETCH_SIZE and
+    WRITE_SIZE in separate passes) — used only when it was measured on this exact libart.so."""
+    prof = os.path.join(ROOT, "profiles", f"traffic_config{cfg_index}.json")
+    if not os.path.exists(prof):
+        return None, "no PMC traffic file for this config"
+    try:
+        t = json.load(open(prof))
+    except Exception as e:  # noqa: BLE001
+        return None, f"unreadable traffic file: {e}"
+    if t.get("lib_sha256") != lib_sha256():
+        return None, f"traffic file measured on another build ({str(t.get('lib_sha256'))[:12]}); not used"
+    return t.get("raytrace_bytes_per_launch"), f"PMC pass on this build (lib sha256 {t['lib_sha256'][:12]})"
+
+
+def jitter_records(rng, recs, scale):
+    """Moved copies of collider records: centres shifted by up to `scale` (half bits via float16)."""
+    out = recs.copy()
+    c = out["center"].view(np.float16).astype(np.float32)
+    c += rng.uniform(-scale, scale, c.shape).astype(np.float32)
+    out["center"] = c.astype(np.float16).view(np.uint16).reshape(out["center"].shape)
+    return out
+
+
+def dynamic_step(cfg, scene, params, org, S, steps, warmup, sp):
+    """Device step with a moving scene: per step 1 % of the colliders move (art_collider_set_many),
+    art_colliders_sync uploads only those, decodes them and refits the BVH / sorted copies in place,
+    then the frame runs on the resident scene (AudioColliderManager.UpdateJobBatch
+    Audio/AudioColliderManager.cs:115-122 -> NativeJobBatch.UpdateJobBatch NativeJobBatch.cs:36-50,
+    then the jobs). Also: a frame whose colliders all change (full upload, decode, BVH rebuild)."""
+    from art.colliders import ColliderStore, resident_frame
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rctx = art.Context(1 << torch.cuda.current_device())
+    store = ColliderStore(rctx)
+    fields = {abi.ART_KIND_SPHERE: scene.spheres, abi.ART_KIND_AABB: scene.aabbs, abi.ART_KIND_OBB: scene.obbs}
+    for k, arr in fields.items():
+        for i in range(arr.size):
+            store.add(k, arr[i])
+    store.sync()
+    rctx.set_flags(abi.ART_CTX_RESIDENT_COLLIDERS)
+    out = art.FanOutputs(S, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+    rframe = resident_frame(art.Frame(scene, params, org, out))
+    lay = art.fan_layout(rframe)
+    rctx.bind(rframe)
+    d_org = torch.from_numpy(np.ascontiguousarray(org)).to(dev)
+    d_blk = torch.zeros(S * lay["stride"], dtype=torch.uint8, device=dev)
+    rng = np.random.default_rng(7)
+    n_all = sum(x.size for x in fields.values())
+    variants = []
+    for v in range(8):  # pre-baked moved records (the caller's bake is not part of the step)
+        moves = {}
+        for k, arr in fields.items():
+            if arr.size:
+                ids = rng.choice(arr.size, max(1, arr.size // 100), replace=False).astype(np.int32)
+                moves[k] = (ids, jitter_records(rng, arr[ids], 0.05))
+        variants.append(moves)
+
+    def one(i):
+        for k, (ids, recs) in variants[i % len(variants)].items():
+            store.set_many(k, ids, recs)
+        store.sync()
+        rctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(i)
+    torch.cuda.synchronize()
+    dyn_ms = (time.perf_counter() - t0) / steps * 1e3
+    moved = int(sum(ids.size for ids, _ in variants[0].values()))
+    rctx.close()
+
+    # full rebuild: every collider changed each frame through the Unity-facing API (upload, decode,
+    # Morton sort, BVH build, frame, D2H)
+    ctx = art.Context(1 << torch.cuda.current_device())
+    scenes = []
+    for v in range(2):
+        sc = art.Scene(dirs=scene.dirs, targets=scene.targets, spheres=jitter_records(rng, scene.spheres, 0.05) if scene.spheres.size else scene.spheres,
+                       aabbs=jitter_records(rng, scene.aabbs, 0.05) if scene.aabbs.size else scene.aabbs,
+                       obbs=jitter_records(rng, scene.obbs, 0.05) if scene.obbs.size else scene.obbs)
+        scenes.append(art.Frame(sc, params, org, art.FanOutputs(S, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)))
+    ms = []
+    for i in range(25):
+        t1 = time.perf_counter()
+        ctx.run(scenes[i % 2])
+        if i >= 5:
+            ms.append((time.perf_counter() - t1) * 1e3)
+    ctx.close()
+    return {"ms_per_step_dynamic": dyn_ms, "moved_per_step": moved, "colliders": n_all,
+            "note": "device step incl. art_collider_set_many + art_colliders_sync (H2D of the moved records, decode, "
+                    "in-place BVH/sorted-copy refit) + art_launch_device, timed over the same K steps",
+            "p50_frame_ms_rebuild": statistics.median(ms),
+            "p50_frame_ms_rebuild_note": "art_schedule..art_complete with every collider changed each frame: full "
+                                         "H2D, record decode, Morton sort and BVH build, kernels, D2H"}
+
+
 def main():
     a = parse()
+    if a.path != "raytrace" and a.steps <= 0:
+        a.steps = 50
     if a.path == "dsp":
         return main_dsp(a)
     if a.path == "dirs":
@@ -321,46 +476,58 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     cfg = art.CONFIGS[a.config]
-    S_total = cfg.S * world
+    scaling = a.scaling if a.scaling != "auto" else ("strong" if cfg.index == 4 else "weak")
+    S_total = cfg.S if scaling == "strong" else cfg.S * world
     scene, org_all, params = art.synth(cfg, S=S_total, C_scale=a.collider_scale)
-    org = np.ascontiguousarray(org_all[rank * cfg.S:(rank + 1) * cfg.S])
-    S = cfg.S
+    b0, b1 = art.dist.shard_range(S_total, world, rank)
+    org = np.ascontiguousarray(org_all[b0:b1])
+    S = b1 - b0
     ctx = art.Context(1 << torch.cuda.current_device())
     out0 = art.FanOutputs(S, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
     frame = art.Frame(scene, params, org, out0)
     lay = art.fan_layout(frame)
     ctx.bind(frame)
     d_org = torch.from_numpy(org).to(dev)
-    d_blk = torch.zeros(S * lay["stride"], dtype=torch.uint8, device=dev)
+    d_blk = torch.zeros(max(S, 1) * lay["stride"], dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
     counts = ctx.count_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
     tests_rank = sum(counts.values())
-    rt_flops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
+    bf_ops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
 
     def step():
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
         if world > 1:
-            art.dist.all_gather_fan_blocks(d_blk, S_total, lay["stride"], world)
+            art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
 
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    steps = a.steps
+    if steps <= 0:  # about 1.5 s of timed work, so the driver's sampler sees the GPU busy
+        per = (time.perf_counter() - tw) / max(1, a.warmup)
+        steps = int(min(5000, max(20, 1.5 / max(per, 1e-6))))
+        if world > 1:
+            t = torch.tensor([steps], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            steps = int(t.item())
     ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
     ctx.kernel_timing()  # reset
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     ktimes = ctx.kernel_timing()
-    # work the kernel actually executed in one frame (broad phase: fewer exact tests than counted)
+    # work the kernels actually executed in one frame (broad phase: far fewer exact tests)
     ctx.set_flags(abi.ART_CTX_COUNT_EXECUTED)
     ctx.executed_counts()  # reset
     ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
@@ -386,38 +553,9 @@ def main():
             if i >= 5:
                 frame_ms.append((time.perf_counter() - t1) * 1e3)
 
-    # the same frames with the resident collider store (include/art_colliders.h): each frame moves
-    # 1 % of the colliders (art_collider_set), syncs (uploads only those), then runs the frame
-    frame_ms_res, sync_info = [], None
-    if rank == 0:
-        from art.colliders import KINDS, ColliderStore, resident_frame
-        rctx = art.Context(1 << torch.cuda.current_device())
-        store = ColliderStore(rctx)
-        fields = {abi.ART_KIND_SPHERE: scene.spheres, abi.ART_KIND_AABB: scene.aabbs, abi.ART_KIND_OBB: scene.obbs}
-        for k, arr in fields.items():
-            for i in range(arr.size):
-                store.add(k, arr[i])
-        store.sync()
-        rctx.set_flags(abi.ART_CTX_RESIDENT_COLLIDERS)
-        rframe = resident_frame(art.Frame(scene, params, org, art.FanOutputs(S, cfg.R, cfg.H, cfg.T, 1,
-                                                                             dsp=params.dsp is not None)))
-        rng = np.random.default_rng(5)
-        n_all = sum(x.size for x in fields.values())
-        moves = max(1, n_all // 100)
-        for i in range(a.frames + 5):
-            picks = {k: rng.integers(0, arr.size, max(1, moves * arr.size // n_all)).astype(np.int32)
-                     for k, arr in fields.items() if arr.size}
-            recs = {k: fields[k][ids] for k, ids in picks.items()}  # re-baked by the caller: same records here
-            t1 = time.perf_counter()
-            for k, ids in picks.items():
-                store.set_many(k, ids, recs[k])
-            st = store.sync()
-            rctx.run(rframe)
-            if i >= 5:
-                frame_ms_res.append((time.perf_counter() - t1) * 1e3)
-        sync_info = {"moved_per_frame": int(sum(v.size for v in picks.values())), "colliders": n_all, "last_sync": st,
-                     "collider_h2d_bytes_full_upload": int(sum(x.nbytes for x in fields.values()))}
-        rctx.close()
+    dyn = None
+    if rank == 0 and world == 1 and not a.no_dynamic:
+        dyn = dynamic_step(cfg, scene, params, org, S, steps, a.warmup, sp)
 
     if rank != 0:
         if world > 1:
@@ -426,72 +564,63 @@ def main():
 
     n_rt = max(1, ktimes["launches"])
     rt_ms = ktimes["raytrace_ms"] / n_rt
-    achieved_tflops = rt_flops / (rt_ms * 1e-3) / 1e12
+    bf_tflops = bf_ops / (rt_ms * 1e-3) / 1e12
     ex_launches = max(1, executed["launches"])
     ex_ops = (executed["sphere"] * OPS["rt_sphere"] + executed["aabb"] * OPS["rt_aabb"] + executed["obb"] * OPS["rt_obb"] +
               executed["cull_box"] * CULL_OPS["cull_box"] + executed["cull_cone"] * CULL_OPS["cull_cone"]) / ex_launches
     ex_tests = (executed["sphere"] + executed["aabb"] + executed["obb"]) / ex_launches
     ex_tflops = ex_ops / (rt_ms * 1e-3) / 1e12
-    # algorithmic HBM bytes of one raytrace launch: collider AoS->SoA records are L2-resident after
-    # the first wave, so the compulsory traffic is the SoA records + dirs + origins + outputs.
+    # algorithmic HBM bytes of one raytrace launch: the decoded collider records, directions,
+    # origins and the fans' result blocks (everything else is L2-resident scratch)
     rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 32 + scene.obbs.size * 64  # hot records
     alg_bytes = rec_bytes + cfg.R * 6 + S * 12 + S * lay["stride"]
     hbm_gbs = alg_bytes / (rt_ms * 1e-3) / 1e9
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", f"traffic_config{cfg.index}.json")
-    if os.path.exists(prof):
-        try:
-            traffic = json.load(open(prof)).get("raytrace_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_note = read_traffic(cfg.index)
 
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        fans = a.cpu_fans or S  # the full frame of this config (no extrapolation)
-        v, cdt, ctests, cframes = cpu_baseline(cfg, scene, params, org, fans, threads, a.cpu_seconds)
-        cpu = {"value": v, "unit": "ray-collider tests/s", "cores": threads, "kind": "port",
-               "sample": f"{cframes} frames x {fans} of {S} fans of config {cfg.index} ({ctests} tests, {cdt:.1f} s) "
-                         f"through the C oracle (oracle/art_oracle.c, gcc -O3 -ffp-contract=off), one fan per task"}
+        cpu = cpu_baseline(cfg, scene, params, org, a.cpu_seconds)
 
-    value = tests_all * a.steps / dt
+    value = tests_all * steps / dt
     res = {
         "metric": "ray-collider tests/sec + p50 per-frame batch ms, 256src\u00d7512ray\u00d74096col",  # BASELINE.json "metric"
         "value": value,
-        "unit": "ray-collider tests/s",
+        "unit": "equivalent ray-collider tests/s",
         "n_gpus": world,
-        "steps": a.steps,
+        "steps": steps,
         "warmup": a.warmup,
-        "ms_per_step": dt / a.steps * 1e3,
+        "ms_per_step": dt / steps * 1e3,
         "p50_frame_ms": statistics.median(frame_ms) if frame_ms else None,
         "p50_frame_ms_note": "art_schedule..art_complete on rank 0, host arrays, H2D + kernels + D2H (PCIe-inclusive)",
-        "p50_frame_ms_resident": statistics.median(frame_ms_res) if frame_ms_res else None,
-        "p50_frame_ms_resident_note": "same frame with the resident collider store: 1 % of the colliders moved "
-                                      "(art_collider_set_many) + art_colliders_sync + art_schedule..art_complete",
-        "resident_sync": sync_info,
+        "dynamic": dyn,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"config{cfg.index}: {cfg.description}", "fans_per_gpu": S, "rays": cfg.R,
-                   "colliders": cfg.C, "targets": cfg.T, "max_hits_per_ray": cfg.H, "tests_per_frame_per_gpu": tests_rank,
+        "config": {"workload": f"config{cfg.index}: {cfg.description}", "fans_total": S_total, "fans_rank0": S,
+                   "rays": cfg.R, "colliders": cfg.C, "targets": cfg.T, "max_hits_per_ray": cfg.H,
+                   "reference_tests_per_frame_rank0": tests_rank, "reference_tests_per_frame_all": tests_all,
                    "parallelism": f"fan-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
-        "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "raytrace stage: nearest_first_kernel + raytrace_fast_kernel + pair sort + vis_kernel + vis_finalize", "kernel_ms": rt_ms,
-                     "note": "FP32 VALU roof (no MFMA-shaped work). achieved = the reference algorithm's tests x ops per "
-                             "test (SURVEY.md 8(d)) per launch / kernel time: brute-force-equivalent, since the kernel's "
-                             "exact broad phase skips tests that cannot hit. 'executed' is the work the kernel did.",
-                     "executed": {"achieved": ex_tflops, "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS,
-                                  "ops_per_launch": ex_ops, "exact_lane_tests_per_launch": ex_tests,
-                                  "reference_tests_per_launch": tests_rank,
-                                  "counts": {k: v // ex_launches for k, v in executed.items() if k != "launches"},
-                                  "note": "lane-tests = wave-level tests x 64 (all lanes issue); broad-phase bound "
-                                          "tests at CULL_OPS ops each"},
+        "roofline": {"bound": "valu", "achieved": ex_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic, "traffic_note": traffic_note,
+                     "kernel": "raytrace stage: nearest_first_kernel + raytrace_fast_kernel + pair sort + vis_kernel + vis_finalize",
+                     "kernel_ms": rt_ms,
+                     "note": "FP32 VALU roof (no MFMA-shaped work). achieved = ops the kernels executed per launch (exact "
+                             "tests x SURVEY.md 8(d) ops per test, lane-tests = wave-level tests x 64, plus broad-phase "
+                             "bound tests at CULL_OPS) / raytrace-stage time (HIP events on the launch stream)",
+                     "single_issue": {"achieved": ex_ops / (rt_ms * 1e-3) / 1e12, "peak": SINGLE_ISSUE_TLOPS,
+                                      "unit": "T lane-op/s", "frac": ex_ops / (rt_ms * 1e-3) / 1e12 / SINGLE_ISSUE_TLOPS},
+                     "executed": {"ops_per_launch": ex_ops, "exact_lane_tests_per_launch": ex_tests,
+                                  "counts": {k: v // ex_launches for k, v in executed.items() if k != "launches"}},
+                     "equivalent": {"achieved": bf_tflops, "frac": bf_tflops / FP32_VALU_PEAK_TFLOPS,
+                                    "reference_tests_per_launch": tests_rank,
+                                    "note": "brute-force-equivalent: the reference algorithm's tests x ops per test / "
+                                            "stage time; the broad phase skips most of them, so this is not a roofline"},
                      "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
                              "algorithmic_bytes": alg_bytes}},
         "kernel_ms": {"raytrace": rt_ms, "permeate": ktimes["permeate_ms"] / n_rt, "reduce": ktimes["reduce_ms"] / n_rt},
+        "lib_sha256": lib_sha256(),
         "cpu_baseline": cpu,
     }
     print(json.dumps(res))

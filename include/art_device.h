@@ -90,6 +90,13 @@ ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);
 /* Sum of kernel times since the last call (needs ART_CTX_TIME_KERNELS); synchronizes. */
 ART_API int art_kernel_timing(art_ctx* ctx, art_kernel_times* out);
 
+/* Context over an explicit list of HIP devices: fans of every art_schedule are sharded
+ * contiguously over the list (one HIP stream, one scene copy and one set of buffers per entry).
+ * An id may repeat: art_create_on({0, 0, 0}, 3, &ctx) runs the in-process multi-device split and
+ * gather as three shards on three streams of device 0 (how the one-GPU tests exercise it).
+ * art_create(mask) is art_create_on over the mask's set bits. */
+ART_API int art_create_on(const int32_t* device_ids, int32_t count, art_ctx** out);
+
 /* Number of HIP devices visible (0 when none); never fails. */
 ART_API int art_device_count(void);
 

@@ -861,16 +861,18 @@ static void or_dsp_source(const art_spatializer_settings* st, art_audio_source* 
     {
         const float* ld = src->local_dir;
         float dist = src->listener_distance;
-        float azimuth = atan2f(ld[0], ld[2]) * OR_TODEGREES;                              /* :17 */
+        /* Unbursted managed code (BinauralDSP.cs has no [BurstCompile]): Unity.Mathematics' float
+         * atan2/sin/cos are (float)System.Math.Atan2/Sin/Cos, i.e. double precision rounded once. */
+        float azimuth = (float)atan2((double)ld[0], (double)ld[2]) * OR_TODEGREES;        /* :17 */
         float effectivePanStrength = st->pan_strength;                                    /* :19 */
         if (st->distance_based_panning) {                                                 /* :20-24 */
             float distanceFactor = usaturate(dist / st->max_pan_distance);
             effectivePanStrength *= distanceFactor;
         }
-        float pan = sinf(azimuth * OR_TORADIANS) * effectivePanStrength;                  /* :27 */
+        float pan = (float)sin((double)(azimuth * OR_TORADIANS)) * effectivePanStrength; /* :27 */
         float leftGain = sqrtf(0.5f * (1.0f - pan));                                      /* :28 */
         float rightGain = sqrtf(0.5f * (1.0f + pan));                                     /* :29 */
-        float frontFactor = umax(0.0f, cosf(azimuth * OR_TORADIANS));                     /* :32 */
+        float frontFactor = umax(0.0f, (float)cos((double)(azimuth * OR_TORADIANS)));    /* :32 */
         float rearAtten = ulerp(1.0f - st->rear_attenuation_strength, 1.0f, frontFactor); /* :33 */
         if (st->distance_based_rear_attenuation) {                                        /* :35-40 */
             float distanceFactor = usaturate(1.0f - (dist / st->max_rear_attenuation_distance));

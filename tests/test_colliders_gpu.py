@@ -241,6 +241,61 @@ def test_device_resident_path_follows_syncs(fresh_ctx):
         ref_ctx.close()
 
 
+def test_pipelined_device_frames_and_syncs(fresh_ctx):
+    """Device frames on the caller's stream and collider syncs issued back to back with no host
+    wait: each sync (record rewrite + in-place BVH refit on the context stream) must wait for the
+    frame before it, and each frame for the sync before it. Every frame's block must equal a frame
+    computed from its own collider snapshot."""
+    import torch
+    S, R = 64, 512
+    scene, org, params = art.synth(art.CONFIGS[2], S=S, R=R, C_scale=0.5)
+    store, model = ColliderStore(fresh_ctx), ListsModel()
+    load(store, model, scene)
+    store.sync()
+    model.synced()
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    fr = art.Frame(scene, params, org, art.FanOutputs(S, R, params.max_hits_per_ray, scene.T, params.thread_count))
+    lay = art.fan_layout(fr)
+    fresh_ctx.set_flags(abi.ART_CTX_RESIDENT_COLLIDERS)
+    snapshots, blocks = [], []
+    try:
+        fresh_ctx.bind(resident_frame(fr))
+        d_org = torch.from_numpy(np.ascontiguousarray(org)).to(dev)
+        st = torch.cuda.current_stream().cuda_stream
+        for rnd in range(6):
+            snapshots.append(scene_with(scene, model))
+            blk = torch.zeros(S * lay["stride"], dtype=torch.uint8, device=dev)
+            fresh_ctx.launch_device(d_org.data_ptr(), S, blk.data_ptr(), 0, st)
+            blocks.append(blk)
+            for k in KINDS:  # move a third of the colliders far (the refit changes many bounds)
+                arr = model.array(k)
+                if not arr.size:
+                    continue
+                ids = rng.choice(arr.size, max(1, arr.size // 3), replace=False)
+                recs = arr[ids].copy()
+                c = recs["center"].view(np.float16).astype(np.float32)
+                c += rng.uniform(-8, 8, c.shape).astype(np.float32)
+                recs["center"] = c.astype(np.float16).view(np.uint16).reshape(recs["center"].shape)
+                store.set_many(k, ids.astype(np.int32), recs)
+                for j, i in enumerate(ids):
+                    model.set(k, int(i), recs[j])
+            store.sync()
+            model.synced()
+        torch.cuda.synchronize()
+    finally:
+        fresh_ctx.set_flags(0)
+    ref_ctx = art.Context(1)
+    try:
+        for rnd, (snap, blk) in enumerate(zip(snapshots, blocks)):
+            out = art.FanOutputs(S, R, params.max_hits_per_ray, scene.T, params.thread_count)
+            ref_ctx.run(art.Frame(snap, params, org, out))
+            got = art.unpack_block(blk.cpu().numpy(), lay, S, R, params.max_hits_per_ray, scene.T, 1)
+            assert all(got.equal(out).values()), (rnd, got.equal(out))
+    finally:
+        ref_ctx.close()
+
+
 def test_errors_and_state(fresh_ctx):
     scene, org, params = art.synth(art.CONFIGS[2], S=2, R=64, C_scale=0.05)
     store = ColliderStore(fresh_ctx)

@@ -1,0 +1,141 @@
+"""The sharded paths on the HIP device (SURVEY.md §8 e): fans split over shards must give the same
+bytes as one shard.
+
+* In-process split (art_create_on): one context whose fans are sharded over several "devices" —
+  here N entries naming device 0, i.e. N streams, N scene copies and N result blocks on one GPU —
+  exactly the code path art_create(mask) takes on an 8-GPU node (per-device upload, enqueue,
+  D2H into the shared pinned block, completion over every device's event).
+* Multi-process split: world-2 gloo group whose ranks share device 0; each rank binds the scene and
+  computes its contiguous fan shard through libart's device entry point (art_launch_device), the
+  blocks are all-gathered (art.dist.all_gather_fan_blocks) and must equal the single-process
+  frame byte for byte. Reference: one fan = one AudioRayTracer job graph
+  (Audio/AudioRayTracer.cs:161-237); fans are independent.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import art
+from art import abi
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shards,ci,S", [(2, 5, 9), (3, 2, 16), (4, 1, 3)])
+def test_in_process_shards_on_one_device(ctx, shards, ci, S):
+    """art_create_on([0]*N): the multi-device split, one stream per shard, equals the single-device
+    context and the oracle; more shards than fans leaves some shards empty (S=3, N=4)."""
+    cfg = art.CONFIGS[ci]
+    scene, org, params = art.synth(cfg, S=S, R=128 if ci != 1 else 64, C_scale=0.1 if ci != 1 else None)
+    dsp = params.dsp is not None
+    hits = ci in (1, 5)
+    one = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, 1, hits=hits, dsp=dsp).fill_random(4)
+    many, ref = one.copy(), one.copy()
+    ctx.set_flags(0)
+    ctx.run(art.Frame(scene, params, org, one))
+    with art.Context(devices=[0] * shards) as mctx:
+        h = mctx.schedule(art.Frame(scene, params, org, many))
+        h.complete()
+        # a second frame through the same context (buffers and the cached device scenes reused)
+        again = one.copy()
+        mctx.run(art.Frame(scene, params, org, again))
+        # counting frames accumulate the per-shard test counts
+        cnt = one.copy()
+        mctx.set_flags(abi.ART_CTX_COUNT_TESTS)
+        mctx.run(art.Frame(scene, params, org, cnt))
+        counts = mctx.last_test_counts()
+    cref = oracle.run_frame(art.Frame(scene, params, org, ref), threads=16)
+    assert all(many.equal(ref).values()), many.equal(ref)
+    assert all(many.equal(one).values())
+    assert all(again.equal(ref).values())
+    assert all(cnt.equal(ref).values())
+    assert counts == cref
+
+
+def test_in_process_shards_thread_count_slots(ctx):
+    """TC > 1 (stale slots travel with the frame) through a 2-shard context."""
+    scene, org, params = art.synth(art.CONFIGS[1], S=5, R=64)
+    params.thread_count = 3
+    a = art.FanOutputs(5, 64, params.max_hits_per_ray, scene.T, 3, hits=True).fill_random(9)
+    ref = a.copy()
+    with art.Context(devices=[0, 0]) as mctx:
+        mctx.run(art.Frame(scene, params, org, a))
+    oracle.run_frame(art.Frame(scene, params, org, ref), threads=8)
+    assert all(a.equal(ref).values())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ci, S, R, cs, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "audio-raytracer_amd"))
+    import torch
+    import torch.distributed as dist
+    import art as A
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = A.CONFIGS[ci]
+        scene, org, params = A.synth(cfg, S=S, R=R, C_scale=cs)
+        b, e = A.dist.shard_range(S, world, rank)
+        shard = np.ascontiguousarray(org[b:e])
+        out = A.FanOutputs(max(e - b, 1), R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+        fr = A.Frame(scene, params, shard if e > b else org[:1], out)
+        lay = A.fan_layout(fr)
+        with A.Context(1) as c:
+            c.bind(fr)
+            d_org = torch.from_numpy(shard.copy() if e > b else np.zeros((1, 3), np.float32)).cuda()
+            d_blk = torch.zeros(max(e - b, 1) * lay["stride"], dtype=torch.uint8, device="cuda")
+            st = torch.cuda.current_stream()
+            c.launch_device(d_org.data_ptr(), e - b, d_blk.data_ptr(), 0, st.cuda_stream)
+            st.synchronize()
+            local = d_blk[: (e - b) * lay["stride"]].cpu()
+        full = A.dist.all_gather_fan_blocks(local, S, lay["stride"], world)
+        if rank == 0:
+            q.put(full.numpy().tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ci,S,R,cs", [(5, 9, 128, 0.1), (4, 6, 256, 1 / 16)])
+def test_world2_ranks_compute_shards_through_libart(ctx, ci, S, R, cs):
+    import torch.multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    world = 2
+    procs = [mpc.Process(target=_worker, args=(r, world, port, ci, S, R, cs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    cfg = art.CONFIGS[ci]
+    scene, org, params = art.synth(cfg, S=S, R=R, C_scale=cs)
+    out = art.FanOutputs(S, R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+    fr = art.Frame(scene, params, org, out)
+    ctx.set_flags(0)
+    ctx.run(fr)
+    ref = art.pack_block(out, art.fan_layout(fr))
+    lay = art.fan_layout(fr)
+    back = art.unpack_block(np.frombuffer(got, np.uint8), lay, S, R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+    assert all(back.equal(out).values()), back.equal(out)
+    # and against the oracle
+    o_ref = art.FanOutputs(S, R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
+    oracle.run_frame(art.Frame(scene, params, org, o_ref), threads=16)
+    assert all(out.equal(o_ref).values())
+    assert ref.size == len(got)

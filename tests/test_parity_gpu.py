@@ -164,14 +164,18 @@ def test_full_size_config2_sampled(ctx):
                                                                          out.settings[perm].view(np.uint8))
 
 
-@pytest.mark.parametrize("ci", [3, 5])
-def test_full_size_sampled(ctx, ci):
+@pytest.mark.parametrize("ci,every", [(3, 32), (5, 32), (4, 64)])
+def test_full_size_sampled(ctx, ci, every):
+    """Full-size configs through the host API, every `every`-th fan byte-compared with the oracle.
+    Config 4 (1024 fans x 1024 rays x 16384 mixed colliders: 16384 ray groups, 5.2 M visibility
+    pairs) is the launch shape the sharded bench runs per rank at G = 1."""
     cfg = art.CONFIGS[ci]
     scene, org, params = art.synth(cfg)
     dsp = params.dsp is not None
     out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1, dsp=dsp)
+    ctx.set_flags(0)
     ctx.run(art.Frame(scene, params, org, out))
-    sub = np.arange(0, cfg.S, 32)
+    sub = np.arange(0, cfg.S, every)
     ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1, dsp=dsp)
     oracle.run(scene, params, np.ascontiguousarray(org[sub]), ref, threads=16)
     for name in ("echo", "muffle", "perm", "settings") + (("dsp",) if dsp else ()):
@@ -296,3 +300,38 @@ def test_inputs_change_between_frames(ctx):
     scene.targets[:] = base_t
     c = check()                                       # back to the first frame's inputs
     assert all(c.equal(a).values()) and not all(b.equal(a).values())
+
+
+def test_fan_chunks_equal_one_launch(ctx, monkeypatch):
+    """Frames larger than the fast path's 32-bit pair / block offsets run as consecutive fan chunks
+    (fast_fans_per_launch); forcing 3-fan chunks must not change a byte (muffle accumulators,
+    pair counter reset per chunk, multi-hit ray state)."""
+    for ci in (2, 5):
+        scene, org, params = art.synth(art.CONFIGS[ci], S=11, R=128, C_scale=0.1)
+        a = art.FanOutputs(11, 128, params.max_hits_per_ray, scene.T, 1, hits=True, dsp=params.dsp is not None)
+        b = a.copy()
+        ctx.set_flags(0)
+        ctx.run(art.Frame(scene, params, org, a))
+        monkeypatch.setenv("ART_FAST_CHUNK_FANS", "3")
+        ctx.run(art.Frame(scene, params, org, b))
+        monkeypatch.delenv("ART_FAST_CHUNK_FANS")
+        assert all(a.equal(b).values()), a.equal(b)
+
+
+def test_bind_and_launch_refused_while_in_flight(ctx):
+    """art_scene_bind / art_launch_device between art_schedule and art_complete would overwrite the
+    in-flight frame's layout and staging: they return ART_E_STATE; the frame still completes."""
+    scene, org, params = art.synth(art.CONFIGS[1])
+    out = art.FanOutputs(8, 64, 5, 4, 1)
+    ref = out.copy()
+    fr = art.Frame(scene, params, org, out)
+    h = ctx.schedule(fr)
+    with pytest.raises(art.ArtError) as e:
+        ctx.bind(fr)
+    assert e.value.code == abi.ART_E_STATE
+    with pytest.raises(art.ArtError) as e:
+        ctx.launch_device(1, 1, 1)
+    assert e.value.code == abi.ART_E_STATE
+    h.complete()
+    oracle.run_frame(art.Frame(scene, params, org, ref), threads=8)
+    assert all(out.equal(ref).values())

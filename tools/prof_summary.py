@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Summarise one tools/gpu_round.sh output directory into profiles/ (committed evidence).
 
-  python tools/prof_summary.py gpurun_out/<tag> <tag>
+  python tools/prof_summary.py gpurun_out/<tag> <tag> [config]
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_pmc.csv            per-kernel mean of every PMC counter collected (one pass each)
   profiles/<tag>_bench.json         the bench line of the same round
-  profiles/traffic_config2.json     HBM bytes per raytrace launch from FETCH_SIZE / WRITE_SIZE,
-                                    corrected as MI355X_MICROARCH.md prescribes (bench.py reads it)
+  profiles/traffic_config<k>.json   HBM bytes per raytrace launch from FETCH_SIZE / WRITE_SIZE,
+                                    corrected as MI355X_MICROARCH.md prescribes, stamped with the
+                                    sha256 of the libart.so the passes ran (bench.py uses it only
+                                    for that same build)
 """
 import csv
 import glob
@@ -34,6 +36,9 @@ def short(name: str) -> str:
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    sha_f = os.path.join(src, "lib.sha256")
+    lib_sha = open(sha_f).read().split()[0] if os.path.exists(sha_f) else None
     os.makedirs(PROF, exist_ok=True)
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
@@ -84,9 +89,11 @@ def main():
             # wide read (64 B tallied per 128-B request) -> double it; WRITE_SIZE is exact.
             "raytrace_bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0,
             "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024; FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 note",
-            "source": f"profiles/{tag}_pmc.csv (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)",
+            "source": f"profiles/{tag}_pmc.csv (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --config {cfg})",
+            "config": cfg,
+            "lib_sha256": lib_sha,
         }
-        json.dump(rec, open(os.path.join(PROF, "traffic_config2.json"), "w"), indent=1)
+        json.dump(rec, open(os.path.join(PROF, f"traffic_config{cfg}.json"), "w"), indent=1)
         print(json.dumps(rec))
     for r in rows:
         print(f'{r["kernel"][:48]:48s} {r["counter"]:18s} {r["mean"]:.4g}')
