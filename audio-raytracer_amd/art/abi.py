@@ -48,11 +48,8 @@ ERROR_NAMES = {ART_E_INVALID: "ART_E_INVALID", ART_E_DEVICE: "ART_E_DEVICE", ART
 ART_CTX_COUNT_TESTS = 0x1
 ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
-ART_CTX_WAVEFRONT = 0x8
 ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
-ART_CTX_NO_BVH = 0x40
-ART_CTX_VIS_BVH = 0x80
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 

@@ -192,7 +192,7 @@ int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   sc.sph_s = sb.sph_s; sc.aabb_s = sb.aabb_s; sc.obb_s = sb.obb_s; sc.cull_s = sb.cull_s; sc.chunks = sb.chunks;
   sc.nchunks = nch;
   // the BVH reuses the key / value / temp buffers: stream order puts it after the gather above
-  return fast_uses_bvh() ? launch_build_bvh(sc, sb, st) : 0;
+  return launch_build_bvh(sc, sb, st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -309,9 +309,20 @@ __global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __r
   leaves[j] = u;
 }
 
-// Inner levels, bottom-up, in one workgroup (they hold a third of the leaf count).
-__global__ __launch_bounds__(1024) void bvh_upper_kernel(CullRec* __restrict__ nodes, int levels) {
-  for (int l = levels - 2; l >= 0; --l) {
+// One inner level l (large trees: levels with more nodes than one workgroup handles quickly).
+__global__ __launch_bounds__(256) void bvh_level_kernel(CullRec* __restrict__ nodes, int l) {
+  const int first = ((1 << (2 * l)) - 1) / 3, cnt = 1 << (2 * l);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= cnt) return;
+  const int g = first + i;
+  CullRec u = cull_empty();
+  for (int k = 1; k <= 4; ++k) cull_union(u, nodes[4 * g + k]);
+  nodes[g] = u;
+}
+
+// Inner levels top_level .. 0, bottom-up, in one workgroup (they hold a third of the leaf count).
+__global__ __launch_bounds__(1024) void bvh_upper_kernel(CullRec* __restrict__ nodes, int top_level) {
+  for (int l = top_level; l >= 0; --l) {
     const int first = ((1 << (2 * l)) - 1) / 3, cnt = 1 << (2 * l);
     for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
       const int g = first + i;
@@ -321,6 +332,14 @@ __global__ __launch_bounds__(1024) void bvh_upper_kernel(CullRec* __restrict__ n
     }
     __syncthreads();
   }
+}
+
+// Inner levels L-2 .. 0: levels of more than 4096 nodes one launch each, the rest in one workgroup.
+static void launch_bvh_upper(CullRec* nodes, int L, hipStream_t st) {
+  int l = L - 2;
+  for (; l >= 0 && (1 << (2 * l)) > 4096; --l)
+    hipLaunchKernelGGL(bvh_level_kernel, dim3(((1 << (2 * l)) + 255) / 256), dim3(256), 0, st, nodes, l);
+  if (l >= 0) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, nodes, l);
 }
 
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
@@ -337,7 +356,7 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   const int nleaf = total - leaf0;
   hipLaunchKernelGGL(bvh_leaf_kernel<false>, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, sb.perm, sc.ns, sc.na, n,
                      sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
-  if (L > 1) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, sb.bvh, L);
+  launch_bvh_upper(sb.bvh, L, st);
   sc.bvh = sb.bvh; sc.bvh_ref = sb.bvh_ref; sc.bvh_leaf = sb.bvh_leaf; sc.bvh_levels = L; sc.bvh_leaf0 = leaf0;
   return 0;
 }
@@ -357,7 +376,7 @@ int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
     const int leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1;  // 4^(L-1) leaves
     hipLaunchKernelGGL(bvh_leaf_kernel<true>, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, (const int*)nullptr,
                        sc.ns, sc.na, n, sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
-    if (sc.bvh_levels > 1) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, sb.bvh, sc.bvh_levels);
+    launch_bvh_upper(sb.bvh, sc.bvh_levels, st);
   }
   return 0;
 }

@@ -24,7 +24,6 @@
 #include "../../include/art_dsp.h"
 #include "../../include/art_colliders.h"
 #include "art_internal.hpp"
-#include "art_wavefront.hpp"
 #include "unity_math.hpp"
 
 #include <cmath>
@@ -101,7 +100,6 @@ struct Device {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
-  DevBuf work;  // ticket counters of the persistent raytrace kernel (self-rearming, zeroed once)
   DevBuf exec;  // executed-work counters (ART_CTX_COUNT_EXECUTED)
   DevBuf pairs; // global visibility pairs of the split raytrace path
   DevBuf dsp;   // per-sample DSP batch (art_dsp_process): samples, offsets, frames, params, states
@@ -115,8 +113,6 @@ struct Device {
   hipEvent_t launch_done = nullptr;  // after the last art_launch_device frame (caller's stream)
   bool launch_pending = false;       // a sync must wait for it before rewriting records / BVH
   uint64_t exec_launches = 0;
-  DevBuf wf_rays, wf_alive, wf_items, wf_flags, wf_cnt;  // wavefront pipeline scratch
-  int wf_blocks = 0;
   int fan_begin = 0, fan_count = 0;
   DevScene sc{};
   SortBufs sb{};  // buffers of the spatially sorted scene copy (art_bvh.hip), set by upload_scene
@@ -209,6 +205,8 @@ int validate_desc(art_ctx* c, const art_frame_desc* d) {
   if ((long long)d->ray_count * d->max_hits_per_ray > (1 << 24)) return fail(c, ART_E_UNSUPPORTED, "R*H > 2^24");
   if (d->batch_size <= 0 || d->batch_slots <= 0) return fail(c, ART_E_INVALID, "batch_size and batch_slots must be > 0");
   if (d->aabb_count < 0 || d->obb_count < 0 || d->sphere_count < 0) return fail(c, ART_E_INVALID, "negative collider count");
+  if ((long long)d->aabb_count + d->obb_count + d->sphere_count > kMaxColliders)
+    return fail(c, ART_E_UNSUPPORTED, "more than %lld colliders", kMaxColliders);
   if ((d->aabb_count && !d->aabb_colliders) || (d->obb_count && !d->obb_colliders) || (d->sphere_count && !d->sphere_colliders))
     return fail(c, ART_E_INVALID, "collider pointer is NULL with a non-zero count");
   if (d->stages & ~ART_STAGE_ALL) return fail(c, ART_E_INVALID, "unknown stage bits");
@@ -441,7 +439,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sc.sph_s = nullptr; sc.aabb_s = nullptr; sc.obb_s = nullptr; sc.cull_s = nullptr; sc.chunks = nullptr; sc.nchunks = 0;
   sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
   dv.sb = sb;
-  if (fast_uses_sorted_scene()) {
+  {
     const bool reuse = f.resident && dv.sorted_gen != ~0ull && dv.sorted_soa == dv.soa.p && dv.sorted_n[0] == f.ns &&
                        dv.sorted_n[1] == f.na && dv.sorted_n[2] == f.no;
     if (reuse) {  // same resident colliders (or only moved ones): keep the orders, refit if needed
@@ -504,42 +502,6 @@ int check_resident(art_ctx* c, const art_frame_desc* d) {
   return ART_OK;
 }
 
-// Throughput raytrace implementation: the single-launch K-way block kernel (default, targets up
-// to fast_max_targets()) or the per-bounce wavefront pipeline (targets up to 31; selected for all
-// target counts with ART_RAYTRACE_KERNEL=wavefront, for comparisons).
-bool use_block_kernel() {
-  static const int v = [] {
-    const char* e = getenv("ART_RAYTRACE_KERNEL");
-    return (e && strcmp(e, "wavefront") == 0) ? 0 : 1;
-  }();
-  return v == 1;
-}
-
-int enqueue_wavefront(art_ctx* c, Device& dv, const Frame& f, const FrameParams& fp, const float* d_origins, int fan_count,
-                      uint8_t* d_block, uint32_t* acc, const int* ray_order, hipStream_t st) {
-  const size_t nr = (size_t)fan_count * f.R, Q = (size_t)f.T + 1;
-  if (nr * Q >= (1ull << 32)) return fail(c, ART_E_UNSUPPORTED, "fans * rays * (targets + 1) >= 2^32");
-  if (!dv.wf_rays.reserve(nr * sizeof(WfRay)) || !dv.wf_alive.reserve(2 * nr * 4) || !dv.wf_items.reserve(nr * Q * sizeof(WfItem)) ||
-      !dv.wf_flags.reserve(nr * Q) || !dv.wf_cnt.reserve((size_t)(f.H + 1) * sizeof(WfCounters)))
-    return fail(c, ART_E_NOMEM, "device allocation failed");
-  if (dv.wf_blocks == 0) dv.wf_blocks = wf_persistent_blocks();
-  HIP_TRY(c, hipMemsetAsync(dv.wf_cnt.p, 0, (size_t)(f.H + 1) * sizeof(WfCounters), st));
-  HIP_TRY(c, hipMemsetAsync(dv.wf_flags.p, 0, nr * Q, st));
-  WfArgs a{};
-  a.origins = d_origins;
-  a.block = d_block;
-  a.muffle_acc = acc;
-  a.ray_order = ray_order;
-  a.rays = static_cast<WfRay*>(dv.wf_rays.p);
-  a.alive[0] = static_cast<uint32_t*>(dv.wf_alive.p);
-  a.alive[1] = a.alive[0] + nr;
-  a.items = static_cast<WfItem*>(dv.wf_items.p);
-  a.flags = static_cast<uint8_t*>(dv.wf_flags.p);
-  a.cnt = static_cast<WfCounters*>(dv.wf_cnt.p);
-  for (int b = 0; b < f.H; ++b) wf_launch_bounce(dv.sc, fp, f.L, a, b, kWfParts, dv.wf_blocks, st);
-  return ART_OK;
-}
-
 hipEvent_t pool_event(Device& dv, size_t i) {
   while (dv.ev_pool.size() <= i) {
     hipEvent_t e;
@@ -593,11 +555,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     const int* order = reinterpret_cast<const int*>(raw + f.off_order);
     if (count || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER)) {
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
-    } else if (use_block_kernel() && !(c->flags & ART_CTX_WAVEFRONT) && f.T <= fast_max_targets()) {
-      if (!dv.work.p) {
-        if (!dv.work.reserve(256)) return fail(c, ART_E_NOMEM, "device allocation failed");
-        HIP_TRY(c, hipMemsetAsync(dv.work.p, 0, 256, st));
-      }
+    } else {
       FrameParams fpx = fp;
       fpx.exec = nullptr;
       if (c->flags & ART_CTX_COUNT_EXECUTED) {
@@ -615,22 +573,13 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       FrameParams fps = fpx;
       fps.S = std::min(fan_count, chunk);
       if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
-      DevScene scx = dv.sc;
-      if (c->flags & ART_CTX_NO_BVH) scx.bvh_levels = 0;  // cone / K-way split path
-      fpx.vis_bvh = (c->flags & ART_CTX_VIS_BVH) ? 1 : 0;
       for (int b0 = 0; b0 < fan_count; b0 += chunk) {
         FrameParams fpc = fpx;
         fpc.S = std::min(chunk, fan_count - b0);
         if (b0) HIP_TRY(c, hipMemsetAsync(pair_count, 0, 16, st));
-        launch_raytrace_fast(scx, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
-                             acc + (size_t)b0 * f.TC * f.T, order, static_cast<uint32_t*>(dv.work.p), dv.pairs.p, pair_count,
-                             st);
+        launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
+                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st);
       }
-    } else if (f.T <= 31) {
-      int rc = enqueue_wavefront(c, dv, f, fp, d_origins, fan_count, d_block, acc, order, st);
-      if (rc) return rc;
-    } else {
-      launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
     }
     if (timing) tstop(ti);
     HIP_TRY(c, hipGetLastError());
@@ -764,11 +713,10 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
-    dv.work.release(); dv.exec.release(); dv.pairs.release(); dv.dsp.release();
+    dv.exec.release(); dv.pairs.release(); dv.dsp.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
     if (dv.st_done) (void)hipEventDestroy(dv.st_done);
     if (dv.launch_done) (void)hipEventDestroy(dv.launch_done);
-    dv.wf_rays.release(); dv.wf_alive.release(); dv.wf_items.release(); dv.wf_flags.release(); dv.wf_cnt.release();
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
@@ -1144,6 +1092,8 @@ ART_API int art_colliders_sync(art_ctx* c) {
   if (!c) return ART_E_INVALID;
   if (c->inflight) return fail(c, ART_E_STATE, "art_colliders_sync: a frame is in flight (sync after art_complete)");
   const int n[3] = {c->kinds[0].count, c->kinds[1].count, c->kinds[2].count};
+  if ((long long)n[0] + n[1] + n[2] > kMaxColliders)
+    return fail(c, ART_E_UNSUPPORTED, "art_colliders_sync: more than %lld colliders", kMaxColliders);
   bool counts_changed = !c->store_synced;
   for (int k = 0; k < 3; ++k) counts_changed |= n[k] != c->synced[k];
   // device capacity: grow (x2) and re-upload everything when a list outgrows it
@@ -1257,7 +1207,7 @@ ART_API int art_colliders_sync(art_ctx* c) {
     t.cull = cull;
     dv.st_fresh = false;
     if (dv.bound && c->fr.resident) {  // a bound device-resident scene sees the new snapshot
-      if (fast_uses_sorted_scene() && counts_changed) {
+      if (counts_changed) {
         dv.bound = false;  // the sorted copies are sized by count: bind again
       } else {
         dv.sc.sph = t.sph; dv.sc.sphc = t.sphc; dv.sc.ns = t.ns;
@@ -1265,7 +1215,7 @@ ART_API int art_colliders_sync(art_ctx* c) {
         dv.sc.obb = t.obb; dv.sc.obbc = t.obbc; dv.sc.no = t.no;
         dv.sc.cull = t.cull;
         // moved colliders: refit the sorted copies and the BVH in place (device only, no H2D)
-        if (fast_uses_sorted_scene() && nd) {
+        if (nd) {
           if (launch_refit_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider refit failed");
           if (dv.sorted_gen != ~0ull) dv.sorted_gen = c->sync_gen;
           HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));  // device-path launches wait for the sort too

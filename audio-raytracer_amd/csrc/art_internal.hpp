@@ -89,9 +89,10 @@ struct DevScene {
   int bvh_levels;                 // 0: no BVH
   int bvh_leaf0;
 };
-constexpr int kBvhLeaf = 4;       // colliders per leaf
-constexpr int kBvhMaxLevels = 8;  // <= 4 * 4^7 colliders; node ids fit the u16 traversal stack
-constexpr int kBvhStack = 3 * (kBvhMaxLevels - 1);
+constexpr int kBvhLeaf = 4;        // colliders per leaf
+constexpr int kBvhMaxLevels = 12;  // up to kBvhLeaf * 4^11 = 2^24 colliders per scene
+constexpr int kBvhStack = 3 * (kBvhMaxLevels - 1);  // u32 node ids per traversal stack
+constexpr long long kMaxColliders = (long long)kBvhLeaf << (2 * (kBvhMaxLevels - 1));
 
 struct SortBufs {
   float* box;                     // 6 floats
@@ -108,11 +109,10 @@ void launch_dsp(float* data, unsigned long long data_bytes, const long long* off
                 int frames_all, const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st);
 
 size_t sort_scene_temp_bytes(int n);
-bool fast_uses_sorted_scene();  // whether the throughput kernel reads the sorted copies (or the BVH)
-bool fast_uses_bvh();           // whether launch_sort_scene also builds the BVH
+// Spatially sorted copies, chunk bounds and the BVH (art_bvh.hip), built per upload.
 int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
-// Node count of the BVH over n colliders (0 when n is 0 or too large for the u16 stack), and its
-// build (after launch_sort_scene's buffers are free again; same stream).
+// Node count of the BVH over n colliders (0 when n is 0 or above kMaxColliders), and its build
+// (after launch_sort_scene's buffers are free again; same stream).
 size_t bvh_node_count(int n);
 size_t bvh_slot_count(int n);
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
@@ -139,7 +139,6 @@ struct FrameParams {
   const float* muf_curve; int muf_n; float muf_len;
   int sample_rate;
   unsigned long long* exec;  // executed-work counters (ExecSlot order) or nullptr
-  int vis_bvh;               // ART_CTX_VIS_BVH: visibility by per-lane BVH traversal
 };
 
 // Slots of FrameParams::exec (art_exec_counts order).
@@ -159,15 +158,15 @@ void launch_scatter_prep(const int* idx_s, const art_sphere* rec_s, int ds, cons
                          AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc, CullRec* cull, hipStream_t st);
 void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, uint32_t* muffle_acc, DevCounts* counts, hipStream_t st);
-// Bytes of the global visibility pair array the throughput kernel needs for this frame (0 when the
-// fused in-block visibility is built).
+// Bytes of the visibility pair buffer of launch_raytrace_fast for this frame (fp.S fans).
 size_t fast_pair_bytes(const FrameParams& fp);
+// Fans per launch_raytrace_fast call (32-bit pair slots and block offsets).
 int fast_fans_per_launch(int R, int H, int T, uint32_t stride);
+// The throughput raytrace stage (art_trace.hip): per bounce nearest_first_kernel + path_kernel,
+// then the pair sort, vis_kernel and vis_finalize. Any target count, every DevScene with a BVH.
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, uint32_t* work, void* pair_buf,
+                          uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf,
                           uint32_t* pair_count, hipStream_t st);
-int fast_split(int S, int R);
-int fast_max_targets();
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, const int2* slot_batch, hipStream_t st);
 void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,

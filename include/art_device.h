@@ -40,17 +40,11 @@ typedef struct {
 
 /* Record hipEvents around every kernel of art_launch_device (art_set_flags). */
 #define ART_CTX_TIME_KERNELS 0x2u
-/* Use the reference-order (one ray per lane) raytrace kernel instead of the K-way split one. */
+/* Frame outputs from the reference-order raytrace kernel (one ray per lane, every collider in
+ * reference order; the kernel the test counts come from) instead of the throughput stage. */
 #define ART_CTX_FORCE_REFERENCE_ORDER 0x4u
-/* Use the per-bounce wavefront pipeline (nearest / compacted visibility queue / finalize) for
- * frames with up to 31 targets instead of the single-launch K-way block kernel. */
-#define ART_CTX_WAVEFRONT 0x8u
-/* Throughput kernel without the collider BVH: first-segment nearest hits by the shared-origin cone
- * over a K-way collider split, later bounces by brute force (the pre-BVH path; A/B and tests). */
-#define ART_CTX_NO_BVH 0x40u
-/* Visibility pairs by per-lane BVH any-hit traversal (vis_bvh_kernel) instead of the sorted-batch
- * chunk sweep (vis_kernel). Same results; slower on the configs measured. */
-#define ART_CTX_VIS_BVH 0x80u
+/* (0x8, 0x40 and 0x80 selected round-1 alternative raytrace implementations; they are gone and
+ * the bits are reserved.) */
 
 ART_API int art_fan_layout_get(const art_frame_desc* desc, uint32_t out_flags, art_fan_layout* out);
 

@@ -5,7 +5,7 @@ by a rounding margin (broad phase). A wrong margin can only show 
 reference's float tests report hits that the true geometry does not have: grazing rays on tiny
 or far spheres, rays in the plane of a box face, huge coordinates, degenerate and non-finite
 colliders. Every scene here is compared bit for bit with the brute-force oracle, through the
-block kernel, the wavefront pipeline and the reference-order kernel (gpu_vs_oracle).
+throughput stage and the reference-order kernel (gpu_vs_oracle).
 """
 import numpy as np
 import pytest

@@ -32,12 +32,12 @@ def _diff_report(a: art.FanOutputs, b: art.FanOutputs) -> str:
     return "\n".join(lines)
 
 
-def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True, wavefront=True):
-    """Run the frame through every raytrace implementation — the throughput path kernel (BVH
-    nearest hits, sorted-batch visibility), the same with BVH visibility (ART_CTX_VIS_BVH) and
-    without the BVH (ART_CTX_NO_BVH: shared-origin cone, K-way split), the wavefront pipeline
-    (ART_CTX_WAVEFRONT) and the reference-order counting kernel — and require each to equal the
-    oracle bit for bit; the counting run's test counts must equal the oracle's."""
+def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True):
+    """Run the frame through both raytrace implementations — the throughput stage (BVH nearest
+    hits, sorted-batch visibility; art_trace.hip) and the reference-order kernel (one ray per lane,
+    every collider in reference order; its counting variant gives the metric's test counts) — and
+    require each to equal the oracle bit for bit; the counting run's test counts must equal the
+    oracle's."""
     S = org.shape[0]
     o_gpu = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, params.thread_count, hits=hits,
                            dsp=params.dsp is not None)
@@ -45,25 +45,17 @@ def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True, 
         o_gpu.fill_random(stale)
     o_ref = o_gpu.copy()
     o_cnt = o_gpu.copy()
+    o_ro = o_gpu.copy()
     cref = oracle.run_frame(art.Frame(scene, params, org, o_ref), threads=16)
     ctx.set_flags(0)
     ctx.run(art.Frame(scene, params, org, o_gpu))
     eq = o_gpu.equal(o_ref)
-    assert all(eq.values()), f"fast kernel: {eq}\n{_diff_report(o_gpu, o_ref)}"
-    for flag, name in ((abi.ART_CTX_VIS_BVH, "BVH visibility"), (abi.ART_CTX_NO_BVH, "no-BVH kernel")):
-        o_v = o_cnt.copy()
-        ctx.set_flags(flag)
-        ctx.run(art.Frame(scene, params, org, o_v))
-        ctx.set_flags(0)
-        eq = o_v.equal(o_ref)
-        assert all(eq.values()), f"{name}: {eq}\n{_diff_report(o_v, o_ref)}"
-    if wavefront:
-        o_wf = o_cnt.copy()
-        ctx.set_flags(abi.ART_CTX_WAVEFRONT)
-        ctx.run(art.Frame(scene, params, org, o_wf))
-        ctx.set_flags(0)
-        eq = o_wf.equal(o_ref)
-        assert all(eq.values()), f"wavefront pipeline: {eq}\n{_diff_report(o_wf, o_ref)}"
+    assert all(eq.values()), f"throughput stage: {eq}\n{_diff_report(o_gpu, o_ref)}"
+    ctx.set_flags(abi.ART_CTX_FORCE_REFERENCE_ORDER)
+    ctx.run(art.Frame(scene, params, org, o_ro))
+    ctx.set_flags(0)
+    eq = o_ro.equal(o_ref)
+    assert all(eq.values()), f"reference-order kernel: {eq}\n{_diff_report(o_ro, o_ref)}"
     if counts:
         ctx.set_flags(abi.ART_CTX_COUNT_TESTS)
         ctx.run(art.Frame(scene, params, org, o_cnt))
@@ -138,6 +130,23 @@ def test_one_target_many_targets(ctx):
     many = art.Scene(dirs=scene.dirs, targets=rng.uniform(-10, 10, (37, 3)).astype(np.float32), spheres=scene.spheres,
                      aabbs=scene.aabbs, obbs=scene.obbs)
     gpu_vs_oracle(ctx, many, params, org)
+
+
+@pytest.mark.parametrize("T", [8, 12, 31, 64, 256])
+def test_many_targets_fast_path(ctx, T):
+    """The throughput path takes any target count (pair emission in rounds of 8 queries, coarser
+    direction cells in the muffle sort key above 8 targets); AudioRaytracerJobBatched.cs:153 loops
+    over every target. Multi-hit config-5 scene with permeation and DSP params; targets spread over
+    the scene and owning colliders of every kind."""
+    scene, org, params = art.synth(art.CONFIGS[5], S=4, R=128, C_scale=0.1)
+    rng = np.random.default_rng(T)
+    tg = rng.uniform(-20, 20, (T, 3)).astype(np.float32)
+    sc = art.Scene(dirs=scene.dirs, targets=tg, spheres=scene.spheres.copy(), aabbs=scene.aabbs.copy(),
+                   obbs=scene.obbs.copy())
+    for arr in (sc.spheres, sc.aabbs, sc.obbs):
+        arr["audio_target_id"] = rng.integers(-1, T, arr.size).astype(np.int16)
+    out, _ = gpu_vs_oracle(ctx, sc, params, org, hits=True, counts=(T <= 64))
+    assert (out.muffle != 0).any()
 
 
 def test_full_size_config2_sampled(ctx):
@@ -335,3 +344,13 @@ def test_bind_and_launch_refused_while_in_flight(ctx):
     h.complete()
     oracle.run_frame(art.Frame(scene, params, org, ref), threads=8)
     assert all(out.equal(ref).values())
+
+
+def test_deep_bvh_large_scene(ctx):
+    """122,880 colliders: a 9-level BVH (87,381 nodes, past the old 16-bit traversal stacks) built
+    level by level; nearest hits, echo traversal and the muffle sweep against the oracle."""
+    scene, org, params = art.synth(art.CONFIGS[5], S=3, R=128, C_scale=30)
+    params.max_hits_per_ray = 3
+    assert scene.C > 4 * 4 ** 7
+    out, _ = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
+    assert (out.echo != 0).any()

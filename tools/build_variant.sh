@@ -9,7 +9,7 @@ pkg=$root/audio-raytracer_amd
 tmp=$(mktemp -d)
 mkdir -p "$root/variants"
 flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden "$@")
-for f in art_kernels art_raytrace_fast art_wavefront art_bvh art_dsp; do
+for f in art_kernels art_trace art_bvh art_dsp; do
   hipcc "${flags[@]}" -c "$pkg/csrc/$f.hip" -o "$tmp/$f.o" &
 done
 hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_capi.cpp" -o "$tmp/art_capi.o" &
