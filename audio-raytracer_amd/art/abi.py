@@ -206,6 +206,8 @@ SIGNATURES = {
     "art_fibonacci_directions": (None, [I32, VP]),
     "art_f32tof16": (C.c_uint16, [C.c_float]),
     "art_f16tof32": (C.c_float, [C.c_uint16]),
+    "art_f32tof16_range": (None, [U32, U32, VP]),
+    "art_f32tof16_device": (I32, [VP, U32, U32, VP, VP]),
 }
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -957,6 +957,15 @@ ART_API int art_fibonacci_directions_device(art_ctx* c, int32_t count, art_half3
   return ART_OK;
 }
 
+ART_API int art_f32tof16_device(art_ctx* c, uint32_t first_bits, uint32_t count, uint16_t* d_out, void* stream) {
+  if (!c) return ART_E_INVALID;
+  if (count > 0 && !d_out) return fail(c, ART_E_INVALID, "art_f32tof16_device: d_out is NULL");
+  HIP_TRY(c, hipSetDevice(c->devs[0].id));
+  launch_half_range(first_bits, count, d_out, static_cast<hipStream_t>(stream));
+  HIP_TRY(c, hipGetLastError());
+  return ART_OK;
+}
+
 ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
   if (!c || !out) return ART_E_INVALID;
   memset(out, 0, sizeof *out);

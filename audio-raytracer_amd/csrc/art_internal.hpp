@@ -152,6 +152,7 @@ void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, co
                  SphereRec* osph, SphereCold* osphc, AabbRec* oaabb, AabbCold* oaabbc, ObbRec* oobb, ObbCold* oobbc,
                  CullRec* cull, hipStream_t st);
 void launch_fibonacci(int count, art_half3* out, hipStream_t st);
+void launch_half_range(uint32_t first, uint32_t count, uint16_t* out, hipStream_t st);
 void launch_scatter_prep(const int* idx_s, const art_sphere* rec_s, int ds, const int* idx_a, const art_aabb* rec_a,
                          int da, const int* idx_o, const art_obb* rec_o, int dob, art_sphere* sph, art_aabb* aabb,
                          art_obb* obb, int ns, int na, SphereRec* osph, SphereCold* osphc, AabbRec* oaabb,

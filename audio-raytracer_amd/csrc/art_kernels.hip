@@ -630,6 +630,17 @@ __global__ void fibonacci_kernel(int count, art_half3* __restrict__ out) {
   out[i] = h;
 }
 
+__global__ void half_range_kernel(uint32_t first, uint32_t count, uint16_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  out[i] = f32tof16(asfloat(first + i));
+}
+
+void launch_half_range(uint32_t first, uint32_t count, uint16_t* out, hipStream_t st) {
+  if (count == 0) return;
+  hipLaunchKernelGGL(half_range_kernel, dim3((count + 255u) / 256u), dim3(256), 0, st, first, count, out);
+}
+
 void launch_fibonacci(int count, art_half3* out, hipStream_t st) {
   if (count <= 0) return;
   hipLaunchKernelGGL(fibonacci_kernel, dim3((count + 255) / 256), dim3(256), 0, st, count, out);

@@ -63,6 +63,9 @@ extern "C" {
 
 ART_API uint16_t art_f32tof16(float x) { return f32tof16(x); }
 ART_API float art_f16tof32(uint16_t h) { return f16tof32(h); }
+ART_API void art_f32tof16_range(uint32_t first_bits, uint32_t count, uint16_t* out) {
+  for (uint32_t i = 0; i < count; ++i) out[i] = f32tof16(asfloat(first_bits + i));
+}
 
 // FibonacciDirectionsJobParallel.Execute (Jobs/FibonacciDirectionsJobParallel.cs:15-35). cos/sin are
 // evaluated in double and rounded to float (the correctly rounded float values), exactly as

@@ -64,6 +64,12 @@ ART_API int art_launch_device(art_ctx* ctx, const float* d_origins, int32_t fan_
  * for bit; directions stay an input of art_frame_desc (the half3 bits are the contract). */
 ART_API int art_fibonacci_directions_device(art_ctx* ctx, int32_t count, art_half3* d_out, void* stream);
 
+/* The kernels' f32tof16 (Utility/HalfDataTypesUtility.cs:86-90 -> Unity.Mathematics math.f32tof16)
+ * over the float bit patterns first_bits .. first_bits + count - 1 (wrapping), into d_out (HBM,
+ * u16[count]) on `stream`: the device conversion every echo, hit point and direction goes through,
+ * exposed so it can be checked against the host and the oracle over all 2^32 inputs. */
+ART_API int art_f32tof16_device(art_ctx* ctx, uint32_t first_bits, uint32_t count, uint16_t* d_out, void* stream);
+
 /* Same frame with the test-counting kernels (for the tests/s metric); synchronizes. */
 ART_API int art_count_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
                              uint32_t out_flags, void* stream, art_test_counts* out);

@@ -39,6 +39,9 @@ ART_API void art_fibonacci_directions(int32_t count, art_half3* out);
 /* Unity.Mathematics f32tof16 / f16tof32 (host), exported for bindings and tests. */
 ART_API uint16_t art_f32tof16(float x);
 ART_API float art_f16tof32(uint16_t h);
+/* Bulk host f32tof16 of the float bit patterns first_bits, first_bits + 1, ... (count of them,
+ * wrapping past 0xFFFFFFFF): out[i] = art_f32tof16(asfloat(first_bits + i)). */
+ART_API void art_f32tof16_range(uint32_t first_bits, uint32_t count, uint16_t* out);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,12 @@ uint16_t or_f32tof16(float x)
     return (uint16_t)(h | (ux & ~msk) >> 16);
 }
 
+/* Bulk form for the exhaustive checks: out[i] = or_f32tof16(asfloat(first + i)). */
+void or_f32tof16_range(uint32_t first, uint32_t count, uint16_t* out)
+{
+    for (uint32_t i = 0; i < count; ++i) out[i] = or_f32tof16(asfloat(first + i));
+}
+
 /* math.f16tof32 (exact) */
 float or_f16tof32(uint16_t hx)
 {

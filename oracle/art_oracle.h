@@ -25,6 +25,7 @@ extern "C" {
 
 /* Unity.Mathematics conversions (App. A.1) */
 uint16_t or_f32tof16(float x);
+void or_f32tof16_range(uint32_t first, uint32_t count, uint16_t* out);
 float or_f16tof32(uint16_t h);
 
 /* Jobs/FibonacciDirectionsJobParallel.cs:15-35 (host libm cosf/sinf). */

@@ -34,6 +34,7 @@ def load():
     lib = C.CDLL(ORACLE_LIB)
     lib.or_f32tof16.restype = C.c_uint16
     lib.or_f32tof16.argtypes = [C.c_float]
+    lib.or_f32tof16_range.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p]
     lib.or_f16tof32.restype = C.c_float
     lib.or_f16tof32.argtypes = [C.c_uint16]
     lib.or_fibonacci_directions.argtypes = [C.c_int32, C.c_void_p]
@@ -76,6 +77,13 @@ def run(scene, params, origins, out: FanOutputs, threads: int = 1):
 
 def f32tof16(x: float) -> int:
     return int(load().or_f32tof16(x))
+
+
+def f32tof16_range(first: int, count: int):
+    import numpy as np
+    out = np.empty(count, np.uint16)
+    load().or_f32tof16_range(first, count, out.ctypes.data)
+    return out
 
 
 def f16tof32(h: int) -> float:
