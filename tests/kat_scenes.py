@@ -189,7 +189,49 @@ def k9_reduce():
     return sc, p, org, expect, prime
 
 
+# Q13 — MuffleRayHits is a ushort: the per-(hit, target) increment (:171) wraps above 65535
+def q13_ushort_wrap():
+    # 70000 Fibonacci rays from the centre of a radius-10 sphere owned by target 0: every ray hits
+    # the sphere from inside (t1, :337-351), every muffle ray to the target at (1,0,0) skips its own
+    # sphere (:413) and is clear, so the count is 70000 = 65536 + 4464.
+    from art.synth import fibonacci_directions
+    R = 70000
+    sc = art.Scene(dirs=fibonacci_directions(R), targets=np.array([[1, 0, 0]], np.float32),
+                   spheres=cat(abi.SPHERE, sphere((0, 0, 0), 10.0, tid=0)))
+    p = params()
+    org = np.zeros((1, 3), np.float32)
+
+    def expect(out):
+        assert out.muffle[0, 0] == 70000 - 65536
+        assert out.echo[0, 0] == h(10.0)  # the echo ray starts inside the sphere: exit at ~20 > 10
+    return sc, p, org, expect
+
+
+# Q19 — degenerate Fibonacci rays i = 0 (+0, 1, +0) and i = R-1 (+-0, -1, +-0) through a frame
+def q19_degenerate_dirs():
+    # ray 0 runs in the face plane x = 0 of the box [0,2]x[4,6]x[-1,1]: (min.x - o.x) * inf is NaN,
+    # Unity's min/max (App. A.2) then give tmin.x = tmax.x = inf, tNear = inf > tFar: a miss (Q19).
+    # ray R-1 hits the box [-1,1]x[-6,-4]x[-1,1] at distance 4: x/z slabs (+-1) * (+-inf) = -+inf.
+    from art.synth import fibonacci_directions
+    R = 64
+    sc = art.Scene(dirs=fibonacci_directions(R), targets=np.array([[0, 0, 3]], np.float32),
+                   aabbs=cat(abi.AABB, aabb((1, 5, 0), (1, 1, 1)), aabb((0, -5, 0), (1, 1, 1))))
+    assert tuple(sc.dirs[0]) == (0, h(1.0), 0) and sc.dirs[R - 1][1] == h(-1.0)
+    assert sc.dirs[R - 1][0] & 0x7FFF == 0 and sc.dirs[R - 1][2] & 0x7FFF == 0
+    p = params()
+    org = np.zeros((1, 3), np.float32)
+
+    def expect(out):
+        assert out.hit_counts[0, 0] == 0 and out.echo[0, 0] == 0
+        assert out.hit_counts[0, R - 1] == 1
+        assert out.echo[0, R - 1] == h(4.0)
+        assert out.hit_points[0, R - 1][1] == h(-4.0)
+    return sc, p, org, expect
+
+
 KATS = {
+    "q13_ushort_wrap": q13_ushort_wrap,
+    "q19_degenerate_dirs": q19_degenerate_dirs,
     "k6_echo1": lambda: k6_single_wall(1.0),
     "k6_echo3": lambda: k6_single_wall(3.0),
     "k7_owner_skip": k7_owner_skip,
