@@ -210,11 +210,13 @@ class JobHandle:
 
 
 class Context:
-    """An art_ctx: one HIP stream per selected device. Raises ArtError(ART_E_DEVICE) without a GPU."""
+    """An art_ctx. device_mask bit i selects HIP device i (one stream each; ArtError(ART_E_DEVICE)
+    without a GPU); device_mask 0 is the CPU backend (worker threads, host entry points only)."""
 
-    def __init__(self, device_mask: int = 0, flags: int = 0, devices: list[int] | None = None):
-        """device_mask: bit i selects HIP device i (art_create); devices: an explicit device list,
-        ids may repeat (art_create_on: shards on separate streams of one device)."""
+    def __init__(self, device_mask: int = 1, flags: int = 0, devices: list[int] | None = None):
+        """device_mask: bit i selects HIP device i, 0 the CPU backend (art_create); devices: an
+        explicit device list, ids may repeat (art_create_on: shards on separate streams of one
+        device)."""
         self.lib = abi.load_library()
         p = C.c_void_p()
         if devices is not None:
@@ -223,7 +225,8 @@ class Context:
         else:
             rc = self.lib.art_create(device_mask, C.byref(p))
         if rc:
-            raise ArtError(rc, "art_create failed (no HIP device?) — the product path has no CPU fallback")
+            raise ArtError(rc, "art_create failed (no HIP device?) — GPU contexts have no CPU fallback; "
+                               "device_mask 0 selects the CPU backend explicitly")
         self.ptr = p
         if flags:
             self.lib.art_set_flags(self.ptr, flags)

@@ -23,6 +23,7 @@
 #include "../../include/art_device.h"
 #include "../../include/art_dsp.h"
 #include "../../include/art_colliders.h"
+#include "art_cpu.hpp"
 #include "art_internal.hpp"
 #include "unity_math.hpp"
 
@@ -139,7 +140,9 @@ struct Device {
 }  // namespace
 
 struct art_ctx {
-  std::vector<Device> devs;
+  std::vector<Device> devs;        // empty for the CPU backend
+  art::CpuEngine* cpu = nullptr;   // art_create(0): the CPU backend (art_cpu.cpp)
+  std::vector<uint8_t> cpu_recs[3];  // CPU backend: the resident store's records at the last sync
   std::string err;
   uint32_t flags = 0;
   HostBuf h_in, h_block;
@@ -695,7 +698,15 @@ static int create_on(const int32_t* ids, int32_t count, art_ctx** out) {
 
 ART_API int art_create(uint32_t device_mask, art_ctx** out) {
   if (!out) return ART_E_INVALID;
-  if (device_mask == 0) device_mask = 1;
+  *out = nullptr;
+  if (device_mask == 0) {  // the CPU backend: worker threads, no HIP device needed
+    art_ctx* c = new (std::nothrow) art_ctx();
+    if (!c) return ART_E_NOMEM;
+    c->cpu = art::cpu_create(0);
+    if (!c->cpu) { delete c; return ART_E_NOMEM; }
+    *out = c;
+    return ART_OK;
+  }
   int32_t ids[32];
   int32_t k = 0;
   for (int i = 0; i < 32; ++i)
@@ -709,6 +720,10 @@ ART_API int art_create_on(const int32_t* device_ids, int32_t count, art_ctx** ou
 
 ART_API void art_destroy(art_ctx* c) {
   if (!c) return;
+  if (c->cpu) {
+    if (c->inflight) art::cpu_complete(c->cpu, nullptr);
+    art::cpu_destroy(c->cpu);
+  }
   for (Device& dv : c->devs) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
@@ -761,6 +776,23 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
     const art_fan& f = fans[i];
     if (!f.echo_ray_distances || !f.muffle_ray_hits || !f.permeation_power_remains || !f.settings)
       return fail(c, ART_E_INVALID, "fan %d: echo/muffle/permeation/settings arrays are required", i);
+  }
+  if (c->cpu) {
+    art::CpuColliders rc_{};
+    const bool res = (c->flags & ART_CTX_RESIDENT_COLLIDERS) != 0;
+    if (res) {
+      rc_.sph = reinterpret_cast<const art_sphere*>(c->cpu_recs[0].data()); rc_.ns = c->synced[0];
+      rc_.aabb = reinterpret_cast<const art_aabb*>(c->cpu_recs[1].data()); rc_.na = c->synced[1];
+      rc_.obb = reinterpret_cast<const art_obb*>(c->cpu_recs[2].data()); rc_.no = c->synced[2];
+    }
+    const bool count = (c->flags & ART_CTX_COUNT_TESTS) != 0;
+    rc = art::cpu_schedule(c->cpu, d, fans, fan_count, res ? &rc_ : nullptr, count);
+    if (rc) return fail(c, rc, "CPU backend: schedule failed");
+    c->counted = count;
+    c->inflight = true;
+    c->handle = c->next_handle++;
+    *out = c->handle;
+    return ART_OK;
   }
   Frame& f = c->fr;
   make_frame(d, hits ? ART_OUT_HIT_RESULTS : 0u, f, (c->flags & ART_CTX_RESIDENT_COLLIDERS) ? c->synced : nullptr);
@@ -828,6 +860,7 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
 ART_API int art_is_completed(art_ctx* c, art_handle h) {
   if (!c) return ART_E_INVALID;
   if (!c->inflight || h != c->handle) return (h != 0 && h < c->next_handle) ? 1 : fail(c, ART_E_STATE, "unknown handle");
+  if (c->cpu) return art::cpu_is_completed(c->cpu) ? 1 : 0;
   for (Device& dv : c->devs) {
     (void)hipSetDevice(dv.id);
     hipError_t e = hipEventQuery(dv.done);
@@ -844,6 +877,11 @@ ART_API int art_complete(art_ctx* c, art_handle h) {
     return fail(c, ART_E_STATE, "unknown handle");
   }
   c->inflight = false;
+  if (c->cpu) {
+    art::cpu_complete(c->cpu, c->counted ? &c->last_counts : nullptr);
+    if (c->counted) c->has_counts = true;
+    return ART_OK;
+  }
   for (Device& dv : c->devs) {
     HIP_TRY(c, hipSetDevice(dv.id));
     HIP_TRY(c, hipEventSynchronize(dv.done));
@@ -887,6 +925,7 @@ ART_API int art_last_test_counts(art_ctx* c, art_test_counts* out) {
 // ---------------------------------------------------------------------------- device-resident
 ART_API int art_scene_bind(art_ctx* c, const art_frame_desc* d) {
   if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
   // the in-flight frame's art_complete reads c->fr and its H2D copy may still read c->h_in
   if (c->inflight) return fail(c, ART_E_STATE, "art_scene_bind: a frame is in flight (bind after art_complete)");
   int rc = validate_desc(c, d);
@@ -909,6 +948,7 @@ ART_API int art_scene_bind(art_ctx* c, const art_frame_desc* d) {
 static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, void* d_block, uint32_t out_flags,
                          void* stream, bool count, art_test_counts* out) {
   if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
   if (c->inflight) return fail(c, ART_E_STATE, "a frame is in flight (launch after art_complete)");
   if (c->devs.empty() || !c->devs[0].bound) return fail(c, ART_E_STATE, "no scene bound (art_scene_bind)");
   if (fan_count < 0 || (fan_count > 0 && (!d_origins || !d_block))) return fail(c, ART_E_INVALID, "bad device buffers");
@@ -949,6 +989,7 @@ ART_API int art_count_device(art_ctx* c, const float* d_origins, int32_t fan_cou
 
 ART_API int art_fibonacci_directions_device(art_ctx* c, int32_t count, art_half3* d_out, void* stream) {
   if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
   if (count < 0 || (count > 0 && !d_out)) return fail(c, ART_E_INVALID, "art_fibonacci_directions_device: bad arguments");
   if (count == 0) return ART_OK;
   HIP_TRY(c, hipSetDevice(c->devs[0].id));
@@ -959,6 +1000,7 @@ ART_API int art_fibonacci_directions_device(art_ctx* c, int32_t count, art_half3
 
 ART_API int art_f32tof16_device(art_ctx* c, uint32_t first_bits, uint32_t count, uint16_t* d_out, void* stream) {
   if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
   if (count > 0 && !d_out) return fail(c, ART_E_INVALID, "art_f32tof16_device: d_out is NULL");
   HIP_TRY(c, hipSetDevice(c->devs[0].id));
   launch_half_range(first_bits, count, d_out, static_cast<hipStream_t>(stream));
@@ -1145,9 +1187,10 @@ ART_API int art_colliders_sync(art_ctx* c) {
       dv.st_pending = false;
     }
   }
+  if (c->cpu) bytes = 0;  // the CPU backend keeps no device copy (it snapshots the lists below)
   if (bytes && !c->h_upd.reserve(bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
   uint8_t* h = static_cast<uint8_t*>(c->h_upd.p);
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; bytes && k < 3; ++k) {
     const auto& K = c->kinds[k];
     const size_t rs = kRecSize[k];
     for (size_t j = 0; j < lists[k].size(); ++j) {
@@ -1257,6 +1300,8 @@ ART_API int art_colliders_sync(art_ctx* c) {
       hist[(size_t)(v + 32768)]++;
     }
   }
+  if (c->cpu)  // the CPU backend reads the synced snapshot (JobBatch) of each list
+    for (int k = 0; k < 3; ++k) c->cpu_recs[k].assign(c->kinds[k].recs.begin(), c->kinds[k].recs.begin() + (size_t)n[k] * kRecSize[k]);
   c->store_synced = true;
   c->last_sync.dirty_records = nd;
   c->last_sync.full_prep = (counts_changed || fresh) ? 1 : 0;
@@ -1275,6 +1320,7 @@ ART_API int art_dsp_source_params_get(const art_spatializer_settings* settings, 
 ART_API int art_dsp_process(art_ctx* c, const art_spatializer_settings* settings, art_audio_source* sources,
                             int32_t count, int32_t sample_rate) {
   if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
   if (!settings || count < 0 || (count > 0 && !sources) || sample_rate <= 0) return fail(c, ART_E_INVALID, "invalid argument");
   if (c->inflight) return fail(c, ART_E_STATE, "a frame is in flight");
   // host: per-buffer scalars; stereo sources with samples go to the device
@@ -1352,6 +1398,7 @@ ART_API int art_dsp_process(art_ctx* c, const art_spatializer_settings* settings
 ART_API int art_dsp_process_device(art_ctx* c, float* d_data, const art_dsp_source_params* d_params,
                                    art_dsp_state* d_state, int32_t count, int32_t frames, void* stream) {
   if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
   if (count < 0 || frames < 0 || (count > 0 && (!d_data || !d_params || !d_state))) return fail(c, ART_E_INVALID, "invalid argument");
   if (count == 0 || frames == 0) return ART_OK;
   Device& dv = c->devs[0];

@@ -24,7 +24,7 @@ struct Seg {
   float a2, a4;  // 2*a and 4*a with a = dot(d, d)
 };
 
-__device__ __forceinline__ Seg make_seg(vec3 o, vec3 d) {
+ART_HD Seg make_seg(vec3 o, vec3 d) {
   Seg s;
   s.o = o; s.d = d;
   s.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -37,7 +37,7 @@ __device__ __forceinline__ Seg make_seg(vec3 o, vec3 d) {
 // Slab test core — RayIntersectsAABB :289-307. EXACT selects Unity's min/max; otherwise IEEE
 // minNum/maxNum (v_min3/v_max3), equal except for the sign of a zero distance.
 template <bool EXACT>
-__device__ __forceinline__ bool slab(float ox, float oy, float oz, float ix, float iy, float iz, float mnx,
+ART_HD bool slab(float ox, float oy, float oz, float ix, float iy, float iz, float mnx,
                                      float mny, float mnz, float mxx, float mxy, float mxz, float& tNear,
                                      float& tFar) {
   float t0x = (mnx - ox) * ix, t0y = (mny - oy) * iy, t0z = (mnz - oz) * iz;
@@ -57,7 +57,7 @@ __device__ __forceinline__ bool slab(float ox, float oy, float oz, float ix, flo
 }
 
 template <bool EXACT>
-__device__ __forceinline__ bool aabb_test(const Seg& s, const AabbRec& b, float& dist) {
+ART_HD bool aabb_test(const Seg& s, const AabbRec& b, float& dist) {
   float tNear, tFar;
   bool hit = slab<EXACT>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, b.mnx, b.mny, b.mnz, b.mxx, b.mxy, b.mxz,
                          tNear, tFar);
@@ -68,7 +68,7 @@ __device__ __forceinline__ bool aabb_test(const Seg& s, const AabbRec& b, float&
 // RayIntersectsOBB :314-320 with rotation q (the stored one for the raytracer, its inverse for
 // the permeation first hit :174).
 template <bool EXACT>
-__device__ __forceinline__ bool obb_test(const Seg& s, const ObbRec& b, quat q, float& dist) {
+ART_HD bool obb_test(const Seg& s, const ObbRec& b, quat q, float& dist) {
   vec3 lo = qmul(q, s.o - mk3(b.cx, b.cy, b.cz));
   vec3 ld = qmul(q, s.d);
   float ix = 1.0f / ld.x, iy = 1.0f / ld.y, iz = 1.0f / ld.z;
@@ -78,11 +78,11 @@ __device__ __forceinline__ bool obb_test(const Seg& s, const ObbRec& b, quat q, 
   return hit;
 }
 
-__device__ __forceinline__ quat stored_q(const ObbRec& b) { quat q; q.x = b.qx; q.y = b.qy; q.z = b.qz; q.w = b.qw; return q; }
-__device__ __forceinline__ quat inverse_q(const ObbCold& b) { quat q; q.x = b.iqx; q.y = b.iqy; q.z = b.iqz; q.w = b.iqw; return q; }
+ART_HD quat stored_q(const ObbRec& b) { quat q; q.x = b.qx; q.y = b.qy; q.z = b.qz; q.w = b.qw; return q; }
+ART_HD quat inverse_q(const ObbCold& b) { quat q; q.x = b.iqx; q.y = b.iqy; q.z = b.iqz; q.w = b.iqw; return q; }
 
 // RayIntersectsSphere :323-355 (general quadratic)
-__device__ __forceinline__ bool sphere_test(const Seg& s, const SphereRec& c, float& dist) {
+ART_HD bool sphere_test(const Seg& s, const SphereRec& c, float& dist) {
   vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
   float b = 2.0f * dot(oc, s.d);
   float cc = dot(oc, oc) - c.r2;

@@ -29,6 +29,7 @@ namespace art {
 
 ART_HD uint32_t asuint(float f) { return __builtin_bit_cast(uint32_t, f); }
 ART_HD float asfloat(uint32_t u) { return __builtin_bit_cast(float, u); }
+ART_HD bool ufinite(float x) { return (asuint(x) & 0x7F800000u) != 0x7F800000u; }  // isfinite on host and device
 
 // math.min / math.max: isnan(y) || x < y ? x : y   (App. A.2)
 ART_HD float umin(float x, float y) { return (y != y || x < y) ? x : y; }

@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=0, help="timed steps (0 = enough for about 1.5 s)")
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", type=int, default=2)
+    p.add_argument("--config", type=int, default=None, help="BASELINE config (default: 2; 1 for --path cpu)")
     p.add_argument("--frames", type=int, default=50, help="host-API frames for the p50 frame latency")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-fans", type=int, default=0, help="fans in the CPU-baseline sample (0 = auto)")
@@ -62,9 +62,10 @@ def parse():
                    help="N > 1: weak = cfg.S fans per rank; strong = cfg.S fans split over the ranks "
                         "(auto: strong for config 4, as BASELINE.json names it, weak otherwise)")
     p.add_argument("--no-dynamic", action="store_true", help="skip the dynamic-scene and rebuild measurements")
-    p.add_argument("--path", choices=("raytrace", "dsp", "dirs"), default="raytrace",
+    p.add_argument("--path", choices=("raytrace", "dsp", "dirs", "cpu"), default="raytrace",
                    help="raytrace: the headline metric; dsp: the per-sample spatializer DSP (SURVEY.md 8 f rank 1); "
-                        "dirs: Fibonacci ray directions on the device (rank 3)")
+                        "dirs: Fibonacci ray directions on the device (rank 3); cpu: config 1 through the C ABI's "
+                        "CPU backend (device_mask 0) on N threads and 1 thread")
     p.add_argument("--dirs-count", type=int, default=1 << 24, help="directions per launch (dirs path)")
     p.add_argument("--dsp-frames", type=int, default=1024, help="frames per OnAudioFilterRead buffer (dsp path)")
     p.add_argument("--dsp-batch", type=int, default=65536, help="sources of the large-batch roofline run (dsp path)")
@@ -455,10 +456,57 @@ def dynamic_step(cfg, scene, params, org, S, steps, warmup, sp):
                                          "H2D, record decode, Morton sort and BVH build, kernels, D2H"}
 
 
+def cpu_frames(ctx, frame, min_seconds, max_frames=2000):
+    """p50 and mean art_schedule..art_complete time (ms) of repeated frames on a CPU-backend context."""
+    for _ in range(3):
+        ctx.run(frame)
+    ms, t0 = [], time.perf_counter()
+    while len(ms) < max_frames and (time.perf_counter() - t0 < min_seconds or len(ms) < 5):
+        t1 = time.perf_counter()
+        ctx.run(frame)
+        ms.append((time.perf_counter() - t1) * 1e3)
+    return statistics.median(ms), sum(ms) / len(ms), len(ms)
+
+
+def main_cpu(a):
+    """BASELINE config 1 (8 sources x 64 rays x 256 AABB colliders, the reference's CPU-runnable
+    case): frames through the C ABI's CPU backend (art_create(0): worker threads over fans, the
+    jobs' loop order) on the host's cores and on one thread."""
+    cfg = art.CONFIGS[a.config]
+    scene, org, params = art.synth(cfg, C_scale=a.collider_scale)
+    host = host_cpu_info()
+    res = {}
+    for label, threads in (("n", host["threads_used"]), ("one", 1)):
+        os.environ["ART_CPU_THREADS"] = str(threads)
+        with art.Context(0) as ctx:
+            out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1, hits=True, dsp=params.dsp is not None)
+            frame = art.Frame(scene, params, org, out)
+            ctx.set_flags(abi.ART_CTX_COUNT_TESTS)
+            ctx.run(frame)
+            tests = sum(ctx.last_test_counts().values())
+            ctx.set_flags(0)
+            p50, mean, n = cpu_frames(ctx, frame, a.cpu_seconds / 2)
+        res[label] = {"threads": threads, "p50_frame_ms": p50, "mean_frame_ms": mean, "frames": n,
+                      "tests_per_frame": tests, "tests_per_s": tests / (mean * 1e-3)}
+    os.environ.pop("ART_CPU_THREADS", None)
+    print(json.dumps({
+        "metric": f"config{cfg.index} CPU-backend ray-collider tests/s + p50 frame ms (plumbing through the C ABI)",
+        "value": res["n"]["tests_per_s"], "unit": "ray-collider tests/s", "n_gpus": 0, "steps": res["n"]["frames"],
+        "warmup": 3, "ms_per_step": res["n"]["mean_frame_ms"], "p50_frame_ms": res["n"]["p50_frame_ms"],
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"config{cfg.index}: {cfg.description}", "backend": "art_create(device_mask = 0)",
+                   "fans": cfg.S, "rays": cfg.R, "colliders": cfg.C, "targets": cfg.T, "max_hits_per_ray": cfg.H},
+        "threads_n": res["n"], "threads_1": res["one"], "host": host}))
+
+
 def main():
     a = parse()
+    if a.config is None:
+        a.config = 1 if a.path == "cpu" else 2
     if a.path != "raytrace" and a.steps <= 0:
         a.steps = 50
+    if a.path == "cpu":
+        return main_cpu(a)
     if a.path == "dsp":
         return main_dsp(a)
     if a.path == "dirs":

@@ -16,8 +16,10 @@
  *
  * All entry points are extern "C", take plain pointers and sizes, and never throw.
  * Return 0 (ART_OK) on success, a negative ART_E_* code on error; art_last_error()
- * gives the message.  There is NO CPU backend: a context needs a HIP device, and
- * art_create fails loudly (ART_E_DEVICE) when none is present.
+ * gives the message.  art_create(mask != 0) needs the HIP devices it names and fails loudly
+ * (ART_E_DEVICE) without them: a GPU context never falls back to the CPU.  art_create(0)
+ * selects the CPU backend explicitly (worker threads over fans, the jobs' own loop order;
+ * the host entry points of this header and art_colliders.h only).
  */
 #ifndef ART_H
 #define ART_H
@@ -175,8 +177,10 @@ typedef uint64_t art_handle;
 #define ART_E_NOMEM       -4
 #define ART_E_STATE       -5  /* unknown handle, frame already in flight, ... */
 
-/* device_mask: bit i selects HIP device i; 0 selects device 0. Fans are sharded contiguously
- * over the selected devices.  Fails with ART_E_DEVICE when HIP has no device. */
+/* device_mask: bit i selects HIP device i; fans are sharded contiguously over the selected
+ * devices; fails with ART_E_DEVICE when a selected device is missing.  device_mask 0: the CPU
+ * backend (Unity's Burst/CPU job path), ART_CPU_THREADS worker threads (default:
+ * the hardware threads); frames run asynchronously between art_schedule and art_complete. */
 ART_API int art_create(uint32_t device_mask, art_ctx** out);
 ART_API void art_destroy(art_ctx* ctx);
 ART_API const char* art_last_error(const art_ctx* ctx);

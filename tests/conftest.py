@@ -16,6 +16,6 @@ def pytest_configure(config):
 def ctx():
     """One art_ctx for the whole GPU session (device 0)."""
     import art
-    c = art.Context(0)
+    c = art.Context(1)
     yield c
     c.close()

@@ -62,9 +62,12 @@ def test_no_gpu_fails_loudly():
     if lib.art_device_count() > 0:
         pytest.skip("a HIP device is present")
     p = C.c_void_p()
-    assert lib.art_create(0, C.byref(p)) == abi.ART_E_DEVICE
+    assert lib.art_create(1, C.byref(p)) == abi.ART_E_DEVICE
     with pytest.raises(art.ArtError):
-        art.Context(0)
+        art.Context(1)
+    # device_mask 0 is the CPU backend: it needs no device; its device entry points refuse
+    with art.Context(0) as cpu:
+        assert cpu.lib.art_launch_device(cpu.ptr, None, 0, None, 0, None) == abi.ART_E_UNSUPPORTED
 
 
 def _frame(ci=1, **over):

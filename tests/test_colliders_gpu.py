@@ -82,7 +82,7 @@ def run_both(ctx, scene, params, org, model, check_oracle=False):
 
 @pytest.fixture
 def fresh_ctx():
-    c = art.Context(0)
+    c = art.Context(1)
     yield c
     c.close()
 
@@ -213,7 +213,7 @@ def test_device_resident_path_follows_syncs(fresh_ctx):
     store.sync()
     model.synced()
     dev = torch.device("cuda", 0)
-    ref_ctx = art.Context(0)
+    ref_ctx = art.Context(1)
     try:
         fr = art.Frame(scene, params, org, art.FanOutputs(8, scene.R, params.max_hits_per_ray, scene.T, params.thread_count))
         lay = art.fan_layout(fr)

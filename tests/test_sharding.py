@@ -1,7 +1,8 @@
 """The N>1 path on CPU: fan sharding + all-gather of packed fan blocks over gloo (world size 2
-and 3). Each rank computes its shard with the oracle (the CPU stand-in for the device kernels),
-packs it in the device block layout and all-gathers; the gathered bytes must equal the
-single-process full frame bit for bit (the multi-GPU invariance of SURVEY.md §8 e)."""
+and 3). Each rank computes its shard through libart's C ABI on the CPU backend (art_create with
+device_mask 0; tests/test_multigpu_gpu.py runs the same split on the HIP path), packs it in the
+device block layout and all-gathers; the gathered bytes must equal the oracle's single-process
+full frame bit for bit (the multi-GPU invariance of SURVEY.md §8 e)."""
 import os
 import socket
 
@@ -28,7 +29,6 @@ def _worker(rank, world, port, S, q):
     sys.path.insert(0, os.path.join(root, "audio-raytracer_amd"))
     sys.path.insert(0, os.path.join(root, "tests"))
     import art as A
-    import oracle as O
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -39,7 +39,8 @@ def _worker(rank, world, port, S, q):
         out = A.FanOutputs(e - b, 64, cfg.H, cfg.T, 1, dsp=True)
         fr = A.Frame(scene, params, np.ascontiguousarray(org[b:e]), out)
         if e > b:
-            O.run_frame(fr, threads=1)
+            with A.Context(0) as cpu:  # libart's CPU backend
+                cpu.run(fr)
         lay = A.fan_layout(fr)
         local = torch.from_numpy(A.pack_block(out, lay))
         full = A.dist.all_gather_fan_blocks(local, S, lay["stride"], world)
