@@ -22,6 +22,10 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SM
   echo "[gpu_round] pmc $c"
   timeout -k 10 120 rocprofv3 --pmc $c --output-format csv -d "$out/pmc_$n" -o run -- python3 bench.py $short --steps 5 --warmup 1 --frames 1 > "$out/pmc_$n.log" 2>&1
 done
+# HBM traffic per raytrace launch from the two PMC passes, stamped with this build's sha256, so
+# the bench line below reports it (bench.py reads profiles/traffic_config<k>.json)
+python3 tools/prof_summary.py "$out" "$tag" "$cfg" > "$out/prof_summary.log" 2>&1
+cp "profiles/traffic_config$cfg.json" "$out/"
 echo "[gpu_round] bench"
 timeout -k 10 400 python bench.py --config $cfg > "$out/bench.log" 2>&1
 tail -1 "$out/bench.log" > "$out/bench.json"
