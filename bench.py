@@ -62,6 +62,8 @@ def parse():
                    help="N > 1: weak = cfg.S fans per rank; strong = cfg.S fans split over the ranks "
                         "(auto: strong for config 4, as BASELINE.json names it, weak otherwise)")
     p.add_argument("--no-dynamic", action="store_true", help="skip the dynamic-scene and rebuild measurements")
+    p.add_argument("--targets", type=int, default=None,
+                   help="audio targets T (experiments; BASELINE's configs use 4): the same scene generator with T targets")
     p.add_argument("--path", choices=("raytrace", "dsp", "dirs", "cpu"), default="raytrace",
                    help="raytrace: the headline metric; dsp: the per-sample spatializer DSP (SURVEY.md 8 f rank 1); "
                         "dirs: Fibonacci ray directions on the device (rank 3); cpu: config 1 through the C ABI's "
@@ -524,6 +526,9 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     cfg = art.CONFIGS[a.config]
+    if a.targets:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, T=a.targets, description=f"{cfg.description}, T = {a.targets} audio targets")
     scaling = a.scaling if a.scaling != "auto" else ("strong" if cfg.index == 4 else "weak")
     S_total = cfg.S if scaling == "strong" else cfg.S * world
     scene, org_all, params = art.synth(cfg, S=S_total, C_scale=a.collider_scale)

@@ -14,6 +14,7 @@ for f in art_kernels art_trace art_bvh art_dsp; do
 done
 hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_capi.cpp" -o "$tmp/art_capi.o" &
 hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_synth.cpp" -o "$tmp/art_synth.o" &
+hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_cpu.cpp" -o "$tmp/art_cpu.o" &
 wait
 hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/variants/libart_$name.so" "$tmp"/*.o
 rm -rf "$tmp"

@@ -22,10 +22,10 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-HOT = ("nearest_first_kernel", "raytrace_fast_kernel", "pair_hist_kernel", "pair_colscan_kernel", "pair_scatter_kernel", "vis_kernel", "vis_finalize", "wf_nearest", "wf_visibility", "wf_finalize",
+HOT = ("nearest_first_kernel", "path_kernel", "pair_hist_kernel", "pair_colscan_kernel", "pair_scatter_kernel", "vis_kernel", "vis_finalize",
        "raytrace_kernel", "permeate_kernel", "reduce_kernel")
 # kernels of the timed raytrace stage (one launch of each per frame)
-STAGE = ("nearest_first_kernel", "raytrace_fast_kernel", "pair_hist_kernel", "pair_colscan_kernel", "pair_scatter_kernel",
+STAGE = ("nearest_first_kernel", "path_kernel", "pair_hist_kernel", "pair_colscan_kernel", "pair_scatter_kernel",
          "vis_kernel", "vis_finalize")
 
 
