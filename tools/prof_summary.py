@@ -79,8 +79,15 @@ def main():
         def mean(k, c):
             v = per[k].get(c, [])
             return sum(v) / len(v) if v else 0.0
-        fetch_kb = sum(mean(k, "FETCH_SIZE") for k in stage)
-        write_kb = sum(mean(k, "WRITE_SIZE") for k in stage)
+        # launches per frame: multi-hit frames run nearest_first_kernel and path_kernel once per
+        # bounce; vis_kernel runs once per frame
+        ref = max((len(v.get("FETCH_SIZE", [])) for k, v in per.items() if k.startswith("pair_hist_kernel")), default=1) or 1
+
+        def per_frame(k, c):  # mean per dispatch x dispatches per frame (rounded ratio to pair_hist_kernel's)
+            v = per[k].get(c, [])
+            return sum(v) / len(v) * max(1, round(len(v) / ref)) if v else 0.0
+        fetch_kb = sum(per_frame(k, "FETCH_SIZE") for k in stage)
+        write_kb = sum(per_frame(k, "WRITE_SIZE") for k in stage)
         rec = {
             "kernels": sorted(stage),
             "fetch_size_kb_raw": fetch_kb,
