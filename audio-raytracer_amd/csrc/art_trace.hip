@@ -125,13 +125,10 @@ __device__ __forceinline__ bool node_entry(const Seg& s, const CullRec& r, float
 // broken by the global order code (type rank << 28 | index), the reference's first minimum over
 // Sphere, AABB, OBB order (ShootRayCast :225-280).
 // ------------------------------------------------------------------------------------------
-template <int SEL>
-__device__ __forceinline__ int quad_bcast(int v) {
-  return __builtin_amdgcn_mov_dpp(v, SEL | (SEL << 2) | (SEL << 4) | (SEL << 6), 0xf, 0xf, false);
-}
 template <int CTRL>
 __device__ __forceinline__ int quad_perm(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false); }
 constexpr int kQuadXor1 = 1 | (0 << 2) | (3 << 4) | (2 << 6), kQuadXor2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);
+constexpr int kQuadRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6), kQuadRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);
 
 // (distance, order) minimum over the quad's four lanes.
 __device__ __forceinline__ void quad_min(float& d, int& dc) {
@@ -195,7 +192,17 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
   const bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0;
   int g = alive ? 0 : -1, sp = 0;
-  auto pop = [&]() { g = sp ? (int)my[sp - 1] : -1; sp = sp ? sp - 1 : 0; };
+  const int qshift = lane & ~3;
+  // branch-free pop: the stack slot is read unconditionally (clamped), the select picks -1 when empty
+  auto pop = [&]() {
+    const int t = (int)my[sp > 0 ? sp - 1 : 0];
+    g = sp > 0 ? t : -1;
+    sp = sp > 0 ? sp - 1 : 0;
+  };
+  // Near-first order by rank: each lane's key is its child's entry bits with the child index in the
+  // two low bits (unique in the quad; non-entered children 0xffffffff), its rank the number of
+  // smaller keys among the quad's other three (three DPP rotations). Children of rank 1 .. n-1 are
+  // pushed far first (each lane writes its own stack slot), rank 0 is descended into.
   auto inner_step = [&]() {
     const int c0 = 4 * g + 1;
     if (EX && qd == 0) ++nnode;
@@ -203,25 +210,18 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
     float tn;
     const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
-    const bool live = r.lox <= r.hix;  // empty nodes (past the last collider) have lo > hi
-    const float ek = (live && (force || (h && en <= best))) ? (force ? 0.0f : en) : INFINITY;
-    // full near-first order: the entered children sorted by entry (sorting network), pushed far first
-    const int eb = __float_as_int(ek);
-    float e[4] = {__int_as_float(quad_bcast<0>(eb)), __int_as_float(quad_bcast<1>(eb)),
-                  __int_as_float(quad_bcast<2>(eb)), __int_as_float(quad_bcast<3>(eb))};
-    int c[4] = {0, 1, 2, 3};
-    auto cswap = [&](int a, int b) {
-      if (e[b] < e[a]) { const float te = e[a]; e[a] = e[b]; e[b] = te; const int tc = c[a]; c[a] = c[b]; c[b] = tc; }
-    };
-    cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
-    if (e[0] < INFINITY) {
-#pragma unroll
-      for (int k = 3; k >= 1; --k)
-        if (e[k] < INFINITY) {
-          if (qd == 0) my[sp] = (uint32_t)(c0 + c[k]);
-          ++sp;
-        }
-      g = c0 + c[0];
+    const bool enter = (r.lox <= r.hix) & (force | (h & (en <= best)));  // bitwise: no branch
+    const uint32_t key = enter ? (((force ? 0u : (uint32_t)__float_as_int(en)) & ~3u) | (uint32_t)qd) : 0xffffffffu;
+    const uint32_t k1 = (uint32_t)quad_perm<kQuadRot1>((int)key), k2 = (uint32_t)quad_perm<kQuadXor2>((int)key),
+                   k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
+    const int rank = (int)(k1 < key) + (int)(k2 < key) + (int)(k3 < key);
+    const uint32_t em = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
+    const int nent = __popc(em);
+    const uint32_t fm = (uint32_t)(__ballot(enter && rank == 0) >> qshift) & 0xFu;
+    if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
+    if (nent) {
+      g = c0 + (int)__builtin_ctz(fm);
+      sp += nent - 1;
     } else {
       pop();
     }
@@ -288,6 +288,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
   unsigned long long* ex = EX ? fp.exec : nullptr;
   float best;
   int code;
+  vec3 o, d;
+  bool alive, write;
+  size_t out;
   if (step > 0) {  // the previous bounce's list of live ray slots
     const uint32_t* live = live_list(state, ngroups);
     const uint32_t cnt = live[(size_t)ngroups * 64 + step];
@@ -296,21 +299,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
     const bool ok = e < cnt;
     const uint32_t i = ok ? live[e] : 0u;
     const float4 a = state[2 * (size_t)i], b = state[2 * (size_t)i + 1];
-    const Seg s = make_seg(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
-    const bool alive = ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
-    quad_nearest_core<EX>(sc, s, alive, lane, my, best, code, ex);
-    if ((lane & 3) == 0 && ok) hits[i] = make_int2(__float_as_int(best), code);
-    return;
+    o = mk3(a.x, a.y, a.z);
+    d = mk3(b.x, b.y, b.z);
+    alive = ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
+    write = ok;
+    out = i;
+  } else {
+    if (state && blockIdx.x == 0 && threadIdx.x < kLiveCounters)  // multi-hit frame: clear the counters
+      live_list(state, ngroups)[(size_t)ngroups * 64 + threadIdx.x] = 0u;
+    const int fan = g / nrb;
+    const int slot = (g - fan * nrb) * 64 + rr;
+    alive = slot < fp.R;
+    const int ray = alive ? ray_order[slot] : 0;
+    o = load3(origins, fan);
+    d = load_dir(sc.dirs, ray);
+    write = true;
+    out = (size_t)g * 64 + rr;
   }
-  if (state && blockIdx.x == 0 && threadIdx.x < kLiveCounters)  // multi-hit frame: clear the counters
-    live_list(state, ngroups)[(size_t)ngroups * 64 + threadIdx.x] = 0u;
-  const int fan = g / nrb;
-  const int slot = (g - fan * nrb) * 64 + rr;
-  const bool valid = slot < fp.R;
-  const int ray = valid ? ray_order[slot] : 0;
-  const Seg s = make_seg(load3(origins, fan), load_dir(sc.dirs, ray));
-  quad_nearest_core<EX>(sc, s, valid, lane, my, best, code, ex);
-  if ((lane & 3) == 0) hits[(size_t)g * 64 + rr] = make_int2(__float_as_int(best), code);
+  quad_nearest_core<EX>(sc, make_seg(o, d), alive, lane, my, best, code, ex);
+  if ((lane & 3) == 0 && write) hits[out] = make_int2(__float_as_int(best), code);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1042,7 +1049,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       const CullRec r = sc.bvh[c0 + qd];
       float tn;
       const bool h = node_entry(s, r, om, tn);
-      const bool enter = r.lox <= r.hix && (force || (h && tn <= maxd));
+      const bool enter = (r.lox <= r.hix) & (force | (h & (tn <= maxd)));  // bitwise: no branch
       const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);
