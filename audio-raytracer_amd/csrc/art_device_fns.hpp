@@ -21,7 +21,7 @@ constexpr float kEps = 0.0001f;  // AudioRaytracerJobBatched.cs:57
 // ------------------------------------------------------------------------------------------
 struct Seg {
   vec3 o, d, inv;
-  float a2, a4;  // 2*a and 4*a with a = dot(d, d)
+  float a2;  // 2*a with a = dot(d, d); 4*a = 2 * a2 exactly (power-of-two scaling)
 };
 
 ART_HD Seg make_seg(vec3 o, vec3 d) {
@@ -30,7 +30,6 @@ ART_HD Seg make_seg(vec3 o, vec3 d) {
   s.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float a = dot(d, d);
   s.a2 = 2.0f * a;
-  s.a4 = 4.0f * a;
   return s;
 }
 
@@ -86,7 +85,7 @@ ART_HD bool sphere_test(const Seg& s, const SphereRec& c, float& dist) {
   vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
   float b = 2.0f * dot(oc, s.d);
   float cc = dot(oc, oc) - c.r2;
-  float disc = b * b - s.a4 * cc;
+  float disc = b * b - (2.0f * s.a2) * cc;  // 4 * a * c (:329)
   if (disc < 0.0f) return false;
   float sq = sqrtf(disc);
   float t0 = (-b - sq) / s.a2;

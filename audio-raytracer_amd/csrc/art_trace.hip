@@ -34,7 +34,7 @@ __device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c
   vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
   float b = 2.0f * dot(oc, s.d);
   float cc = dot(oc, oc) - c.r2;
-  float disc = b * b - s.a4 * cc;
+  float disc = b * b - (2.0f * s.a2) * cc;  // 4 * a * c (:329)
   bool hit = false;
   dist = 0.0f;
   if (disc >= 0.0f) {
@@ -145,7 +145,9 @@ __device__ __forceinline__ void quad_min(float& d, int& dc) {
 }
 
 // Exact test of leaf slot `sl` (64 B: the hot record's test fields and the order code, art_bvh.hip
-// bvh_leaf_kernel) against segment s; tid = the collider's AudioTargetId.
+// bvh_leaf_kernel) against segment s; tid = the collider's AudioTargetId. OBB = false: the scene has
+// no OBBs (no rank-2 slots), their test compiles out.
+template <bool OBB>
 __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const float4* sl, int& cc, float& dist, int& tid,
                                                unsigned* nt) {
   const float4 qa = sl[0], qb = sl[1];
@@ -161,7 +163,7 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const float4* sl, i
     ++nt[0];
     return sphere_hit_dist(s, r, dist);
   }
-  if (t == 1) {
+  if (t == 1 || !OBB) {
     AabbRec r;
     r.mnx = qa.x; r.mny = qa.y; r.mnz = qa.z; r.mxx = qa.w; r.mxy = qb.x; r.mxz = qb.y;
     tid = __float_as_int(qb.z);
@@ -180,7 +182,7 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const float4* sl, i
 
 // Nearest hit of the quad's ray s (identical in the 4 lanes; `my` = the ray's kBvhStack-entry
 // stack): (distance, order) minimum in best / code of every lane of the quad.
-template <bool EX>
+template <bool EX, bool OBB>
 __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg& s, bool alive, int lane, uint32_t* my,
                                                   float& best, int& code, unsigned long long* ex) {
   const int qd = lane & 3;
@@ -230,7 +232,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
     const float4* sl = sc.bvh_leaf + (size_t)(leaf - leaf0) * (4 * kBvhLeaf) + 4 * qd;
     int cc, tid;
     float dd;
-    const bool h = leaf_slot_test(s, sl, cc, dd, tid, nt);
+    const bool h = leaf_slot_test<OBB>(s, sl, cc, dd, tid, nt);
     // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue)
     float d = INFINITY;
     int dc = kNoHit;
@@ -274,7 +276,8 @@ __device__ __forceinline__ uint32_t* live_list(float4* state, int ngroups) {
   return reinterpret_cast<uint32_t*>(state + 2 * (size_t)ngroups * 64);
 }
 
-template <bool EX>  // EX: count the executed tests (fp.exec)
+// EX: count the executed tests (fp.exec); OBB: the scene has OBBs.
+template <bool EX, bool OBB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step) {
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
   int code;
   vec3 o, d;
   bool alive, write;
-  size_t out;
+  uint32_t out;  // ray slot (< 2^31: fast_fans_per_launch)
   if (step > 0) {  // the previous bounce's list of live ray slots
     const uint32_t* live = live_list(state, ngroups);
     const uint32_t cnt = live[(size_t)ngroups * 64 + step];
@@ -314,9 +317,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
     o = load3(origins, fan);
     d = load_dir(sc.dirs, ray);
     write = true;
-    out = (size_t)g * 64 + rr;
+    out = (uint32_t)g * 64u + (uint32_t)rr;
   }
-  quad_nearest_core<EX>(sc, make_seg(o, d), alive, lane, my, best, code, ex);
+  quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, best, code, ex);
   if ((lane & 3) == 0 && write) hits[out] = make_int2(__float_as_int(best), code);
 }
 
@@ -324,22 +327,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
 // Visibility pairs. The path kernel emits every (hit, query) pair with its output destination;
 // visibility never feeds back into ray paths (echo :124-145 and muffle :150-173 only write
 // outputs), so the verdicts can be computed after all bounces.
-// Pair arrays (struct of arrays, pair index = emission order):
-//   seg[2 i], seg[2 i + 1]  (o.xyz, maxd), (d.xyz, owner)   32 B, read by the visibility sweep;
+// Pair arrays (struct of arrays). Echo pairs i in [0, echo_cap), emission order (the 64 rays of a
+// wave share the fan origin, one batch each):
+//   seg[2 i], seg[2 i + 1]  (o.xyz, maxd), (d.xyz, kNoOwner)  32 B, read by the echo traversal;
 //                           1/d and dot(d, d) are recomputed there by make_seg (same operations)
-//   out[i]                  (dest, val)                      8 B, read by vis_finalize
-//   flag[i]                 0 = no blocker found yet, 1 = blocked
-// Echo pairs fill [0, echo_cap) in emission order (the 64 rays of a wave share the fan origin, one
-// batch each); muffle pairs fill [echo_cap, echo_cap + S R H T). counts[0] / counts[1] = echo /
+//   out[i]                  (u16 index of the echo in the fan blocks, echo half)  8 B, vis_finalize
+// Muffle pairs e in [0, S R H T), emission order:
+//   mrec[e]                 (off.xyz, e << tbits | t)  16 B: the segment's start and its target
+//                           (bit 31 of w: blocked, set in the sorted copy by the sweep);
+//                           maxd and the direction to the target are recomputed by the sweep with
+//                           the path kernel's operations
+//   mdest[e]                muffle_acc index  4 B, read by vis_finalize
+//   msorted[]               mrec counting-sorted by key (pair_scatter_kernel): the sweep reads its
+//                           batches of 64 coalesced, 16 B per pair
+// flag[i] / flag[echo_cap + e]: 0 = no blocker found yet, 1 = blocked. counts[0] / counts[1] = echo /
 // muffle pairs emitted.
 // ------------------------------------------------------------------------------------------
 struct VisPairs {
   float4* seg;
-  uint2* out;      // dest: echo u16 index into the fan blocks / muffle_acc index; val: echo half | kPairMuffle
+  uint2* out;
   uint32_t* flag;
+  float4* mrec;
+  float4* msorted;
+  uint32_t* mdest;
   uint32_t echo_cap;  // multiple of 64
+  int tbits;          // target bits of a muffle record's w
 };
-constexpr uint32_t kPairMuffle = 1u << 16;
+
+// Bits of a target index (T targets): the muffle records pack (e << bits | t) into 32 bits.
+__host__ __device__ inline int target_bits(int T) {
+  int b = 0;
+  while ((1 << b) < T) ++b;
+  return b;
+}
 
 __device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Seg& s, float& maxd, int& owner) {
   const float4 q0 = vp.seg[2 * (size_t)i], q1 = vp.seg[2 * (size_t)i + 1];
@@ -525,29 +545,23 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
         for (int qq = 0; qq < kMaxQueries; ++qq) {
           const int q = q0 + qq;
           if (q <= T && ((actbits >> qq) & 1u)) {
-            vec3 qdir;
-            float maxd;
-            int owner;
-            uint2 ov;
-            if (q == 0) {
-              qdir = normalize(O - off); maxd = dist0; owner = kNoOwner;
-              ov.x = (uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k);
-              ov.y = f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
-            } else {
-              const vec3 tp = load3(sc.targets, q - 1);
-              maxd = distance(off, tp);
-              qdir = normalize(tp - off);
-              owner = q - 1;                                      // :413, :426, :439
-              ov.x = (uint32_t)(((size_t)fan * fp.TC + my_slot) * T + (q - 1));
-              ov.y = kPairMuffle;
-            }
             const uint32_t rank = (uint32_t)__popcll(mq[qq] & lt);
-            const uint32_t at = q == 0 ? eb + rank : vp.echo_cap + pos + rank;
-            vp.seg[2 * (size_t)at] = make_float4(off.x, off.y, off.z, maxd);
-            vp.seg[2 * (size_t)at + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(owner));
-            vp.out[at] = ov;
-            vp.flag[at] = 0u;
-            if (q > 0 && pkeys) pkeys[pos + rank] = vis_sort_key(q - 1, T, mk3(-qdir.x, -qdir.y, -qdir.z));
+            if (q == 0) {  // the echo ray to the fan origin (:124-145): its segment in full
+              const uint32_t at = eb + rank;
+              const vec3 qdir = normalize(O - off);
+              vp.seg[2 * (size_t)at] = make_float4(off.x, off.y, off.z, dist0);
+              vp.seg[2 * (size_t)at + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(kNoOwner));
+              vp.out[at] = make_uint2((uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k),
+                                      f32tof16(dist0 * echo_of(sc, type, idx)));  // :142-144
+              vp.flag[at] = 0u;
+            } else {  // a muffle ray to target q - 1 (:150-173): its start, target and counter
+              const uint32_t e = pos + rank;
+              const vec3 qdir = normalize(load3(sc.targets, q - 1) - off);  // :158-160
+              vp.mrec[e] = make_float4(off.x, off.y, off.z, __uint_as_float((e << vp.tbits) | (uint32_t)(q - 1)));
+              vp.mdest[e] = (uint32_t)(((size_t)fan * fp.TC + my_slot) * T + (q - 1));
+              vp.flag[vp.echo_cap + e] = 0u;
+              pkeys[e] = vis_sort_key(q - 1, T, mk3(-qdir.x, -qdir.y, -qdir.z));
+            }
           }
           if (q > 0 && q <= T) pos += (uint32_t)__popcll(mq[qq]);
         }
@@ -707,7 +721,8 @@ __global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16
                                                                     const uint32_t* __restrict__ count,
                                                                     const uint32_t* __restrict__ prefix,
                                                                     const uint32_t* __restrict__ tot,
-                                                                    uint32_t* __restrict__ order, int nblk, int nbins) {
+                                                                    const float4* __restrict__ mrec,
+                                                                    float4* __restrict__ msorted, int nblk, int nbins) {
   __shared__ uint32_t cur[kSortBins];
   __shared__ uint32_t s_part[kSortThreads];
   constexpr int kPer = kSortBins / kSortThreads;
@@ -743,7 +758,7 @@ __global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16
 #pragma unroll
   for (uint32_t j = 0; j < 16u; ++j) {
     if (i0 + j >= e) break;
-    order[atomicAdd(&cur[kk[j]], 1u)] = i0 + j;
+    msorted[atomicAdd(&cur[kk[j]], 1u)] = mrec[i0 + j];
   }
 }
 
@@ -870,6 +885,7 @@ __device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet&
 // the members of the candidate chunks (lane = collider), then exact wave-uniform tests of the
 // candidates. Any-hit is an OR over the colliders, so the order is free. Returns the lane's
 // verdict (true = blocked).
+template <bool OBB>
 __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid, int lane,
                                            unsigned long long* ex, int c_lo, int c_hi, const VisCone& vc) {
   const int cs_n = (sc.ns + kChunk - 1) / kChunk, ca_n = (sc.na + kChunk - 1) / kChunk;
@@ -920,7 +936,7 @@ __device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, flo
           float d;
           return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
         }, nt[1]);
-      } else {
+      } else if (OBB) {
         // OBB candidates (118-op exact test): first each lane's slab test against the collider's own
         // widened bounds (a blocker's segment enters them before maxd); the
         // exact test runs only where a live lane passes
@@ -961,54 +977,52 @@ __host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) {
   return 2 * sc.no > sc.ns + sc.na + sc.no ? 8 : (sc.no > 0 ? 4 : 2);
 }
 
-// Pair of lane `lane` in batch b: echo batches cover [0, echo_cap) in emission order, muffle batches
-// the sorted muffle pairs (order = sorted position -> muffle pair, or identity). Returns false for
-// a batch past the emitted pairs; n_in = the batch's valid lanes (the others get the batch's first
-// pair, so every lane holds a real segment).
-__device__ __forceinline__ bool batch_pair(const VisPairs& vp, const uint32_t* count, const uint32_t* order, uint32_t b,
-                                           int lane, uint32_t& pi, uint32_t& n_in) {
-  const uint32_t base = b * 64u;
-  uint32_t rel, n, off;
-  if (base < vp.echo_cap) { rel = base; n = ldc(count, 0); off = 0u; }
-  else { rel = base - vp.echo_cap; n = ldc(count, 1); off = vp.echo_cap; }
-  if (rel >= n) return false;
-  n_in = min(64u, n - rel);
-  const uint32_t q = rel + ((uint32_t)lane < n_in ? (uint32_t)lane : 0u);
-  pi = off + ((order && off) ? order[q] : q);
-  return true;
-}
-
-// Work item i of the sweep = (chunk range r, batch b), range-major: r = i / nbv, b = i % nbv over
-// the muffle batches [b_first, nb_max). A batch's later ranges usually start after its earlier
-// ones finished and skip the pairs those already blocked (a stale read only costs work). Verdicts
-// meet in VisPairs::flag through relaxed device-scope atomicOr (no fences: an agent-scope release
-// writes back the XCD's L2); vis_finalize writes the outputs after the kernel boundary.
+// Work item i of the muffle sweep = (chunk range r, sorted batch b), range-major: r = i / nbm,
+// b = i % nbm. Lane = sorted position 64 b + lane: its record gives the segment's start, its target
+// t and its emission index e; maxd and the direction to the target are recomputed with the path
+// kernel's operations (:158-168), so the segment is the one the reference tests. A batch's later
+// ranges usually start after its earlier ones finished and skip the pairs those already blocked:
+// a blocker sets bit 31 of the sorted record (coalesced, read with the record; a stale read only
+// costs work) and the pair's flag[echo_cap + e] for vis_finalize, both by relaxed device-scope
+// atomicOr (no fences: an agent-scope release writes back the XCD's L2); vis_finalize writes the
+// outputs after the kernel boundary.
+template <bool OBB>
 __device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                               uint32_t nb_max, const uint32_t* order, unsigned long long* ex,
-                                               uint32_t b_first, uint32_t blk) {
+                                               uint32_t nbm, unsigned long long* ex, uint32_t blk) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nbv = nb_max - b_first;
   const uint32_t item = blk * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t r = item / nbv, b = b_first + (item - r * nbv);
+  const uint32_t r = item / nbm, b = item - r * nbm;
   const int nranges = vis_ranges(sc);
-  uint32_t pi, n_in;
-  if (r >= (uint32_t)nranges || !batch_pair(vp, count, order, b, lane, pi, n_in)) return;
-  uint32_t* flag = vp.flag + pi;
-  // pairs an earlier range already blocked are skipped (not loaded, and out of the wave's box)
-  const bool valid = (uint32_t)lane < n_in && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  const uint32_t base = b * 64u, n = ldc(count, 1);
+  if (r >= (uint32_t)nranges || base >= n) return;
+  const uint32_t n_in = min(64u, n - base);
+  const uint32_t p = base + ((uint32_t)lane < n_in ? (uint32_t)lane : 0u);
+  const float4 rec = vp.msorted[p];
+  const uint32_t wv = __float_as_uint(rec.w), e = (wv & 0x7fffffffu) >> vp.tbits;
+  const int t = (int)(wv & ((1u << vp.tbits) - 1u));
+  // pairs an earlier range already blocked (bit 31 of the sorted record) are skipped (out of the
+  // wave's box)
+  const bool valid = (uint32_t)lane < n_in && (wv >> 31) == 0u;
   if (!__any(valid)) return;
   Seg s;
   float maxd = 0.0f;
-  int owner = kNoOwner;
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
-  s.a2 = s.a4 = 0.0f;
-  if (valid) load_pair_seg(vp, pi, s, maxd, owner);
+  s.a2 = 0.0f;
+  if (valid) {
+    const vec3 off = mk3(rec.x, rec.y, rec.z), tp = load3(sc.targets, t);
+    maxd = distance(off, tp);                // :165
+    s = make_seg(off, normalize(tp - off));  // :158-160
+  }
   const int nch = sc.nchunks;
   const int c_lo = (int)(((long long)nch * r) / nranges), c_hi = (int)(((long long)nch * (r + 1)) / nranges);
   const float om = wave_max(valid ? fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd : 0.0f);
   const VisCone vc = make_vis_cone(s, maxd, valid, om);
-  const bool blocked = cull_sweep(sc, s, maxd, owner, valid, lane, ex, c_lo, c_hi, vc);
-  if (valid && blocked) __hip_atomic_fetch_or(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool blocked = cull_sweep<OBB>(sc, s, maxd, t, valid, lane, ex, c_lo, c_hi, vc);  // owner = t (:413, :426, :439)
+  if (valid && blocked) {
+    __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(vp.msorted + p) + 3, 0x80000000u, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(vp.flag + vp.echo_cap + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1020,20 +1034,21 @@ __device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPair
 // entry), 4 lanes per segment (lane q: child q / leaf slot q; the quad agrees through ballots),
 // the first blocker ends the segment.
 // ------------------------------------------------------------------------------------------
+template <bool OBB>
 __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                              const uint32_t* order, unsigned long long* ex, uint32_t blk, uint32_t* s_stk) {
+                                              unsigned long long* ex, uint32_t blk, uint32_t* s_stk) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
   const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64-pair batch
-  uint32_t p, n_in;
+  const uint32_t base = blk * 64u, n = ldc(count, 0);
   if (sc.bvh_levels == 0) return;                              // no colliders: nothing blocks
-  if (!batch_pair(vp, count, order, blk, slot, p, n_in)) return;
-  if ((uint32_t)(w * 16) >= n_in) return;                      // this wave's 16 segments are past the batch's end
-  const bool valid = (uint32_t)slot < n_in;
+  if (base + (uint32_t)(w * 16) >= n) return;                  // this wave's 16 segments are past the emitted pairs
+  const bool valid = base + (uint32_t)slot < n;
+  const uint32_t p = valid ? base + (uint32_t)slot : base;
   Seg s;
   float maxd = 0.0f;
   int owner = kNoOwner;
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
-  s.a2 = s.a4 = 0.0f;
+  s.a2 = 0.0f;
   if (valid) load_pair_seg(vp, p, s, maxd, owner);
   const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
   const bool force = force_all(s, om);
@@ -1066,7 +1081,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       const float4* sl = sc.bvh_leaf + (size_t)(g - leaf0) * (4 * kBvhLeaf) + 4 * qd;
       int cc, tid;
       float d;
-      const bool hh = leaf_slot_test(s, sl, cc, d, tid, nt);
+      const bool hh = leaf_slot_test<OBB>(s, sl, cc, d, tid, nt);
       const bool blk_here = hh && d < maxd && tid != owner;  // :373-394, :411-447
       if ((uint32_t)(__ballot(blk_here) >> qshift) & 0xFu) {
         blocked = true;
@@ -1090,14 +1105,14 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 // the echo batches by quad BVH traversal (longer jobs first), the others run the sweep's items.
 // EX: count the executed tests (fp.exec); without it the counters compile out. 8 waves per SIMD
 // (a few VGPRs spill; measured faster than 6 or 7).
-template <bool EX>
+template <bool EX, bool OBB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nb_max,
-                const uint32_t* __restrict__ order, unsigned long long* ex, uint32_t n_echo) {
+void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nbm, unsigned long long* ex,
+                uint32_t n_echo) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
   unsigned long long* e = EX ? ex : nullptr;
-  if (blockIdx.x < n_echo) vis_quad_body(sc, vp, count, order, e, blockIdx.x, s_stk);
-  else vis_sweep_body(sc, vp, count, nb_max, order, e, n_echo, blockIdx.x - n_echo);
+  if (blockIdx.x < n_echo) vis_quad_body<OBB>(sc, vp, count, e, blockIdx.x, s_stk);
+  else vis_sweep_body<OBB>(sc, vp, count, nbm, e, blockIdx.x - n_echo);
 }
 
 // Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
@@ -1111,9 +1126,12 @@ __global__ __launch_bounds__(256) void vis_finalize(VisPairs vp, const uint32_t*
   if (__builtin_amdgcn_readfirstlane(rel - lane) >= n) return;
   const bool valid = rel < n;
   uint32_t flag = 1u, dest = 0u, val = 0u;
-  if (valid) { flag = vp.flag[p]; const uint2 o = vp.out[p]; dest = o.x; val = o.y; }
+  const bool muf = !echo_region;
+  if (valid) {
+    flag = vp.flag[p];
+    if (muf) { dest = vp.mdest[rel]; } else { const uint2 o = vp.out[p]; dest = o.x; val = o.y; }
+  }
   const bool vis = valid && flag == 0u;
-  const bool muf = (val & kPairMuffle) != 0;
   if (vis && !muf) reinterpret_cast<uint16_t*>(block)[dest] = (uint16_t)(val & 0xffffu);  // :142-144
   // muffle counts (:171): one atomic per distinct counter of the wave (its pairs come from one or
   // two (fan, target) groups of the emission order)
@@ -1129,12 +1147,13 @@ __global__ __launch_bounds__(256) void vis_finalize(VisPairs vp, const uint32_t*
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
-// Pair buffer: VisPairs (seg | out | flag) | first-segment hits | ray state + live list (multi-hit)
-// | muffle keys u16 | sorted order u32 | hist, scanned hist u32[bins x blocks] | bucket totals.
+// Pair buffer: VisPairs (echo seg | echo out | flag | muffle records | sorted records | muffle dest)
+// | first-segment hits | ray state + live list (multi-hit) | muffle keys u16 | hist, scanned hist
+// u32[bins x blocks] | bucket totals.
 struct PairBufs {
   VisPairs vp;
   uint16_t* keys;
-  uint32_t *order, *hist, *prefix, *tot;
+  uint32_t *hist, *prefix, *tot;
   int2* pre;        // [groups * 64] nearest hits of the current bounce
   float4* state;    // [groups * 64][2] ray state between the bounce launches (multi-hit frames)
   size_t total;
@@ -1152,10 +1171,14 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   uint8_t* p = static_cast<uint8_t*>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) { uint8_t* q = p ? p + off : nullptr; off += align256(bytes); return q; };
-  b.vp.seg = reinterpret_cast<float4*>(take(max_pairs * 32));
-  b.vp.out = reinterpret_cast<uint2*>(take(max_pairs * 8));
+  b.vp.seg = reinterpret_cast<float4*>(take(ecap * 32));
+  b.vp.out = reinterpret_cast<uint2*>(take(ecap * 8));
   b.vp.flag = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
+  b.vp.mrec = reinterpret_cast<float4*>(take(mcap * 16));
+  b.vp.msorted = reinterpret_cast<float4*>(take(mcap * 16));
+  b.vp.mdest = reinterpret_cast<uint32_t*>(take(mcap * 4));
   b.vp.echo_cap = (uint32_t)ecap;
+  b.vp.tbits = target_bits(fp.T);
   b.pre = reinterpret_cast<int2*>(take(slots * sizeof(int2)));
   if (fp.H > 1) b.state = reinterpret_cast<float4*>(take(slots * (2 * sizeof(float4) + 4) + kLiveCounters * 4));
   if (mcap) {
@@ -1163,7 +1186,6 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
     b.nbins = fp.T << sort_dir_bits(fp.T);  // keys (target << bits | cell) < T << bits <= kSortBins
     const size_t cells = (size_t)b.nbins * b.nblk;
     b.keys = reinterpret_cast<uint16_t*>(take(mcap * 2 + 64));  // + padding for load_keys16 past the end
-    b.order = reinterpret_cast<uint32_t*>(take(mcap * 4));
     b.hist = reinterpret_cast<uint32_t*>(take(cells * 4));
     b.prefix = reinterpret_cast<uint32_t*>(take(cells * 4));
     b.tot = reinterpret_cast<uint32_t*>(take((size_t)b.nbins * 4));
@@ -1175,13 +1197,16 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
 size_t fast_pair_bytes(const FrameParams& fp) { return pair_bufs(nullptr, fp).total; }
 
 // Fans per launch_raytrace_fast call: pair slots (echo + muffle, R*H*(T+1) per fan) stay below
-// 2^31 (u32 slots and sorted positions) and a fan's echo halves stay addressable with a 32-bit
-// half offset into the block (fan * stride / 2 < 2^32).
+// 2^31 (u32 slots and sorted positions), muffle emission indices fit the records' 31 - tbits bits,
+// and a fan's echo halves stay addressable with a 32-bit half offset into the block
+// (fan * stride / 2 < 2^32).
 int fast_fans_per_launch(int R, int H, int T, uint32_t stride) {
   const unsigned long long per_fan = (unsigned long long)R * H * (T + 1) + 64;
   const unsigned long long by_pairs = ((1ull << 31) - 64) / per_fan;
+  const unsigned long long mper_fan = (unsigned long long)R * H * (T > 0 ? T : 1);
+  const unsigned long long by_rec = ((1ull << (31 - target_bits(T))) - 1) / mper_fan;
   const unsigned long long by_block = ((1ull << 33) - 1) / (stride ? stride : 1) - 1;
-  unsigned long long n = std::min(std::min(by_pairs, by_block), (unsigned long long)(1 << 24));
+  unsigned long long n = std::min(std::min(std::min(by_pairs, by_rec), by_block), (unsigned long long)(1 << 24));
   if (const char* e = getenv("ART_FAST_CHUNK_FANS")) {  // test hook: force small chunks
     const long long v = atoll(e);
     if (v > 0) n = std::min(n, (unsigned long long)v);
@@ -1198,13 +1223,14 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const unsigned groups = (unsigned)((size_t)fp.S * ((fp.R + 63) / 64));
   const unsigned path_blocks = (groups + kPathWaves - 1) / kPathWaves;
   const bool multi = fp.H > 1;
+  const bool obb = sc.no > 0;  // OBB-free scenes run instantiations without the OBB tests
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
-    if (fp.exec)
-      hipLaunchKernelGGL(nearest_first_kernel<true>, dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre,
-                         pb.state, k);
-    else
-      hipLaunchKernelGGL(nearest_first_kernel<false>, dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre,
-                         pb.state, k);
+#define ART_NEAREST(EX_, OBB_)                                                                                      \
+  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
+                     pb.state, k)
+    if (fp.exec) { if (obb) ART_NEAREST(true, true); else ART_NEAREST(true, false); }
+    else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
+#undef ART_NEAREST
 #define ART_PATH(H_, M_)                                                                                              \
   hipLaunchKernelGGL((path_kernel<H_, M_>), dim3(path_blocks), dim3(64 * kPathWaves), 0, st, sc, fp, L, origins, block, \
                      ray_order, pb.vp, pair_count, pb.keys, pb.pre, pb.state, k)
@@ -1220,19 +1246,20 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     hipLaunchKernelGGL(pair_colscan_kernel, dim3((pb.nbins + 63) / 64), dim3(64), 0, st, pb.hist, pb.prefix, pb.tot, pb.nblk,
                        pb.nbins);
     hipLaunchKernelGGL(pair_scatter_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.prefix, pb.tot,
-                       pb.order, pb.nblk, pb.nbins);
+                       pb.vp.mrec, pb.vp.msorted, pb.nblk, pb.nbins);
   }
   // echo batches by quad BVH traversal, the muffle batches by the sweep (4 items per workgroup)
   const uint32_t eb = pb.vp.echo_cap / 64;
-  const size_t vitems = (size_t)(nb_max - eb) * vis_ranges(sc);
+  const uint32_t nbm = nb_max - eb;  // muffle batches
+  const size_t vitems = (size_t)nbm * vis_ranges(sc);
   const size_t blocks = eb + (vitems + 3) / 4;
   if (blocks) {
-    if (fp.exec)
-      hipLaunchKernelGGL(vis_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max,
-                         pb.order, fp.exec, eb);
-    else
-      hipLaunchKernelGGL(vis_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nb_max,
-                         pb.order, nullptr, eb);
+#define ART_VIS(EX_, OBB_)                                                                                         \
+  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nbm,     \
+                     EX_ ? fp.exec : nullptr, eb)
+    if (fp.exec) { if (obb) ART_VIS(true, true); else ART_VIS(true, false); }
+    else { if (obb) ART_VIS(false, true); else ART_VIS(false, false); }
+#undef ART_VIS
   }
   hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                      muffle_acc);
