@@ -806,8 +806,10 @@ void or_quat_mul_vec(const float q[4], const float v[3], float out[3])
  *    (Audio/AudioTarget/AudioSpatializer.cs:70-87) = MuffleDSP.Process (MuffleDSP.cs:13-32),
  *    ReverbDSP.Process (ReverbDSP.cs:10-24), BinauralDSP.Process (BinauralDSP.cs:15-82), volume.
  *    Literal: per-sample quantities are recomputed inside the loops as the C# does.
- *    math.sin/cos/atan2 are the host libm (Burst's are not reproducible here: parity for those
- *    per-buffer scalars is unpinned by the reference).
+ *    BinauralDSP runs in managed code (no [BurstCompile] under Audio/), where Unity.Mathematics'
+ *    math.atan2/sin/cos(float) are (float)System.Math.Atan2/Sin/Cos: evaluated in double and
+ *    rounded once (BinauralDSP.cs:17,27,32); the host libm's double functions are correctly
+ *    rounded for these arguments in practice, .NET's may differ in rare last bits (unpinned).
  * ====================================================================================== */
 #define OR_TODEGREES 57.29578f      /* Unity.Mathematics math.degrees factor */
 #define OR_TORADIANS 0.0174532924f  /* math.radians factor */
