@@ -133,6 +133,10 @@ struct Device {
   bool raw_valid = false;
   DevScene last_sc{};
   bool bound = false;
+  // side stream of the permeation job: it runs beside the raytrace stage (the reference schedules
+  // the two jobs independently, AudioRayTracer.cs:191,213), joined before the reduce job (:237)
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
   std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
 };
@@ -540,19 +544,39 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     nhit = reinterpret_cast<unsigned long long*>(static_cast<uint8_t*>(dv.counts.p) + sizeof(DevCounts));
     HIP_TRY(c, hipMemsetAsync(dv.counts.p, 0, sizeof(DevCounts) + 16, st));
   }
-  auto tstart = [&](int kind) -> size_t {
+  auto tstart = [&](int kind, hipStream_t on) -> size_t {
     size_t i = dv.ev_used.size() * 2;
     hipEvent_t e = pool_event(dv, i);
     pool_event(dv, i + 1);
-    if (e) (void)hipEventRecord(e, st);
+    if (e) (void)hipEventRecord(e, on);
     dv.ev_used.push_back({kind, i});
     return i;
   };
-  auto tstop = [&](size_t i) { hipEvent_t e = pool_event(dv, i + 1); if (e) (void)hipEventRecord(e, st); };
+  auto tstop = [&](size_t i, hipStream_t on) { hipEvent_t e = pool_event(dv, i + 1); if (e) (void)hipEventRecord(e, on); };
+
+  // The permeation job (read-only scene and origins, writes only the fans' permeation sections)
+  // runs on the side stream concurrently with the raytrace stage, whose kernels leave CUs idle in
+  // their tails; the reduce job waits for both. Counting frames stay serial.
+  const bool both = (f.stages & ART_STAGE_RAYTRACE) && (f.stages & ART_STAGE_PERMEATE);
+  const bool overlap = both && !count;
+  if (overlap) {
+    if (!dv.side) {
+      HIP_TRY(c, hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking));
+      HIP_TRY(c, hipEventCreateWithFlags(&dv.fork, hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&dv.join, hipEventDisableTiming));
+    }
+    HIP_TRY(c, hipEventRecord(dv.fork, st));
+    HIP_TRY(c, hipStreamWaitEvent(dv.side, dv.fork, 0));
+    size_t ti = timing ? tstart(1, dv.side) : 0;
+    launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, dv.side);
+    if (timing) tstop(ti, dv.side);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(dv.join, dv.side));
+  }
 
   if (f.stages & ART_STAGE_RAYTRACE) {
     HIP_TRY(c, hipMemsetAsync(acc, 0, acc_bytes, st));
-    size_t ti = timing ? tstart(0) : 0;
+    size_t ti = timing ? tstart(0, st) : 0;
     // The counting variant sweeps colliders in exact reference order per lane (its per-lane
     // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
     const int* order = reinterpret_cast<const int*>(raw + f.off_order);
@@ -584,13 +608,14 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
                              acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st);
       }
     }
-    if (timing) tstop(ti);
+    if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
   }
-  if (f.stages & ART_STAGE_PERMEATE) {
-    size_t ti = timing ? tstart(1) : 0;
+  if (overlap) HIP_TRY(c, hipStreamWaitEvent(st, dv.join, 0));
+  if ((f.stages & ART_STAGE_PERMEATE) && !overlap) {
+    size_t ti = timing ? tstart(1, st) : 0;
     launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, st);
-    if (timing) tstop(ti);
+    if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
     if (count) {
       launch_perm_count(dv.sc, fp, d_origins, counts, nhit, st);
@@ -598,9 +623,9 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     }
   }
   if (f.stages & (ART_STAGE_RAYTRACE | ART_STAGE_REDUCE)) {
-    size_t ti = timing ? tstart(2) : 0;
+    size_t ti = timing ? tstart(2, st) : 0;
     launch_reduce(dv.sc, fp, f.L, d_block, acc, muffle_reset, st);
-    if (timing) tstop(ti);
+    if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
   }
   return ART_OK;
@@ -734,6 +759,10 @@ ART_API void art_destroy(art_ctx* c) {
     if (dv.launch_done) (void)hipEventDestroy(dv.launch_done);
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
+    if (dv.side) (void)hipStreamSynchronize(dv.side);
+    if (dv.fork) (void)hipEventDestroy(dv.fork);
+    if (dv.join) (void)hipEventDestroy(dv.join);
+    if (dv.side) (void)hipStreamDestroy(dv.side);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
   }
   c->h_in.release();
