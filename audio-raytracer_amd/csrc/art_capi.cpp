@@ -137,6 +137,7 @@ struct Device {
   // the two jobs independently, AudioRayTracer.cs:191,213), joined before the reduce job (:237)
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  SideStream echo;  // the echo visibility beside the pair sort and the muffle sweep
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
   std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
 };
@@ -593,6 +594,11 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         fpx.exec = static_cast<unsigned long long*>(dv.exec.p);
         dv.exec_launches++;
       }
+      if (!dv.echo.st) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&dv.echo.st, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.fork, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.join, hipEventDisableTiming));
+      }
       // The pair arrays index pairs with 32-bit slots (sorted below 2^31) and the echo outputs with
       // 32-bit half offsets into the block: larger frames run as consecutive fan chunks on the
       // stream (the pair buffer and counter are reused, the muffle accumulators offset per chunk).
@@ -605,7 +611,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         fpc.S = std::min(chunk, fan_count - b0);
         if (b0) HIP_TRY(c, hipMemsetAsync(pair_count, 0, 16, st));
         launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
-                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st);
+                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, dv.echo);
       }
     }
     if (timing) tstop(ti, st);
@@ -763,6 +769,10 @@ ART_API void art_destroy(art_ctx* c) {
     if (dv.fork) (void)hipEventDestroy(dv.fork);
     if (dv.join) (void)hipEventDestroy(dv.join);
     if (dv.side) (void)hipStreamDestroy(dv.side);
+    if (dv.echo.st) (void)hipStreamSynchronize(dv.echo.st);
+    if (dv.echo.fork) (void)hipEventDestroy(dv.echo.fork);
+    if (dv.echo.join) (void)hipEventDestroy(dv.echo.join);
+    if (dv.echo.st) (void)hipStreamDestroy(dv.echo.st);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
   }
   c->h_in.release();

@@ -165,9 +165,15 @@ size_t fast_pair_bytes(const FrameParams& fp);
 int fast_fans_per_launch(int R, int H, int T, uint32_t stride);
 // The throughput raytrace stage (art_trace.hip): per bounce nearest_first_kernel + path_kernel,
 // then the pair sort, vis_kernel and vis_finalize. Any target count, every DevScene with a BVH.
+// echo_st (optional, with two events): the echo visibility runs there, beside the pair sort and the
+// muffle sweep on st, joined before vis_finalize.
+struct SideStream {
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf,
-                          uint32_t* pair_count, hipStream_t st);
+                          uint32_t* pair_count, hipStream_t st, const SideStream& echo);
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, const int2* slot_batch, hipStream_t st);
 void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,

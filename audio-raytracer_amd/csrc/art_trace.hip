@@ -1260,7 +1260,7 @@ int fast_fans_per_launch(int R, int H, int T, uint32_t stride) {
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf, uint32_t* pair_count,
-                          hipStream_t st) {
+                          hipStream_t st, const SideStream& echo) {
   if (fp.S == 0) return;
   const PairBufs pb = pair_bufs(pair_buf, fp);
   const size_t mcap = muffle_cap_of(fp), max_pairs = (size_t)pb.vp.echo_cap + mcap;
@@ -1284,6 +1284,27 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   }
   const uint32_t nb_max = (uint32_t)(pb.vp.echo_cap / 64 + (mcap + 63) / 64);
   if (!nb_max) return;
+  const uint32_t eb = pb.vp.echo_cap / 64;  // echo batches (one workgroup each)
+  const uint32_t nbm = nb_max - eb;         // muffle batches (vis_ranges items each, 4 per workgroup)
+  const size_t mblocks = ((size_t)nbm * vis_ranges(sc) + 3) / 4;
+#define ART_VIS(S_, BLOCKS_, NECHO_, EX_, OBB_)                                                                  \
+  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, nbm, \
+                     EX_ ? fp.exec : nullptr, NECHO_)
+#define ART_VIS_ANY(S_, BLOCKS_, NECHO_)                                                                          \
+  do {                                                                                                           \
+    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, true, true); else ART_VIS(S_, BLOCKS_, NECHO_, true, false); } \
+    else { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, false, true); else ART_VIS(S_, BLOCKS_, NECHO_, false, false); }    \
+  } while (0)
+  // The echo traversal (latency-bound) needs only the path kernel's pairs: on the side stream it
+  // runs beside the pair sort and the VALU-bound muffle sweep; without a side stream both halves
+  // share one vis_kernel launch (echo workgroups first).
+  const bool split = echo.st && eb && mcap;
+  if (split) {
+    (void)hipEventRecord(echo.fork, st);
+    (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+    ART_VIS_ANY(echo.st, eb, eb);
+    (void)hipEventRecord(echo.join, echo.st);
+  }
   if (mcap) {
     hipLaunchKernelGGL(pair_hist_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.hist, pb.nblk,
                        pb.nbins);
@@ -1292,19 +1313,14 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     hipLaunchKernelGGL(pair_scatter_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.prefix, pb.tot,
                        pb.vp.mrec, pb.vp.msorted, pb.nblk, pb.nbins);
   }
-  // echo batches by quad BVH traversal, the muffle batches by the sweep (4 items per workgroup)
-  const uint32_t eb = pb.vp.echo_cap / 64;
-  const uint32_t nbm = nb_max - eb;  // muffle batches
-  const size_t vitems = (size_t)nbm * vis_ranges(sc);
-  const size_t blocks = eb + (vitems + 3) / 4;
-  if (blocks) {
-#define ART_VIS(EX_, OBB_)                                                                                         \
-  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)blocks), dim3(256), 0, st, sc, pb.vp, pair_count, nbm,     \
-                     EX_ ? fp.exec : nullptr, eb)
-    if (fp.exec) { if (obb) ART_VIS(true, true); else ART_VIS(true, false); }
-    else { if (obb) ART_VIS(false, true); else ART_VIS(false, false); }
-#undef ART_VIS
+  if (split) {
+    ART_VIS_ANY(st, mblocks, 0u);
+    (void)hipStreamWaitEvent(st, echo.join, 0);
+  } else if (eb + mblocks) {
+    ART_VIS_ANY(st, eb + mblocks, eb);
   }
+#undef ART_VIS_ANY
+#undef ART_VIS
   hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
                      muffle_acc);
 }
