@@ -555,13 +555,16 @@ def main():
             art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
 
     torch.cuda.synchronize()
-    tw = time.perf_counter()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     steps = a.steps
     if steps <= 0:  # about 1.5 s of timed work, so the driver's sampler sees the GPU busy
-        per = (time.perf_counter() - tw) / max(1, a.warmup)
+        tp = time.perf_counter()  # per-step time from 10 steps after the warmup (first-call costs excluded)
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - tp) / 10
         steps = int(min(5000, max(20, 1.5 / max(per, 1e-6))))
         if world > 1:
             t = torch.tensor([steps], dtype=torch.int64, device=dev)
