@@ -884,6 +884,8 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
       for (Device& e : c->devs) {
         (void)hipSetDevice(e.id);
         (void)hipStreamSynchronize(e.stream);
+        if (e.side) (void)hipStreamSynchronize(e.side);  // a forked stage may not have joined
+        if (e.echo.st) (void)hipStreamSynchronize(e.echo.st);
       }
       return rc;
     }
