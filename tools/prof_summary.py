@@ -80,7 +80,7 @@ def main():
             v = per[k].get(c, [])
             return sum(v) / len(v) if v else 0.0
         # launches per frame: multi-hit frames run nearest_first_kernel and path_kernel once per
-        # bounce; vis_kernel runs once per frame
+        # bounce; vis_kernel twice (echo launch on the side stream, muffle sweep launch)
         ref = max((len(v.get("FETCH_SIZE", [])) for k, v in per.items() if k.startswith("pair_hist_kernel")), default=1) or 1
 
         def per_frame(k, c):  # mean per dispatch x dispatches per frame (rounded ratio to pair_hist_kernel's)
