@@ -531,7 +531,8 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   fp.muf_curve = reinterpret_cast<const float*>(raw + f.off_muf);
   const int2* slot_batch = reinterpret_cast<const int2*>(raw + f.off_tab);
   const uint8_t* muffle_reset = raw + f.off_reset;
-  // muffle accumulators, then (16-B aligned) the visibility pair counter: one memset clears both
+  // muffle accumulators, then (16-B aligned) the visibility pair counters: cleared by the first
+  // nearest_first_kernel of each fast-path chunk, by one memset before the reference-order kernel
   const size_t acc_words = ((size_t)fan_count * f.TC * f.T + 3) & ~(size_t)3;
   const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16;
   if (!dv.acc.reserve(acc_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
@@ -576,12 +577,12 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   }
 
   if (f.stages & ART_STAGE_RAYTRACE) {
-    HIP_TRY(c, hipMemsetAsync(acc, 0, acc_bytes, st));
     size_t ti = timing ? tstart(0, st) : 0;
     // The counting variant sweeps colliders in exact reference order per lane (its per-lane
     // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
     const int* order = reinterpret_cast<const int*>(raw + f.off_order);
     if (count || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER)) {
+      HIP_TRY(c, hipMemsetAsync(acc, 0, acc_bytes, st));
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
     } else {
       FrameParams fpx = fp;
@@ -609,7 +610,6 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       for (int b0 = 0; b0 < fan_count; b0 += chunk) {
         FrameParams fpc = fpx;
         fpc.S = std::min(chunk, fan_count - b0);
-        if (b0) HIP_TRY(c, hipMemsetAsync(pair_count, 0, 16, st));
         launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
                              acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, dv.echo);
       }

@@ -324,7 +324,8 @@ __device__ __forceinline__ uint32_t* live_list(float4* state, int ngroups) {
 template <bool EX, bool OBB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
-    int2* __restrict__ hits, float4* __restrict__ state, int step) {
+    int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
+    uint32_t* __restrict__ counters) {
   __shared__ uint32_t s_stk[kBvhStack * 64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
@@ -354,6 +355,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
   } else {
     if (state && blockIdx.x == 0 && threadIdx.x < kLiveCounters)  // multi-hit frame: clear the counters
       live_list(state, ngroups)[(size_t)ngroups * 64 + threadIdx.x] = 0u;
+    // the frame's muffle accumulators and pair counters, consumed only by later launches (no
+    // memset dispatch between frames)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
+    if (counters && blockIdx.x == 0 && threadIdx.x < 4) counters[threadIdx.x] = 0u;
     const int fan = g / nrb;
     const int slot = (g - fan * nrb) * 64 + rr;
     alive = slot < fp.R;
@@ -1268,10 +1273,11 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const unsigned path_blocks = (groups + kPathWaves - 1) / kPathWaves;
   const bool multi = fp.H > 1;
   const bool obb = sc.no > 0;  // OBB-free scenes run instantiations without the OBB tests
+  const uint32_t nacc = (uint32_t)((size_t)fp.S * fp.TC * fp.T);  // this chunk's muffle accumulators
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
 #define ART_NEAREST(EX_, OBB_)                                                                                      \
   hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
-                     pb.state, k)
+                     pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr)
     if (fp.exec) { if (obb) ART_NEAREST(true, true); else ART_NEAREST(true, false); }
     else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
 #undef ART_NEAREST
