@@ -413,12 +413,21 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
   uint32_t zeros = 0;
   for (int base = 0; base < n; base += kChunkF) {
     const int m = min(kChunkF, n - base);
-    for (int i0 = 0; i0 < m; i0 += 64) {
-      const int i = i0 + lane;
-      const bool in = i < m;
-      const float e = in ? f16tof32(echo[base + i]) : 0.0f;
-      if (in) s_f[i] = e;
-      zeros += __popcll(__ballot(in && e == 0.0f));
+    for (int i0 = 0; i0 < m; i0 += 8 * 64) {  // 8 independent loads per lane in flight
+      uint16_t h[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 64 * j + lane;
+        h[j] = i < m ? echo[base + i] : (uint16_t)0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 64 * j + lane;
+        const bool in = i < m;
+        const float e = f16tof32(h[j]);
+        if (in) s_f[i] = e;
+        zeros += __popcll(__ballot(in && e == 0.0f));
+      }
     }
     __syncthreads();
     if (lane == 0) {
