@@ -551,9 +551,12 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       const int rank = bc >> 28;
       idx = bc & 0x0fffffff;
       type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
-      // exact (Unity min/max) re-evaluation: a zero distance keeps the reference's sign
-      if (type == kAabb) aabb_test<true>(s, sc.aabb[idx], dist);
-      if (type == kObb) { const ObbRec r = sc.obb[idx]; obb_test<true>(s, r, stored_q(r), dist); }
+      // exact (Unity min/max) re-evaluation of a zero distance: IEEE and Unity min/max differ only
+      // in the sign of an equal-magnitude zero pair, so only a zero result can differ (its sign)
+      if (dist == 0.0f) {
+        if (type == kAabb) aabb_test<true>(s, sc.aabb[idx], dist);
+        if (type == kObb) { const ObbRec r = sc.obb[idx]; obb_test<true>(s, r, stored_q(r), dist); }
+      }
       o = o + d * dist;  // :111
       life -= dist;      // :112
       hits += 1;         // :113
