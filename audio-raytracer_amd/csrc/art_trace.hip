@@ -289,6 +289,14 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
   // run with most quads busy. The order in which leaves are tested does not change the minimum.
   int pend = -1;
   while (__any(g >= 0 || pend >= 0)) {
+    {  // Wave priority by unfinished rays: the waves with the most rays left (the ones that set the
+       // kernel's length) issue first, the nearly finished ones fill the gaps (s_setprio, 0..3)
+      const int act = __popcll(__ballot((g >= 0 || pend >= 0) && qd == 0));
+      if (act > 12) __builtin_amdgcn_s_setprio(3);
+      else if (act > 8) __builtin_amdgcn_s_setprio(2);
+      else if (act > 4) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     for (;;) {
       if (g >= leaf0 && pend < 0) { pend = g; pop(); }
       const bool inner = g >= 0 && g < leaf0;
@@ -777,6 +785,7 @@ __global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16
                                                                     float4* __restrict__ msorted, int nblk, int nbins) {
   __shared__ uint32_t cur[kSortBins];
   __shared__ uint32_t s_part[kSortThreads];
+  __builtin_amdgcn_s_setprio(3);  // on the critical path; issues ahead of the echo traversal beside it
   constexpr int kPer = kSortBins / kSortThreads;
   const int t = threadIdx.x;
   uint32_t v[kPer], sum = 0;
@@ -1042,6 +1051,7 @@ template <bool OBB>
 __device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
                                                uint32_t nbm, unsigned long long* ex, uint32_t blk) {
   const int lane = threadIdx.x & 63;
+  __builtin_amdgcn_s_setprio(1);  // the sweep ends the frame's critical path; the echo waves beside it have slack
   const uint32_t item = blk * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t r = item / nbm, b = item - r * nbm;
   const int nranges = vis_ranges(sc);
