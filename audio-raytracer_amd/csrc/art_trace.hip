@@ -323,9 +323,13 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
 constexpr int kLiveCounters = 32;  // per-bounce live-list counters (H <= 32)
 
 // Ray state between bounce launches: [groups * 64][2] float4 (o, life | d, hits | alive << 8),
-// then the live list u32[groups * 64] and its per-bounce counters u32[kLiveCounters].
+// then the live list u32[groups * 64], its per-bounce counters u32[kLiveCounters] and the echo
+// pairs each bounce emitted u32[kLiveCounters] (bounce k's echo pairs follow bounce k-1's).
 __device__ __forceinline__ uint32_t* live_list(float4* state, int ngroups) {
   return reinterpret_cast<uint32_t*>(state + 2 * (size_t)ngroups * 64);
+}
+__device__ __forceinline__ uint32_t* echo_counts(float4* state, int ngroups) {
+  return live_list(state, ngroups) + (size_t)ngroups * 64 + kLiveCounters;
 }
 
 // EX: count the executed tests (fp.exec); OBB: the scene has OBBs.
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
     write = ok;
     out = i;
   } else {
-    if (state && blockIdx.x == 0 && threadIdx.x < kLiveCounters)  // multi-hit frame: clear the counters
+    if (state && blockIdx.x == 0 && threadIdx.x < 2 * kLiveCounters)  // multi-hit frame: clear the counters
       live_list(state, ngroups)[(size_t)ngroups * 64 + threadIdx.x] = 0u;
     // the frame's muffle accumulators and pair counters, consumed only by later launches (no
     // memset dispatch between frames)
@@ -493,6 +497,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int k = 0; k < K; ++k) t += s_agg[par][k][threadIdx.x];
       s_aggb[par][threadIdx.x] = t ? atomicAdd(&counter[threadIdx.x], t) : 0u;
+      if (MULTI && threadIdx.x == 0 && t) atomicAdd(echo_counts(state, ngroups) + step, t);  // bounce step's echoes
     }
     __syncthreads();
     b0 = s_aggb[par][0];
@@ -1098,10 +1103,19 @@ __device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPair
 // ------------------------------------------------------------------------------------------
 template <bool OBB>
 __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                              unsigned long long* ex, uint32_t blk, uint32_t* s_stk) {
+                                              unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
+                                              const uint32_t* ecnt, int bounce) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
   const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64-pair batch
-  const uint32_t base = blk * 64u, n = ldc(count, 0);
+  // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
+  uint32_t start = 0u, n;
+  if (bounce < 0) {
+    n = ldc(count, 0);
+  } else {
+    for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
+    n = start + ldc(ecnt, bounce);
+  }
+  const uint32_t base = start + blk * 64u;
   if (sc.bvh_levels == 0) return;                              // no colliders: nothing blocks
   if (base + (uint32_t)(w * 16) >= n) return;                  // this wave's 16 segments are past the emitted pairs
   const bool valid = base + (uint32_t)slot < n;
@@ -1170,10 +1184,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 template <bool EX, bool OBB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nbm, unsigned long long* ex,
-                uint32_t n_echo) {
+                uint32_t n_echo, const uint32_t* __restrict__ ecnt, int bounce) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
   unsigned long long* e = EX ? ex : nullptr;
-  if (blockIdx.x < n_echo) vis_quad_body<OBB>(sc, vp, count, e, blockIdx.x, s_stk);
+  if (blockIdx.x < n_echo) vis_quad_body<OBB>(sc, vp, count, e, blockIdx.x, s_stk, ecnt, bounce);
   else vis_sweep_body<OBB>(sc, vp, count, nbm, e, blockIdx.x - n_echo);
 }
 
@@ -1242,7 +1256,7 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   b.vp.echo_cap = (uint32_t)ecap;
   b.vp.tbits = target_bits(fp.T);
   b.pre = reinterpret_cast<int2*>(take(slots * sizeof(int2)));
-  if (fp.H > 1) b.state = reinterpret_cast<float4*>(take(slots * (2 * sizeof(float4) + 4) + kLiveCounters * 4));
+  if (fp.H > 1) b.state = reinterpret_cast<float4*>(take(slots * (2 * sizeof(float4) + 4) + 2 * kLiveCounters * 4));
   if (mcap) {
     b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
     b.nbins = fp.T << sort_dir_bits(fp.T);  // keys (target << bits | cell) < T << bits <= kSortBins
@@ -1287,6 +1301,27 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const bool multi = fp.H > 1;
   const bool obb = sc.no > 0;  // OBB-free scenes run instantiations without the OBB tests
   const uint32_t nacc = (uint32_t)((size_t)fp.S * fp.TC * fp.T);  // this chunk's muffle accumulators
+  const uint32_t nb_max = (uint32_t)(pb.vp.echo_cap / 64 + (mcap + 63) / 64);
+  const uint32_t eb = pb.vp.echo_cap / 64;  // echo batches (one workgroup each)
+  const uint32_t nbm = nb_max - eb;         // muffle batches (vis_ranges items each, 4 per workgroup)
+  const size_t mblocks = ((size_t)nbm * vis_ranges(sc) + 3) / 4;
+  uint32_t* ecnt = pb.state ? reinterpret_cast<uint32_t*>(pb.state + 2 * (size_t)groups * 64) + (size_t)groups * 64 + kLiveCounters
+                            : nullptr;  // per-bounce echo counts (echo_counts)
+#define ART_VIS(S_, BLOCKS_, NECHO_, B_, EX_, OBB_)                                                                \
+  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, nbm, \
+                     EX_ ? fp.exec : nullptr, NECHO_, ecnt, B_)
+#define ART_VIS_ANY(S_, BLOCKS_, NECHO_, B_)                                                                      \
+  do {                                                                                                           \
+    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, B_, true, true); else ART_VIS(S_, BLOCKS_, NECHO_, B_, true, false); } \
+    else { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, B_, false, true); else ART_VIS(S_, BLOCKS_, NECHO_, B_, false, false); }    \
+  } while (0)
+  // The echo traversal (latency-bound) needs only the path kernel's pairs, so it runs on the side
+  // stream: in multi-hit frames each bounce's echoes right after that bounce's path kernel, beside
+  // the next bounces' nearest traversals (their tails leave CUs idle) and then the pair sort; in
+  // one-hit frames beside the pair sort and the VALU-bound muffle sweep. Without a side stream both
+  // halves share one vis_kernel launch (echo workgroups first).
+  const bool split = echo.st && eb && mcap;
+  const bool per_bounce = split && multi && ecnt;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
 #define ART_NEAREST(EX_, OBB_)                                                                                      \
   hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
@@ -1300,30 +1335,19 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
     else { if (multi) ART_PATH(false, true); else ART_PATH(false, false); }
 #undef ART_PATH
+    if (per_bounce) {  // this bounce's echoes (at most one per ray slot: `groups` batches)
+      (void)hipEventRecord(echo.fork, st);
+      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+      ART_VIS_ANY(echo.st, groups, groups, k);
+    }
   }
-  const uint32_t nb_max = (uint32_t)(pb.vp.echo_cap / 64 + (mcap + 63) / 64);
   if (!nb_max) return;
-  const uint32_t eb = pb.vp.echo_cap / 64;  // echo batches (one workgroup each)
-  const uint32_t nbm = nb_max - eb;         // muffle batches (vis_ranges items each, 4 per workgroup)
-  const size_t mblocks = ((size_t)nbm * vis_ranges(sc) + 3) / 4;
-#define ART_VIS(S_, BLOCKS_, NECHO_, EX_, OBB_)                                                                  \
-  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, nbm, \
-                     EX_ ? fp.exec : nullptr, NECHO_)
-#define ART_VIS_ANY(S_, BLOCKS_, NECHO_)                                                                          \
-  do {                                                                                                           \
-    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, true, true); else ART_VIS(S_, BLOCKS_, NECHO_, true, false); } \
-    else { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, false, true); else ART_VIS(S_, BLOCKS_, NECHO_, false, false); }    \
-  } while (0)
-  // The echo traversal (latency-bound) needs only the path kernel's pairs: on the side stream it
-  // runs beside the pair sort and the VALU-bound muffle sweep; without a side stream both halves
-  // share one vis_kernel launch (echo workgroups first).
-  const bool split = echo.st && eb && mcap;
-  if (split) {
+  if (split && !per_bounce) {
     (void)hipEventRecord(echo.fork, st);
     (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-    ART_VIS_ANY(echo.st, eb, eb);
-    (void)hipEventRecord(echo.join, echo.st);
+    ART_VIS_ANY(echo.st, eb, eb, -1);
   }
+  if (split) (void)hipEventRecord(echo.join, echo.st);
   if (mcap) {
     hipLaunchKernelGGL(pair_hist_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.hist, pb.nblk,
                        pb.nbins);
@@ -1333,10 +1357,10 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                        pb.vp.mrec, pb.vp.msorted, pb.nblk, pb.nbins);
   }
   if (split) {
-    ART_VIS_ANY(st, mblocks, 0u);
+    ART_VIS_ANY(st, mblocks, 0u, -1);
     (void)hipStreamWaitEvent(st, echo.join, 0);
   } else if (eb + mblocks) {
-    ART_VIS_ANY(st, eb + mblocks, eb);
+    ART_VIS_ANY(st, eb + mblocks, eb, -1);
   }
 #undef ART_VIS_ANY
 #undef ART_VIS
