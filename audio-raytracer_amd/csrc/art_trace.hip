@@ -482,6 +482,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
   __shared__ uint32_t s_aggb[2][2];
   __shared__ uint32_t s_live[2][K], s_liveb[2];
   int agg_round = 0;  // block-uniform reservation round (the LDS buffers alternate by its parity)
+  __builtin_amdgcn_s_setprio(3);  // on the critical path; in multi-hit frames the echo traversal runs beside it
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;  // 64-ray groups per fan
   const int ngroups = fp.S * nrb;
