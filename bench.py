@@ -615,6 +615,10 @@ def main():
             ctx.run(frame)
             if i >= 5:
                 frame_ms.append((time.perf_counter() - t1) * 1e3)
+    # release this context (its streams) before the dynamic measurement opens its own: HIP maps a
+    # process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and a second live context's
+    # side streams would share a queue with its main stream (streams)
+    ctx.close()
 
     dyn = None
     if rank == 0 and world == 1 and not a.no_dynamic:
