@@ -52,6 +52,13 @@ ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
+# art_fan.ray_hit_ids: ColliderType (Enums/ColliderType.cs) << 30 | index in that type's array
+ART_COLLIDER_AABB, ART_COLLIDER_OBB, ART_COLLIDER_SPHERE = 1, 2, 3
+ART_HIT_NONE = 0xFFFFFFFF
+
+
+def hit_id(ctype: int, index: int) -> int:
+    return (ctype << 30) | index
 
 ART_OWN_SPHERE, ART_OWN_AABB, ART_OWN_OBB = 0, 1, 2
 
@@ -84,7 +91,7 @@ class art_frame_desc(C.Structure):
 class art_fan(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("echo_ray_distances", C.c_void_p), ("muffle_ray_hits", C.c_void_p),
                 ("permeation_power_remains", C.c_void_p), ("settings", C.c_void_p), ("dsp_params", C.c_void_p),
-                ("ray_hit_points", C.c_void_p), ("ray_hit_counts", C.c_void_p)]
+                ("ray_hit_points", C.c_void_p), ("ray_hit_counts", C.c_void_p), ("ray_hit_ids", C.c_void_p)]
 
 
 class art_test_counts(C.Structure):
@@ -97,7 +104,7 @@ class art_test_counts(C.Structure):
 
 class art_fan_layout(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("stride", "settings_off", "dsp_off", "muffle_off", "perm_off", "echo_off",
-                                           "hit_points_off", "hit_counts_off")]
+                                           "hit_points_off", "hit_counts_off", "hit_ids_off")]
 
 
 class art_kernel_times(C.Structure):

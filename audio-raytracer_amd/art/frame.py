@@ -4,7 +4,7 @@
 (RayDirections, AABB/OBB/SphereColliders, AudioTargetPositions), `FrameParams` the serialized
 scalars (AudioRayTracer.cs:9-35, AudioRaytracingManager.cs:13-19), `FanOutputs` the per-fan
 NativeArrays (EchoRayDistances, MuffleRayHits, PermeationPowerRemains, AudioTargetSettings,
-RayHitResults, RayHitResultCounts). `Context.schedule()` / `JobHandle.complete()` are the
+RayHitResults, RayHitResultCounts, and the build's hit identities). `Context.schedule()` / `JobHandle.complete()` are the
 Schedule / Complete surface over the C ABI (include/art.h).
 """
 from __future__ import annotations
@@ -104,6 +104,7 @@ class FanOutputs:
         self.dsp = np.zeros((S, T), abi.DSP_PARAMS) if dsp else None
         self.hit_points = np.zeros((S, R * H, 3), np.uint16) if hits else None
         self.hit_counts = np.zeros((S, R), np.uint8) if hits else None
+        self.hit_ids = np.full((S, R * H), abi.ART_HIT_NONE, np.uint32) if hits else None
 
     def copy(self) -> "FanOutputs":
         o = FanOutputs.__new__(FanOutputs)
@@ -119,6 +120,7 @@ class FanOutputs:
         if self.hit_points is not None:
             self.hit_points[:] = rng.integers(0, 0x7BFF, self.hit_points.shape, dtype=np.uint16)
             self.hit_counts[:] = rng.integers(0, 200, self.hit_counts.shape, dtype=np.uint8)
+            self.hit_ids[:] = rng.integers(0, 2 ** 32, self.hit_ids.shape, dtype=np.uint32)
         return self
 
     def equal(self, other: "FanOutputs") -> dict:
@@ -133,6 +135,7 @@ class FanOutputs:
         if self.hit_points is not None and other.hit_points is not None:
             res["hit_points"] = np.array_equal(self.hit_points, other.hit_points)
             res["hit_counts"] = np.array_equal(self.hit_counts, other.hit_counts)
+            res["hit_ids"] = np.array_equal(self.hit_ids, other.hit_ids)
         return res
 
 
@@ -186,6 +189,7 @@ class Frame:
             f.dsp_params = out.dsp[i].ctypes.data if out.dsp is not None else None
             f.ray_hit_points = out.hit_points[i].ctypes.data if out.hit_points is not None else None
             f.ray_hit_counts = out.hit_counts[i].ctypes.data if out.hit_counts is not None else None
+            f.ray_hit_ids = out.hit_ids[i].ctypes.data if out.hit_ids is not None else None
         self.fans = fans
         self.S = S
 
@@ -336,6 +340,7 @@ def unpack_block(block: np.ndarray, layout: dict, S: int, R: int, H: int, T: int
     if hits:
         out.hit_points[:] = sec(layout["hit_points_off"], R * H * 6, np.uint16).reshape(S, R * H, 3)
         out.hit_counts[:] = sec(layout["hit_counts_off"], R, np.uint8)
+        out.hit_ids[:] = sec(layout["hit_ids_off"], R * H * 4, np.uint32)
     return out
 
 
@@ -358,4 +363,5 @@ def pack_block(out: FanOutputs, layout: dict) -> np.ndarray:
     if out.hit_points is not None:
         put(layout["hit_points_off"], out.hit_points)
         put(layout["hit_counts_off"], out.hit_counts)
+        put(layout["hit_ids_off"], out.hit_ids)
     return b.reshape(-1)

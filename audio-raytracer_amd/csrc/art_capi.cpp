@@ -42,7 +42,7 @@ static_assert(sizeof(art_dsp_params) == 24, "art_dsp_params");
 
 namespace {
 
-constexpr uint32_t kAbiVersion = (1u << 16) | 0u;
+constexpr uint32_t kAbiVersion = (2u << 16) | 0u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
@@ -244,6 +244,7 @@ FanLayout make_layout(const art_frame_desc* d, uint32_t out_flags) {
   L.echo_off = (uint32_t)off; off = align_up(off + RH * 2, 16);
   L.hit_points_off = (uint32_t)off; off = align_up(off + (L.has_hits ? RH * sizeof(art_half3) : 0), 16);
   L.hit_counts_off = (uint32_t)off; off = align_up(off + (L.has_hits ? (size_t)d->ray_count : 0), 16);
+  L.hit_ids_off = (uint32_t)off; off = align_up(off + (L.has_hits ? RH * sizeof(uint32_t) : 0), 16);
   L.stride = (uint32_t)off;
   return L;
 }
@@ -656,7 +657,7 @@ int read_counts(art_ctx* c, Device& dv, hipStream_t st, art_test_counts* out, bo
 
 bool fan_wants_hits(const art_fan* fans, int n) {
   for (int i = 0; i < n; ++i)
-    if (fans[i].ray_hit_points || fans[i].ray_hit_counts) return true;
+    if (fans[i].ray_hit_points || fans[i].ray_hit_counts || fans[i].ray_hit_ids) return true;
   return false;
 }
 
@@ -798,6 +799,7 @@ ART_API int art_fan_layout_get(const art_frame_desc* d, uint32_t out_flags, art_
   out->stride = L.stride; out->settings_off = L.settings_off; out->dsp_off = L.dsp_off; out->muffle_off = L.muffle_off;
   out->perm_off = L.perm_off; out->echo_off = L.echo_off; out->hit_points_off = L.hit_points_off;
   out->hit_counts_off = L.hit_counts_off;
+  out->hit_ids_off = L.hit_ids_off;
   return ART_OK;
 }
 
@@ -859,6 +861,8 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
       if (L.has_hits) {
         if (fn.ray_hit_points) memcpy(rec + L.hit_points_off, fn.ray_hit_points, RH * sizeof(art_half3));
         else memset(rec + L.hit_points_off, 0, RH * sizeof(art_half3));
+        if (fn.ray_hit_ids) memcpy(rec + L.hit_ids_off, fn.ray_hit_ids, RH * sizeof(uint32_t));
+        else memset(rec + L.hit_ids_off, 0xFF, RH * sizeof(uint32_t));
       }
     }
     if (L.has_hits) {
@@ -942,6 +946,7 @@ ART_API int art_complete(art_ctx* c, art_handle h) {
     memcpy(fn.echo_ray_distances, rec + L.echo_off, RH * 2);
     if (L.has_hits && fn.ray_hit_points) memcpy(fn.ray_hit_points, rec + L.hit_points_off, RH * sizeof(art_half3));
     if (L.has_hits && fn.ray_hit_counts) memcpy(fn.ray_hit_counts, rec + L.hit_counts_off, (size_t)f.R);
+    if (L.has_hits && fn.ray_hit_ids) memcpy(fn.ray_hit_ids, rec + L.hit_ids_off, RH * sizeof(uint32_t));
   }
   if (c->counted) {
     memset(&c->last_counts, 0, sizeof c->last_counts);

@@ -155,6 +155,7 @@ void raytrace_batch(const Scene& sc, const Frame& f, const art_fan& fan, int sta
   for (int i = 0; i < cnt * H; ++i) {  // :72-80 (Q1: start + i, not start * H + i)
     fan.echo_ray_distances[start + i] = 0;
     if (fan.ray_hit_points) fan.ray_hit_points[start + i] = art_half3{0, 0, 0};
+    if (fan.ray_hit_ids) fan.ray_hit_ids[start + i] = ART_HIT_NONE;
   }
   for (int t = 0; t < T; ++t) fan.muffle_ray_hits[batch_id * T + t] = 0;  // :82-85
   const vec3 O = mk3(fan.origin[0], fan.origin[1], fan.origin[2]);
@@ -193,6 +194,7 @@ void raytrace_batch(const Scene& sc, const Frame& f, const art_fan& fan, int sta
         if (life < 0.0f) alive = false;
       }
       if (fan.ray_hit_points) fan.ray_hit_points[rid] = result;  // :197
+      if (fan.ray_hit_ids) fan.ray_hit_ids[rid] = ART_HIT_ID(type, idx);
       if (!alive) break;
     }
     if (fan.ray_hit_counts) fan.ray_hit_counts[ray] = (uint8_t)hits;  // :204, :212

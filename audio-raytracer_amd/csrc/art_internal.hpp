@@ -123,7 +123,7 @@ int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
 // Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
 struct FanLayout {
   uint32_t stride;
-  uint32_t settings_off, dsp_off, muffle_off, perm_off, echo_off, hit_points_off, hit_counts_off;
+  uint32_t settings_off, dsp_off, muffle_off, perm_off, echo_off, hit_points_off, hit_counts_off, hit_ids_off;
   int has_dsp, has_hits;
 };
 

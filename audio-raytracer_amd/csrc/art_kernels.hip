@@ -101,6 +101,7 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
   if (ray < fp.R) {
     uint16_t* echo = reinterpret_cast<uint16_t*>(fb + L.echo_off);
     art_half3* hpo = reinterpret_cast<art_half3*>(fb + L.hit_points_off);
+    uint32_t* hid = reinterpret_cast<uint32_t*>(fb + L.hit_ids_off);
     const int H = fp.H;  // <= 32 (validated on the host)
     const int my_slot = slot_of(ray);
     // Reset of this ray's slots (:72-80) under sequential-batch semantics. At TC == 1 every slot
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
         if (!keep) frozen |= 1u << k;
         if (!keep || any_reset) {
           echo[j] = 0;
-          if (HITS) hpo[j] = z;
+          if (HITS) { hpo[j] = z; hid[j] = ART_HIT_NONE; }
         }
       }
     }
@@ -142,6 +143,7 @@ __global__ __launch_bounds__(kRtBlock) void raytrace_kernel(DevScene sc, FramePa
         art_half3 p;
         p.x = f32tof16(o.x); p.y = f32tof16(o.y); p.z = f32tof16(o.z);
         hpo[rid] = p;
+        hid[rid] = ART_HIT_ID(h.type, h.idx);
       }
       // Echo — :124-145
       vec3 off = o - d * kEps;

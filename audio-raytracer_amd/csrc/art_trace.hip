@@ -515,6 +515,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
     uint8_t* fb = block + (size_t)fan * L.stride;
     uint16_t* echo = reinterpret_cast<uint16_t*>(fb + L.echo_off);
     art_half3* hpo = reinterpret_cast<art_half3*>(fb + L.hit_points_off);
+    uint32_t* hid = reinterpret_cast<uint32_t*>(fb + L.hit_ids_off);
     const bool single_slot = fp.TC == 1;
     const int my_slot = (int)(((long long)((ray / fp.bs) * fp.bs) * fp.TC) / fp.R);  // batchId (:63-64)
 
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
         if (!keep) frozen |= 1u << k;
         if (!single_slot && (!keep || any_reset) && step == 0) {
           echo[j] = 0;
-          if (HITS) hpo[j] = z;
+          if (HITS) { hpo[j] = z; hid[j] = ART_HIT_NONE; }
         }
       }
     }
@@ -581,6 +582,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       art_half3 p;
       p.x = f32tof16(o.x); p.y = f32tof16(o.y); p.z = f32tof16(o.z);
       hpo[ray * H + k] = p;
+      hid[ray * H + k] = ART_HIT_ID(type, idx);  // ShootRayCast's (hitColliderType, collider) :225-280
     }
 
     // visibility pairs: q = 0 echo ray to the origin (:124-145), q = 1..T muffle rays (:150-173),
@@ -706,7 +708,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
         const art_half3 z = {0, 0, 0};
         for (int kk = hits; kk < H; ++kk) {
           echo[ray * H + kk] = 0;
-          if (HITS) hpo[ray * H + kk] = z;
+          if (HITS) { hpo[ray * H + kk] = z; hid[ray * H + kk] = ART_HIT_NONE; }
         }
       }
       if (HITS) fb[L.hit_counts_off + ray] = (uint8_t)hits;  // :204, :212

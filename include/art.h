@@ -157,7 +157,19 @@ typedef struct {
     art_dsp_params* dsp_params;         /* [T] or NULL */
     art_half3* ray_hit_points;          /* [R*H] or NULL  RayHitResults (editor-only in the reference) */
     uint8_t* ray_hit_counts;            /* [R] or NULL    RayHitResultCounts (editor-only) */
+    uint32_t* ray_hit_ids;              /* [R*H] or NULL  (build extension) the collider each hit struck:
+                                         * ART_HIT_ID(type, index), written and reset exactly where
+                                         * RayHitResults is (:78, :197); ART_HIT_NONE in reset slots */
 } art_fan;
+
+/* Hit identity = the (hitColliderType, hitAABB / hitOBB / hitSphere) pair ShootRayCast returns
+ * (Jobs/AudioRaytracerJobBatched.cs:225-280): ColliderType (Enums/ColliderType.cs: AABB 1, OBB 2,
+ * Sphere 3) in the top two bits, the collider's index in its own array below. */
+#define ART_COLLIDER_AABB   1u
+#define ART_COLLIDER_OBB    2u
+#define ART_COLLIDER_SPHERE 3u
+#define ART_HIT_ID(type, index) (((uint32_t)(type) << 30) | (uint32_t)(index))
+#define ART_HIT_NONE 0xFFFFFFFFu
 
 /* Number of intersection-routine calls the reference algorithm executes (SURVEY.md §8 d). */
 typedef struct {

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define ART_OUT_HIT_RESULTS 0x1u /* also produce ray_hit_points / ray_hit_counts */
+#define ART_OUT_HIT_RESULTS 0x1u /* also produce ray_hit_points / ray_hit_counts / ray_hit_ids */
 
 typedef struct {
     uint32_t stride;          /* bytes per fan record, multiple of 16 */
@@ -31,6 +31,7 @@ typedef struct {
     uint32_t echo_off;        /* uint16_t (half) [R*H] */
     uint32_t hit_points_off;  /* art_half3[R*H] (iff ART_OUT_HIT_RESULTS) */
     uint32_t hit_counts_off;  /* uint8_t[R]     (iff ART_OUT_HIT_RESULTS) */
+    uint32_t hit_ids_off;     /* uint32_t[R*H]  (iff ART_OUT_HIT_RESULTS): ART_HIT_ID / ART_HIT_NONE */
 } art_fan_layout;
 
 typedef struct {

@@ -170,6 +170,7 @@ typedef struct {
     uint8_t MaxHitsPerRay;
     art_half3* RayHitResults;      /* may be NULL (editor-only) */
     uint8_t* RayHitResultCounts;   /* may be NULL (editor-only) */
+    uint32_t* RayHitIds;           /* may be NULL (build extension: ShootRayCast's type << 30 | index) */
     uint16_t* EchoRayDistances;
     uint16_t* MuffleRayHits; int MuffleRayHitsLength;
     float MaxMuffleHitDistance;
@@ -258,6 +259,18 @@ static int rt_shoot_ray_cast(const rt_job* j, f3 o, f3 d, rt_hit* hit)
         }
     }
     return hit->type != CT_NONE;
+}
+
+/* The (hitColliderType, collider) pair ShootRayCast returns (:225-280), as ART_HIT_ID: the
+ * collider's index is its position in the job's array of that type. */
+static uint32_t rt_hit_id(const rt_job* j, const rt_hit* hit)
+{
+    switch (hit->type) {
+    case CT_AABB: return ART_HIT_ID(CT_AABB, (uint32_t)(hit->aabb - j->AABBColliders));
+    case CT_OBB: return ART_HIT_ID(CT_OBB, (uint32_t)(hit->obb - j->OBBColliders));
+    case CT_SPHERE: return ART_HIT_ID(CT_SPHERE, (uint32_t)(hit->sphere - j->SphereColliders));
+    default: return ART_HIT_NONE;
+    }
 }
 
 /* CanRaySeePoint — :365-397 (echo any-hit, no owner skip) */
@@ -368,6 +381,7 @@ static void rt_execute(const rt_job* j, int rayStartIndex, int totalRays)
         int rayIndex = rayStartIndex + i;
         j->EchoRayDistances[rayIndex] = 0; /* (half)0 */
         if (j->RayHitResults) { art_half3 z = { 0, 0, 0 }; j->RayHitResults[rayIndex] = z; }
+        if (j->RayHitIds) j->RayHitIds[rayIndex] = ART_HIT_NONE;
     }
     /* :82-85 */
     for (int i = 0; i < j->TotalAudioTargets; i++) j->MuffleRayHits[batchId * j->TotalAudioTargets + i] = 0;
@@ -428,6 +442,7 @@ static void rt_execute(const rt_job* j, int rayStartIndex, int totalRays)
                     if (cRayLife < 0) isRayAlive = 0;
                 }
                 if (j->RayHitResults) j->RayHitResults[rayResultId] = rayResult; /* :197 */
+                if (j->RayHitIds) j->RayHitIds[rayResultId] = rt_hit_id(j, &hit);
             } else {
                 if (j->RayHitResultCounts) j->RayHitResultCounts[rayIndex] = cRayHits; /* :204 */
                 break;
@@ -682,7 +697,7 @@ static void run_fan(const art_frame_desc* d, const art_fan* f, counters* cnt)
         j.SphereColliders = d->sphere_colliders; j.SphereColliderCount = d->sphere_count;
         j.AudioTargetPositions = d->audio_target_positions; j.TotalAudioTargets = T;
         j.MaxRayLife = d->max_ray_life; j.MaxHitsPerRay = (uint8_t)d->max_hits_per_ray;
-        j.RayHitResults = f->ray_hit_points; j.RayHitResultCounts = f->ray_hit_counts;
+        j.RayHitResults = f->ray_hit_points; j.RayHitResultCounts = f->ray_hit_counts; j.RayHitIds = f->ray_hit_ids;
         j.EchoRayDistances = f->echo_ray_distances;
         j.MuffleRayHits = f->muffle_ray_hits; j.MuffleRayHitsLength = TC * T;
         j.MaxMuffleHitDistance = d->max_muffle_hit_distance;

@@ -55,6 +55,7 @@ def main():
         stale = {k: getattr(out, k).copy() for k in ("echo", "muffle", "perm", "settings")}
         if out.hit_points is not None:
             stale["hit_points"] = out.hit_points.copy(); stale["hit_counts"] = out.hit_counts.copy()
+            stale["hit_ids"] = out.hit_ids.copy()
         counts = oracle.run(scene, params, org, out, threads=8)[1]
         arrs = dict(dirs=scene.dirs, targets=scene.targets, spheres=scene.spheres, aabbs=scene.aabbs, obbs=scene.obbs,
                     origins=org, params=np.array(params_json(params)), counts=np.array(json.dumps(counts)),
@@ -65,6 +66,7 @@ def main():
             arrs["out_dsp"] = out.dsp
         if out.hit_points is not None:
             arrs["out_hit_points"] = out.hit_points; arrs["out_hit_counts"] = out.hit_counts
+            arrs["out_hit_ids"] = out.hit_ids
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
         print(name, {k: int(v) for k, v in counts.items() if v})
 

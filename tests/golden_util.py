@@ -23,11 +23,11 @@ def load(name):
     S = z["origins"].shape[0]
     hits = "out_hit_points" in z
     fresh = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, params.thread_count, hits=hits, dsp=dsp)
-    for k in ("echo", "muffle", "perm", "settings", "hit_points", "hit_counts"):
+    for k in ("echo", "muffle", "perm", "settings", "hit_points", "hit_counts", "hit_ids"):
         if "in_" + k in z:
             getattr(fresh, k)[...] = z["in_" + k]
     expected = fresh.copy()
-    for k in ("echo", "muffle", "perm", "settings", "dsp", "hit_points", "hit_counts"):
+    for k in ("echo", "muffle", "perm", "settings", "dsp", "hit_points", "hit_counts", "hit_ids"):
         if "out_" + k in z:
             getattr(expected, k)[...] = z["out_" + k]
     return scene, np.ascontiguousarray(z["origins"]), params, fresh, expected, json.loads(str(z["counts"]))

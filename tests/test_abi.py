@@ -50,11 +50,14 @@ def test_struct_sizes_match_csharp_layouts():
     assert abi.OBB.itemsize == 26       # ColliderOBBStruct.cs:10-24
     assert abi.SPHERE.itemsize == 16    # ColliderSphereStruct.cs:10-14
     assert abi.SETTINGS.itemsize == 24  # AudioTargetRTSettings.cs:11-16
-    assert C.sizeof(abi.art_fan) == 12 + 4 + 7 * 8  # origin float[3] + pad + 7 pointers
+    assert C.sizeof(abi.art_fan) == 12 + 4 + 8 * 8  # origin float[3] + pad + 8 pointers
+    offs = {n: getattr(abi.art_fan, n).offset for n, _ in abi.art_fan._fields_}
+    assert offs["ray_hit_counts"] == 64 and offs["ray_hit_ids"] == 72  # appended after the editor arrays
+    assert C.sizeof(abi.art_fan_layout) == 9 * 4
 
 
 def test_version():
-    assert art.load_library().art_version() >> 16 == 1
+    assert art.load_library().art_version() >> 16 == 2  # 2.0: art_fan.ray_hit_ids
 
 
 def test_no_gpu_fails_loudly():
@@ -84,7 +87,9 @@ def test_layout_and_validation_without_device():
     assert lay["stride"] % 16 == 0
     assert lay["echo_off"] >= lay["perm_off"] + 4 * 4
     lay_h = art.fan_layout(fr, abi.ART_OUT_HIT_RESULTS)
-    assert lay_h["stride"] >= lay["stride"] + 64 * 5 * 6 + 64
+    assert lay_h["stride"] >= lay["stride"] + 64 * 5 * 6 + 64 + 64 * 5 * 4
+    assert lay_h["hit_ids_off"] % 16 == 0 and lay_h["hit_ids_off"] >= lay_h["hit_counts_off"] + 64
+    assert lay_h["hit_ids_off"] + 64 * 5 * 4 <= lay_h["stride"]
     with pytest.raises(art.ArtError) as e:
         art.fan_layout(_frame(max_hits_per_ray=33))
     assert e.value.code == abi.ART_E_UNSUPPORTED
@@ -122,3 +127,13 @@ def test_batch_size_matches_reference_formula():
     p = art.FrameParams(thread_count=3)
     assert p.batch_size(314) == 105   # ceil(314 / 3) — AudioRayTracer.cs:161
     assert art.FrameParams(thread_count=1).batch_size(512) == 512
+
+
+def test_hit_id_encoding():
+    """ART_HIT_ID = ColliderType (Enums/ColliderType.cs: None, AABB, OBB, Sphere) << 30 | index."""
+    hdr = open(os.path.join(ROOT, "include", "art.h")).read()
+    for name, v in (("ART_COLLIDER_AABB", 1), ("ART_COLLIDER_OBB", 2), ("ART_COLLIDER_SPHERE", 3)):
+        assert re.search(rf"#define {name}\s+{v}u", hdr)
+        assert getattr(abi, name) == v
+    assert "#define ART_HIT_NONE 0xFFFFFFFFu" in hdr and abi.ART_HIT_NONE == 0xFFFFFFFF
+    assert abi.hit_id(abi.ART_COLLIDER_SPHERE, 5) == 0xC0000005

@@ -63,7 +63,7 @@ def fib_dirs(R):
 def run(ctx, scene, org, H=2, T_owned=False):
     params = art.FrameParams(max_hits_per_ray=H, max_ray_life=1e4, max_muffle_hit_distance=1e5,
                              stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
-    out, counts = gpu_vs_oracle(ctx, scene, params, org, counts=False)
+    out, counts = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
     return out
 
 
@@ -179,7 +179,7 @@ def test_razor_thin_segments_tiny_spheres(ctx):
     scene = art.Scene(dirs=dirs, targets=targets, spheres=sp, aabbs=wall)
     params = art.FrameParams(max_hits_per_ray=1, max_ray_life=1e4, max_muffle_hit_distance=1e5,
                              stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
-    out, _ = gpu_vs_oracle(ctx, scene, params, org, counts=False)
+    out, _ = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
     # the scene must contain both verdicts: some muffle rays blocked by a sphere, some clear
     assert (out.muffle != 0).any() and (out.muffle != R).any()
 
@@ -208,3 +208,8 @@ def test_bvh_exact_ties_across_leaves(ctx):
                              stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
     o_gpu, _ = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
     assert (o_gpu.hit_counts != 0).all()
+    # the first hit of axis ray k is the lowest-index copy of the sphere on that axis (hit ids)
+    s_pos = s_centers[ps]
+    for k in range(6):
+        first = int(np.flatnonzero((s_pos == axes[k] * 10.0).all(1)).min())
+        assert (o_gpu.hit_ids[:, k * 3] == abi.hit_id(abi.ART_COLLIDER_SPHERE, first)).all(), k

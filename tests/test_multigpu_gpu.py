@@ -31,7 +31,7 @@ def test_in_process_shards_on_one_device(ctx, shards, ci, S):
     cfg = art.CONFIGS[ci]
     scene, org, params = art.synth(cfg, S=S, R=128 if ci != 1 else 64, C_scale=0.1 if ci != 1 else None)
     dsp = params.dsp is not None
-    hits = ci in (1, 5)
+    hits = True
     one = art.FanOutputs(S, scene.R, params.max_hits_per_ray, scene.T, 1, hits=hits, dsp=dsp).fill_random(4)
     many, ref = one.copy(), one.copy()
     ctx.set_flags(0)

@@ -50,7 +50,8 @@ def test_k1_nan_and_roundtrip():
 
 
 def test_k1_host_helpers_agree_on_random_bits():
-    """Product host f32tof16 (unity_math.hpp) == oracle restatement on 2^18 random patterns."""
+    """Product host f32tof16 (unity_math.hpp) == oracle restatement on 2^12 random patterns (the
+    exhaustive 2^32 check is tests/test_half_exhaustive.py)."""
     from art.synth import f32tof16 as prod
     rng = np.random.default_rng(5)
     for b in rng.integers(0, 2 ** 32, 2 ** 12, dtype=np.uint64):
@@ -131,8 +132,10 @@ def test_quaternion_inverse_formula():
 
 @pytest.mark.parametrize("name", sorted(K.KATS))
 def test_frame_kats_on_oracle(name):
-    sc, p, org, expect = K.KATS[name]()
-    out = art.FanOutputs(1, sc.R, p.max_hits_per_ray, sc.T, 1, hits=True)
+    sc, p, org, expect, *prime = K.KATS[name]()
+    out = art.FanOutputs(1, sc.R, p.max_hits_per_ray, sc.T, p.thread_count, hits=True)
+    if prime:
+        prime[0](out)
     oracle.run(sc, p, org, out)
     expect(out)
 
@@ -143,3 +146,12 @@ def test_k9_reduce_on_oracle():
     prime(out)
     oracle.run(sc, p, org, out)
     expect(out)
+
+
+def test_unity32_f2h_matches_oracle():
+    """The KATs' numpy f32tof16 (tests/unity32.py) is the same function as the oracle's."""
+    import unity32 as U
+    rng = np.random.default_rng(6)
+    for b in rng.integers(0, 2 ** 32, 2 ** 12, dtype=np.uint64):
+        x = f32(int(b))
+        assert U.f2h(np.float32(x)) == oracle.f32tof16(x)

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 def _diff_report(a: art.FanOutputs, b: art.FanOutputs) -> str:
     lines = []
-    for name in ("echo", "muffle", "perm", "settings", "dsp", "hit_points", "hit_counts"):
+    for name in ("echo", "muffle", "perm", "settings", "dsp", "hit_points", "hit_counts", "hit_ids"):
         x, y = getattr(a, name), getattr(b, name)
         if x is None or y is None:
             continue
@@ -32,7 +32,7 @@ def _diff_report(a: art.FanOutputs, b: art.FanOutputs) -> str:
     return "\n".join(lines)
 
 
-def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True):
+def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True, prime=None):
     """Run the frame through both raytrace implementations — the throughput stage (BVH nearest
     hits, sorted-batch visibility; art_trace.hip) and the reference-order kernel (one ray per lane,
     every collider in reference order; its counting variant gives the metric's test counts) — and
@@ -43,6 +43,8 @@ def gpu_vs_oracle(ctx, scene, params, org, hits=False, stale=None, counts=True):
                            dsp=params.dsp is not None)
     if stale is not None:
         o_gpu.fill_random(stale)
+    if prime is not None:
+        prime(o_gpu)
     o_ref = o_gpu.copy()
     o_cnt = o_gpu.copy()
     o_ro = o_gpu.copy()
@@ -74,7 +76,7 @@ REDUCED = {1: (8, 64, None), 2: (16, 128, 0.25), 3: (8, 96, 0.125), 4: (8, 128, 
 def test_config_reduced(ctx, ci):
     S, R, cs = REDUCED[ci]
     scene, org, params = art.synth(art.CONFIGS[ci], S=S, R=R, C_scale=cs)
-    out, counts = gpu_vs_oracle(ctx, scene, params, org, hits=(ci in (1, 5)))
+    out, counts = gpu_vs_oracle(ctx, scene, params, org, hits=True)
     # the case must exercise the path: some echoes returned, some muffle rays clear
     assert (out.echo != 0).any() and (out.muffle != 0).any()
     assert counts["rt_sphere"] + counts["rt_aabb"] + counts["rt_obb"] > 0
@@ -154,13 +156,14 @@ def test_full_size_config2_sampled(ctx):
     rest through size-independent properties (determinism, fan-permutation invariance)."""
     cfg = art.CONFIGS[2]
     scene, org, params = art.synth(cfg)
-    out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1)
+    out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1, hits=True)
     ctx.run(art.Frame(scene, params, org, out))
     sub = np.arange(0, cfg.S, 8)
-    ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1)
+    ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1, hits=True)
     oracle.run(scene, params, org[sub], ref, threads=16)
-    for name in ("echo", "muffle", "perm", "settings"):
+    for name in ("echo", "muffle", "perm", "settings", "hit_points", "hit_counts", "hit_ids"):
         assert np.array_equal(getattr(out, name)[sub].view(np.uint8), getattr(ref, name).view(np.uint8)), name
+    assert (out.hit_ids != abi.ART_HIT_NONE).any()
     # determinism
     out2 = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1)
     ctx.run(art.Frame(scene, params, org, out2))
@@ -181,13 +184,13 @@ def test_full_size_sampled(ctx, ci, every):
     cfg = art.CONFIGS[ci]
     scene, org, params = art.synth(cfg)
     dsp = params.dsp is not None
-    out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1, dsp=dsp)
+    out = art.FanOutputs(cfg.S, cfg.R, cfg.H, cfg.T, 1, dsp=dsp, hits=True)
     ctx.set_flags(0)
     ctx.run(art.Frame(scene, params, org, out))
     sub = np.arange(0, cfg.S, every)
-    ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1, dsp=dsp)
+    ref = art.FanOutputs(len(sub), cfg.R, cfg.H, cfg.T, 1, dsp=dsp, hits=True)
     oracle.run(scene, params, np.ascontiguousarray(org[sub]), ref, threads=16)
-    for name in ("echo", "muffle", "perm", "settings") + (("dsp",) if dsp else ()):
+    for name in ("echo", "muffle", "perm", "settings", "hit_points", "hit_counts", "hit_ids") + (("dsp",) if dsp else ()):
         assert np.array_equal(getattr(out, name)[sub].view(np.uint8), getattr(ref, name).view(np.uint8)), name
 
 
@@ -247,8 +250,8 @@ import kat_scenes as K  # noqa: E402
 @pytest.mark.parametrize("name", sorted(K.KATS))
 def test_kats_on_gpu(ctx, name):
     """Hand-derived answers hold on the HIP path, through both kernels."""
-    sc, p, org, expect = K.KATS[name]()
-    out, _ = gpu_vs_oracle(ctx, sc, p, org, hits=True)
+    sc, p, org, expect, *prime = K.KATS[name]()
+    out, _ = gpu_vs_oracle(ctx, sc, p, org, hits=True, prime=prime[0] if prime else None)
     expect(out)
 
 
