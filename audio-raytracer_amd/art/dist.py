@@ -23,6 +23,8 @@ def all_gather_fan_blocks(local_block, S: int, stride: int, world: int, group=No
     n_local = local_block.numel() // stride
     if world == 1:
         return local_block
+    if local_block.is_cuda and dist.get_backend(group) == "gloo":  # gloo gathers host buffers
+        return all_gather_fan_blocks(local_block.cpu(), S, stride, world, group).to(local_block.device)
     if n_local == per and S == per * world:
         out = torch.empty(S * stride, dtype=torch.uint8, device=local_block.device)
         dist.all_gather_into_tensor(out, local_block, group=group)

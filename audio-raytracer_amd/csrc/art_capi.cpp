@@ -112,7 +112,8 @@ struct Device {
   hipEvent_t st_done = nullptr; // recorded after the last sync's upload + decode (dv.stream)
   bool st_pending = false;      // st_done recorded and the host staging may still be read
   hipEvent_t launch_done = nullptr;  // after the last art_launch_device frame (caller's stream)
-  bool launch_pending = false;       // a sync must wait for it before rewriting records / BVH
+  bool launch_pending = false;       // work on dv.stream waits for it before reusing the scene / buffers
+  hipStream_t launch_stream = nullptr;  // the caller's stream of that frame
   uint64_t exec_launches = 0;
   int fan_begin = 0, fan_count = 0;
   DevScene sc{};
@@ -396,9 +397,21 @@ void pack_inputs(const art_frame_desc* d, const Frame& f, uint8_t* h) {
   memcpy(h + f.off_order, f.ray_order.data(), (size_t)f.R * 4);
 }
 
+// An art_launch_device frame still running on the caller's stream reads the scene (records, sorted
+// copies, BVH) and uses the context's shared buffers (accumulators, pairs, side streams): work on
+// dv.stream that rewrites or reuses them waits for it first.
+int wait_launch(art_ctx* c, Device& dv) {
+  if (dv.launch_pending) {
+    HIP_TRY(c, hipStreamWaitEvent(dv.stream, dv.launch_done, 0));
+    dv.launch_pending = false;
+  }
+  return ART_OK;
+}
+
 // Upload the packed inputs to one device and build its SoA records (async on dv.stream).
 int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   HIP_TRY(c, hipSetDevice(dv.id));
+  if (int rc = wait_launch(c, dv)) return rc;
   if (!dv.raw.reserve(f.raw_bytes) || !dv.soa.reserve(f.soa_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   const int key[10] = {f.ns, f.na, f.no, f.T, f.R, f.TC, f.H, f.fp.vol_n, f.fp.muf_n, (int)f.raw_bytes};
   if (!f.resident && dv.raw_valid && dv.last_raw_p == dv.raw.p && dv.last_soa_p == dv.soa.p &&
@@ -557,17 +570,41 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   };
   auto tstop = [&](size_t i, hipStream_t on) { hipEvent_t e = pool_event(dv, i + 1); if (e) (void)hipEventRecord(e, on); };
 
+  // Everything the stages allocate or create comes first: once the permeation job is forked to the
+  // side stream, an early error return would leave it writing the caller's block unjoined.
+  const bool fast = (f.stages & ART_STAGE_RAYTRACE) && !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
+  const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.L.stride);
+  if (fast) {
+    if ((c->flags & ART_CTX_COUNT_EXECUTED) && !dv.exec.p) {
+      if (!dv.exec.reserve(64)) return fail(c, ART_E_NOMEM, "device allocation failed");
+      HIP_TRY(c, hipMemsetAsync(dv.exec.p, 0, 64, st));
+    }
+    if (!dv.echo.st) {
+      HIP_TRY(c, hipStreamCreateWithFlags(&dv.echo.st, hipStreamNonBlocking));
+      HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.fork, hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.join, hipEventDisableTiming));
+    }
+    FrameParams fps = fp;
+    fps.S = std::min(fan_count, chunk);
+    if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
+  }
   // The permeation job (read-only scene and origins, writes only the fans' permeation sections)
   // runs on the side stream concurrently with the raytrace stage, whose kernels leave CUs idle in
   // their tails; the reduce job waits for both. Counting frames stay serial.
   const bool both = (f.stages & ART_STAGE_RAYTRACE) && (f.stages & ART_STAGE_PERMEATE);
   const bool overlap = both && !count;
+  if (overlap && !dv.side) {
+    HIP_TRY(c, hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking));
+    HIP_TRY(c, hipEventCreateWithFlags(&dv.fork, hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreateWithFlags(&dv.join, hipEventDisableTiming));
+  }
+  // an error return after the fork drains the side stream first (the caller may free d_block)
+  struct SideDrain {
+    hipStream_t side = nullptr;
+    ~SideDrain() { if (side) (void)hipStreamSynchronize(side); }
+  } drain;
   if (overlap) {
-    if (!dv.side) {
-      HIP_TRY(c, hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking));
-      HIP_TRY(c, hipEventCreateWithFlags(&dv.fork, hipEventDisableTiming));
-      HIP_TRY(c, hipEventCreateWithFlags(&dv.join, hipEventDisableTiming));
-    }
+    drain.side = dv.side;
     HIP_TRY(c, hipEventRecord(dv.fork, st));
     HIP_TRY(c, hipStreamWaitEvent(dv.side, dv.fork, 0));
     size_t ti = timing ? tstart(1, dv.side) : 0;
@@ -582,32 +619,19 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     // The counting variant sweeps colliders in exact reference order per lane (its per-lane
     // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
     const int* order = reinterpret_cast<const int*>(raw + f.off_order);
-    if (count || (c->flags & ART_CTX_FORCE_REFERENCE_ORDER)) {
+    if (!fast) {
       HIP_TRY(c, hipMemsetAsync(acc, 0, acc_bytes, st));
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
     } else {
       FrameParams fpx = fp;
       fpx.exec = nullptr;
       if (c->flags & ART_CTX_COUNT_EXECUTED) {
-        if (!dv.exec.p) {
-          if (!dv.exec.reserve(64)) return fail(c, ART_E_NOMEM, "device allocation failed");
-          HIP_TRY(c, hipMemsetAsync(dv.exec.p, 0, 64, st));
-        }
         fpx.exec = static_cast<unsigned long long*>(dv.exec.p);
         dv.exec_launches++;
-      }
-      if (!dv.echo.st) {
-        HIP_TRY(c, hipStreamCreateWithFlags(&dv.echo.st, hipStreamNonBlocking));
-        HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.fork, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.join, hipEventDisableTiming));
       }
       // The pair arrays index pairs with 32-bit slots (sorted below 2^31) and the echo outputs with
       // 32-bit half offsets into the block: larger frames run as consecutive fan chunks on the
       // stream (the pair buffer and counter are reused, the muffle accumulators offset per chunk).
-      const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.L.stride);
-      FrameParams fps = fpx;
-      fps.S = std::min(fan_count, chunk);
-      if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
       for (int b0 = 0; b0 < fan_count; b0 += chunk) {
         FrameParams fpc = fpx;
         fpc.S = std::min(chunk, fan_count - b0);
@@ -618,7 +642,10 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
   }
-  if (overlap) HIP_TRY(c, hipStreamWaitEvent(st, dv.join, 0));
+  if (overlap) {
+    HIP_TRY(c, hipStreamWaitEvent(st, dv.join, 0));
+    drain.side = nullptr;  // joined: stream order covers it from here
+  }
   if ((f.stages & ART_STAGE_PERMEATE) && !overlap) {
     size_t ti = timing ? tstart(1, st) : 0;
     launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, st);
@@ -664,10 +691,14 @@ bool fan_wants_hits(const art_fan* fans, int n) {
 // One device's share of an art_schedule frame: scene upload, origins and in/out slot arrays H2D,
 // kernels, result blocks D2H, completion event (all async on dv.stream).
 int enqueue_device_frame(art_ctx* c, Device& dv, const Frame& f, const uint8_t* hin, const float* horg, uint8_t* hb,
-                         bool need_echo, bool count) {
+                         bool need_echo, bool count, bool inject_failure = false) {
   const FanLayout& L = f.L;
   int rc = upload_scene(c, dv, f, hin);
   if (rc) return rc;
+  if (inject_failure) {
+    dv.raw_valid = false;  // the scene upload may not have completed: never reuse it
+    return fail(c, ART_E_DEVICE, "injected enqueue failure on shard %d (ART_TEST_FAIL_SHARD)", dv.id);
+  }
   if (dv.fan_count == 0) { HIP_TRY(c, hipEventRecord(dv.done, dv.stream)); return ART_OK; }
   const size_t bbytes = (size_t)dv.fan_count * L.stride;
   if (!dv.origins.reserve((size_t)dv.fan_count * 12) || !dv.block.reserve(bbytes))
@@ -718,8 +749,7 @@ static int create_on(const int32_t* ids, int32_t count, art_ctx** out) {
     if (i < 0 || i >= n || hipSetDevice(i) != hipSuccess || hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&dv.done, hipEventDisableTiming) != hipSuccess) {
       if (dv.stream) (void)hipStreamDestroy(dv.stream);
-      c->devs.push_back(dv);
-      art_destroy(c);
+      art_destroy(c);  // the devices created so far; the failed entry holds nothing
       return ART_E_DEVICE;
     }
     c->devs.push_back(dv);
@@ -882,8 +912,12 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
   // Enqueue per device. An error on device k leaves devices [0, k) (and k itself, partly) with
   // async copies that still read or write the pinned staging: drain every stream before returning,
   // so the next art_schedule can repack h_in / h_block safely.
-  for (Device& dv : c->devs) {
-    rc = enqueue_device_frame(c, dv, f, hin, horg, hb, need_echo, count);
+  // test hook (tests/test_multigpu_gpu.py): shard k's enqueue fails after its scene upload
+  const char* fail_env = getenv("ART_TEST_FAIL_SHARD");
+  const int fail_shard = fail_env ? atoi(fail_env) : -1;
+  for (size_t k = 0; k < c->devs.size(); ++k) {
+    Device& dv = c->devs[k];
+    rc = enqueue_device_frame(c, dv, f, hin, horg, hb, need_echo, count, (int)k == fail_shard);
     if (rc) {
       for (Device& e : c->devs) {
         (void)hipSetDevice(e.id);
@@ -1011,13 +1045,17 @@ static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, 
   }
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL is the HIP default stream (torch's default)
   if (f.resident && dv.st_done) HIP_TRY(c, hipStreamWaitEvent(st, dv.st_done, 0));
+  // frames share the context's accumulators and pair buffers: a launch on another stream than the
+  // previous one waits for it (on the same stream, stream order already does)
+  if (dv.launch_pending && st != dv.launch_stream) HIP_TRY(c, hipStreamWaitEvent(st, dv.launch_done, 0));
   int rc = enqueue_kernels(c, dv, f, d_origins, fan_count, static_cast<uint8_t*>(d_block), st, count);
   if (rc) return rc;
-  if (f.resident) {  // the next art_colliders_sync rewrites the records and refits in place: after this frame
-    if (!dv.launch_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.launch_done, hipEventDisableTiming));
-    HIP_TRY(c, hipEventRecord(dv.launch_done, st));
-    dv.launch_pending = true;
-  }
+  // the next sync, bind or schedule rewrites the scene or reuses the shared buffers on dv.stream:
+  // after this frame (wait_launch)
+  if (!dv.launch_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.launch_done, hipEventDisableTiming));
+  HIP_TRY(c, hipEventRecord(dv.launch_done, st));
+  dv.launch_pending = true;
+  dv.launch_stream = st;
   if (count) return read_counts(c, dv, st, out, false);
   return ART_OK;
 }
@@ -1275,10 +1313,7 @@ ART_API int art_colliders_sync(art_ctx* c) {
     auto* oobbc = reinterpret_cast<ObbCold*>(soa + s_obbc);
     auto* cull = reinterpret_cast<CullRec*>(soa + s_cull);
     // device-path frames on other streams still read the records / BVH being rewritten: wait for them
-    if (dv.launch_pending) {
-      HIP_TRY(c, hipStreamWaitEvent(dv.stream, dv.launch_done, 0));
-      dv.launch_pending = false;
-    }
+    if (int rc = wait_launch(c, dv)) return rc;
     if (nd) {
       HIP_TRY(c, hipMemcpyAsync(up, h, bytes, hipMemcpyHostToDevice, dv.stream));
       launch_scatter_prep(reinterpret_cast<const int*>(up + off_idx[0]), reinterpret_cast<const art_sphere*>(up + off_rec[0]),

@@ -521,14 +521,15 @@ __global__ void fibonacci_kernel(int count, art_half3* __restrict__ out) {
 }
 
 __global__ void half_range_kernel(uint32_t first, uint32_t count, uint16_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  out[i] = f32tof16(asfloat(first + i));
+  out[i] = f32tof16(asfloat(first + (uint32_t)i));  // wraps past 0xFFFFFFFF
 }
 
 void launch_half_range(uint32_t first, uint32_t count, uint16_t* out, hipStream_t st) {
   if (count == 0) return;
-  hipLaunchKernelGGL(half_range_kernel, dim3((count + 255u) / 256u), dim3(256), 0, st, first, count, out);
+  const unsigned blocks = (unsigned)(((unsigned long long)count + 255ull) / 256ull);  // no 32-bit wrap near 2^32
+  hipLaunchKernelGGL(half_range_kernel, dim3(blocks), dim3(256), 0, st, first, count, out);
 }
 
 void launch_fibonacci(int count, art_half3* out, hipStream_t st) {

@@ -62,6 +62,9 @@ def parse():
                    help="N > 1: weak = cfg.S fans per rank; strong = cfg.S fans split over the ranks "
                         "(auto: strong for config 4, as BASELINE.json names it, weak otherwise)")
     p.add_argument("--no-dynamic", action="store_true", help="skip the dynamic-scene and rebuild measurements")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo: host-side all-gather, "
+                        "e.g. ranks sharing one GPU in tests)")
     p.add_argument("--targets", type=int, default=None,
                    help="audio targets T (experiments; BASELINE's configs use 4): the same scene generator with T targets")
     p.add_argument("--path", choices=("raytrace", "dsp", "dirs", "cpu"), default="raytrace",
@@ -133,7 +136,8 @@ def cpu_baseline(cfg, scene, params, org, min_seconds):
     return {"value": many["value"], "unit": "ray-collider tests/s", "cores": n, "kind": "port",
             "label": "reference algorithm (C restatement of the Burst jobs, oracle/art_oracle.c; Burst cannot run here)",
             "sample": f"{many['fans']} fans of config {cfg.index} ({many['tests']} reference tests, {many['seconds']:.1f} s) "
-                      f"on {n} threads, one fan per task; gcc -O3 -march=x86-64-v3 -ffp-contract=off",
+                      f"on {n} threads, one fan per task; gcc -O3 -march=x86-64-v3 -ffp-contract=off (x86-64-v3, "
+                      "not -march=native: the oracle library is built in the container and runs on the GPU box's host)",
             "one_thread": {"value": one["value"], "unit": "ray-collider tests/s",
                            "sample": f"{one['fans']} fans ({one['tests']} tests, {one['seconds']:.1f} s) on 1 thread"},
             "host": host}
@@ -518,12 +522,23 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        gpu = local % max(1, torch.cuda.device_count())  # ranks may share a GPU (gloo tests)
+        torch.cuda.set_device(gpu)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
     else:
         dist = None
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    # scalar reductions over ranks (timing, counts): device tensors over RCCL, host tensors over gloo
+    red_dev = dev if a.dist_backend == "nccl" else torch.device("cpu")
+
+    def allreduce(v, dtype, op=None):
+        t = torch.tensor([v], dtype=dtype, device=red_dev)
+        dist.all_reduce(t, op=op if op is not None else dist.ReduceOp.SUM)
+        return t.item()
 
     cfg = art.CONFIGS[a.config]
     if a.targets:
@@ -549,10 +564,20 @@ def main():
     tests_rank = sum(counts.values())
     bf_ops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
 
-    def step():
+    # the all-gather alone, timed with HIP events on the launch stream around the collective of
+    # every 8th timed step (BASELINE.md cfg 4: "all-gather time")
+    ag = {"ms": 0.0, "n": 0, "events": []}
+
+    def step(timed=False):
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
         if world > 1:
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
             art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
+            if timed:
+                e1.record(stream)
+                ag["events"].append((e0, e1))
 
     torch.cuda.synchronize()
     for _ in range(a.warmup):
@@ -567,9 +592,7 @@ def main():
         per = (time.perf_counter() - tp) / 10
         steps = int(min(5000, max(20, 1.5 / max(per, 1e-6))))
         if world > 1:
-            t = torch.tensor([steps], dtype=torch.int64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            steps = int(t.item())
+            steps = int(allreduce(steps, torch.int64, dist.ReduceOp.MAX))
     # Kernel durations come from HIP events on the launch stream around the stages of every 8th
     # timed step (event records between launches cost a few µs of GPU idle each; sampling keeps
     # that out of the other steps)
@@ -582,7 +605,7 @@ def main():
     for i in range(steps):
         if i % 8 == 0:
             ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
-        step()
+        step(timed=i % 8 == 0)
         if i % 8 == 0:
             ctx.set_flags(0)
     torch.cuda.synchronize()
@@ -590,6 +613,10 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     ktimes = ctx.kernel_timing()
+    allgather_ms = None
+    if ag["events"]:
+        allgather_ms = sum(e0.elapsed_time(e1) for e0, e1 in ag["events"]) / len(ag["events"])
+        allgather_ms = allreduce(allgather_ms, torch.float64, dist.ReduceOp.MAX)
     # work the kernels actually executed in one frame (broad phase: far fewer exact tests)
     ctx.set_flags(abi.ART_CTX_COUNT_EXECUTED)
     ctx.executed_counts()  # reset
@@ -598,12 +625,8 @@ def main():
     executed = ctx.executed_counts()
     ctx.set_flags(0)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        tt = torch.tensor([tests_rank], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt)
-        tests_all = float(tt.item())
+        dt = float(allreduce(dt, torch.float64, dist.ReduceOp.MAX))
+        tests_all = float(allreduce(tests_rank, torch.float64))
     else:
         tests_all = float(tests_rank)
 
@@ -668,10 +691,15 @@ def main():
         "config": {"workload": f"config{cfg.index}: {cfg.description}", "fans_total": S_total, "fans_rank0": S,
                    "rays": cfg.R, "colliders": cfg.C, "targets": cfg.T, "max_hits_per_ray": cfg.H,
                    "reference_tests_per_frame_rank0": tests_rank, "reference_tests_per_frame_all": tests_all,
-                   "parallelism": f"fan-sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+                   "parallelism": f"fan-sharded x{world}" + (f" + all-gather ({'RCCL' if a.dist_backend == 'nccl' else 'gloo'})"
+                                                              if world > 1 else "")},
+        "allgather_ms": allgather_ms,
+        "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
+        "allgather_note": "HIP events on the launch stream around the all-gather of every 8th timed step, max over "
+                          "ranks; the step time includes it" if world > 1 else None,
         "roofline": {"bound": "valu", "achieved": ex_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic, "traffic_note": traffic_note,
-                     "kernel": "raytrace stage: nearest_first_kernel + raytrace_fast_kernel + pair sort + vis_kernel + vis_finalize",
+                     "kernel": "raytrace stage: nearest_first_kernel + path_kernel + pair sort + vis_kernel + vis_finalize",
                      "kernel_ms": rt_ms,
                      "note": "FP32 VALU roof (no MFMA-shaped work). achieved = ops the kernels executed per launch (exact "
                              "tests x SURVEY.md 8(d) ops per test, lane-tests = wave-level tests x 64, plus broad-phase "

@@ -139,3 +139,56 @@ def test_world2_ranks_compute_shards_through_libart(ctx, ci, S, R, cs):
     oracle.run_frame(art.Frame(scene, params, org, o_ref), threads=16)
     assert all(out.equal(o_ref).values())
     assert ref.size == len(got)
+
+
+@pytest.mark.parametrize("fail_shard", [1, 2])
+def test_enqueue_failure_on_later_shard(ctx, monkeypatch, fail_shard):
+    """An error while enqueueing shard k > 0 of art_create_on([0]*3) (injected after shard k's scene
+    upload: shards < k already have copies and kernels in flight on their streams) returns the
+    error from art_schedule after draining every stream; nothing stays in flight, and the next
+    frame on the same context is complete and bit-exact."""
+    cfg = art.CONFIGS[5]
+    scene, org, params = art.synth(cfg, S=9, R=128, C_scale=0.1)
+    with art.Context(devices=[0, 0, 0]) as mctx:
+        bad = art.FanOutputs(9, 128, cfg.H, cfg.T, 1, hits=True, dsp=True)
+        monkeypatch.setenv("ART_TEST_FAIL_SHARD", str(fail_shard))
+        with pytest.raises(art.ArtError) as e:
+            mctx.schedule(art.Frame(scene, params, org, bad))
+        assert e.value.code == abi.ART_E_DEVICE and "injected" in str(e.value)
+        monkeypatch.delenv("ART_TEST_FAIL_SHARD")
+        good = art.FanOutputs(9, 128, cfg.H, cfg.T, 1, hits=True, dsp=True)
+        ref = good.copy()
+        mctx.run(art.Frame(scene, params, org, good))  # no frame in flight: schedule is accepted
+    oracle.run_frame(art.Frame(scene, params, org, ref), threads=16)
+    assert all(good.equal(ref).values()), good.equal(ref)
+
+
+def test_bench_two_ranks_gloo_strong_shards():
+    """bench.py's N > 1 path executes: config 4 (strong scaling, 1024 fans, reduced collider scale)
+    as two ranks sharing device 0 over gloo (torch.distributed.run). The strong-scaled shards'
+    reference test counts must add up to the single-rank count, and the line reports the
+    all-gather time. The RCCL branch is the same code with --dist-backend nccl."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--config", "4", "--collider-scale", "0.0625", "--steps", "3", "--warmup", "1", "--frames", "1",
+              "--no-cpu-baseline", "--no-dynamic"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+
+    def run(cmd):
+        p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-4000:]
+        return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+
+    one = run([sys.executable, "bench.py"] + common)
+    two = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+               "--dist-backend", "gloo"] + common)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["scaling"] == "strong"
+    assert two["config"]["fans_total"] == one["config"]["fans_total"] == 1024
+    assert two["config"]["fans_rank0"] == 512
+    assert two["config"]["reference_tests_per_frame_all"] == one["config"]["reference_tests_per_frame_rank0"]
+    assert two["config"]["reference_tests_per_frame_rank0"] < one["config"]["reference_tests_per_frame_rank0"]
+    assert two["allgather_ms"] is not None and two["allgather_ms"] > 0
+    assert two["allgather_bytes"] > 0 and one["allgather_ms"] is None

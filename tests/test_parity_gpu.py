@@ -357,3 +357,39 @@ def test_deep_bvh_large_scene(ctx):
     assert scene.C > 4 * 4 ** 7
     out, _ = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
     assert (out.echo != 0).any()
+
+
+def test_launch_device_then_schedule_and_bind_without_sync(ctx):
+    """art_launch_device returns without synchronizing; an art_schedule (or art_scene_bind) issued
+    right after rewrites the device scene and reuses the context's buffers on the context stream,
+    so it must wait for the launched frame. Scene A is bound and launched on torch's
+    stream; frame B (other colliders) is scheduled at once through the host API, then A is bound
+    again and launched, and scene C is bound with A's launch still queued: every result equals the
+    oracle."""
+    torch = pytest.importorskip("torch")
+    cfg = art.CONFIGS[5]
+    sa, org, params = art.synth(cfg, S=16, R=128, C_scale=0.25)
+    sb, _, _ = art.synth(art.CONFIGS[2], S=16, R=128, C_scale=0.25)
+    sb = art.Scene(dirs=sa.dirs, targets=sa.targets, spheres=sb.spheres, aabbs=sb.aabbs)
+    fa = art.Frame(sa, params, org, art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True))
+    lay = art.fan_layout(fa)
+    ref_a = art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True)
+    oracle.run_frame(art.Frame(sa, params, org, ref_a), threads=16)
+    ref_b = art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True)
+    oracle.run_frame(art.Frame(sb, params, org, ref_b), threads=16)
+    d_org = torch.from_numpy(org.copy()).cuda()
+    st = torch.cuda.current_stream()
+    for rnd in range(3):
+        ctx.set_flags(0)
+        ctx.bind(fa)
+        d_blk = torch.zeros(16 * lay["stride"], dtype=torch.uint8, device="cuda")
+        ctx.launch_device(d_org.data_ptr(), 16, d_blk.data_ptr(), 0, st.cuda_stream)
+        ob = art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True)
+        if rnd == 2:  # bind another scene instead of scheduling
+            ctx.bind(art.Frame(sb, params, org, ob))
+        else:
+            ctx.run(art.Frame(sb, params, org, ob))
+            assert all(ob.equal(ref_b).values()), ob.equal(ref_b)
+        st.synchronize()
+        got = art.unpack_block(d_blk.cpu().numpy(), lay, 16, 128, cfg.H, cfg.T, 1, dsp=True)
+        assert all(got.equal(ref_a).values()), (rnd, got.equal(ref_a))
