@@ -50,6 +50,7 @@ ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
+ART_CTX_NO_GRAPH = 0x100
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 # art_fan.ray_hit_ids: ColliderType (Enums/ColliderType.cs) << 30 | index in that type's array

@@ -96,8 +96,24 @@ struct Frame {
   size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
 };
 
+// Everything a captured frame graph bakes in: a replay is valid only for an identical key.
+struct GraphKey {
+  DevScene sc;
+  FrameParams fp;
+  FanLayout L;
+  const void *org, *blk, *acc, *pairs, *raw, *exec;
+  uint32_t flags;
+  int fans;
+  bool count;
+};
+
 struct Device {
   int id = 0;
+  // frame graph (enqueue_kernels): capture stream, instantiated graph and its key
+  hipStream_t cap = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  GraphKey gkey{};
+  uint64_t graph_captures = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
@@ -533,6 +549,14 @@ hipEvent_t pool_event(Device& dv, size_t i) {
   return dv.ev_pool[i];
 }
 
+bool graphs_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ART_GRAPH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Enqueue the kernels of one frame for fan_count fans on stream st.
 int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origins, int fan_count, uint8_t* d_block,
                     hipStream_t st, bool count) {
@@ -598,6 +622,15 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     HIP_TRY(c, hipEventCreateWithFlags(&dv.fork, hipEventDisableTiming));
     HIP_TRY(c, hipEventCreateWithFlags(&dv.join, hipEventDisableTiming));
   }
+  unsigned long long* exec_ctr = nullptr;
+  if (fast && (c->flags & ART_CTX_COUNT_EXECUTED)) {
+    exec_ctr = static_cast<unsigned long long*>(dv.exec.p);
+    dv.exec_launches++;
+  }
+
+  // The frame's launch sequence on stream st: stage kernels, side-stream forks and joins. It
+  // allocates nothing and reads no device state on the host, so it can be captured as a graph.
+  auto launch = [&](hipStream_t st) -> int {
   // an error return after the fork drains the side stream first (the caller may free d_block)
   struct SideDrain {
     hipStream_t side = nullptr;
@@ -624,11 +657,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       launch_raytrace(dv.sc, fp, f.L, d_origins, d_block, acc, counts, st);
     } else {
       FrameParams fpx = fp;
-      fpx.exec = nullptr;
-      if (c->flags & ART_CTX_COUNT_EXECUTED) {
-        fpx.exec = static_cast<unsigned long long*>(dv.exec.p);
-        dv.exec_launches++;
-      }
+      fpx.exec = exec_ctr;
       // The pair arrays index pairs with 32-bit slots (sorted below 2^31) and the echo outputs with
       // 32-bit half offsets into the block: larger frames run as consecutive fan chunks on the
       // stream (the pair buffer and counter are reused, the muffle accumulators offset per chunk).
@@ -662,6 +691,40 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
   }
+  return ART_OK;
+  };
+
+  // Graph replay: the launch sequence is captured once on a private stream, with the
+  // side streams' event edges as graph edges, and the instantiated graph is launched on the
+  // caller's stream for every later frame with the same launch key (scene, frame parameters,
+  // buffers, fan count, flags). One graph launch replaces ~10 launches and the host-side fork /
+  // join gaps. Counting and timed frames, and ART_CTX_NO_GRAPH / ART_GRAPH=0, launch directly.
+  if (count || timing || (c->flags & ART_CTX_NO_GRAPH) || !graphs_enabled()) return launch(st);
+  GraphKey key;
+  memset(&key, 0, sizeof key);
+  key.sc = dv.sc; key.fp = fp; key.L = f.L;
+  key.org = d_origins; key.blk = d_block; key.acc = dv.acc.p; key.pairs = dv.pairs.p; key.raw = dv.raw.p;
+  key.exec = exec_ctr; key.flags = c->flags; key.fans = fan_count; key.count = count;
+  if (dv.gexec && memcmp(&key, &dv.gkey, sizeof key) == 0) {
+    HIP_TRY(c, hipGraphLaunch(dv.gexec, st));
+    return ART_OK;
+  }
+  if (dv.gexec) { (void)hipGraphExecDestroy(dv.gexec); dv.gexec = nullptr; }
+  if (!dv.cap) HIP_TRY(c, hipStreamCreateWithFlags(&dv.cap, hipStreamNonBlocking));
+  HIP_TRY(c, hipStreamBeginCapture(dv.cap, hipStreamCaptureModeRelaxed));
+  const int rc = launch(dv.cap);
+  hipGraph_t g = nullptr;
+  const hipError_t ee = hipStreamEndCapture(dv.cap, &g);
+  if (rc || ee != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc ? rc : fail(c, ART_E_DEVICE, "hipStreamEndCapture failed: %s", hipGetErrorString(ee));
+  }
+  const hipError_t ei = hipGraphInstantiate(&dv.gexec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ei != hipSuccess) { dv.gexec = nullptr; return fail(c, ART_E_DEVICE, "hipGraphInstantiate failed: %s", hipGetErrorString(ei)); }
+  dv.gkey = key;
+  dv.graph_captures++;
+  HIP_TRY(c, hipGraphLaunch(dv.gexec, st));
   return ART_OK;
 }
 
@@ -789,6 +852,8 @@ ART_API void art_destroy(art_ctx* c) {
   for (Device& dv : c->devs) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
+    if (dv.gexec) (void)hipGraphExecDestroy(dv.gexec);
+    if (dv.cap) (void)hipStreamDestroy(dv.cap);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.exec.release(); dv.pairs.release(); dv.dsp.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();

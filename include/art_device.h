@@ -47,6 +47,11 @@ typedef struct {
 /* (0x8, 0x40 and 0x80 selected round-1 alternative raytrace implementations; they are gone and
  * the bits are reserved.) */
 
+/* Launch every frame's kernels directly instead of replaying the captured frame graph (a frame's
+ * launch sequence is captured as a hipGraph on first use and replayed while the scene, buffers,
+ * fan count and flags stay the same; ART_GRAPH=0 in the environment also disables it). */
+#define ART_CTX_NO_GRAPH 0x100u
+
 ART_API int art_fan_layout_get(const art_frame_desc* desc, uint32_t out_flags, art_fan_layout* out);
 
 /* Upload the scene (colliders, directions, targets, curves) to every device of the context and

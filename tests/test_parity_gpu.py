@@ -393,3 +393,31 @@ def test_launch_device_then_schedule_and_bind_without_sync(ctx):
         st.synchronize()
         got = art.unpack_block(d_blk.cpu().numpy(), lay, 16, 128, cfg.H, cfg.T, 1, dsp=True)
         assert all(got.equal(ref_a).values()), (rnd, got.equal(ref_a))
+
+
+def test_graph_replay_equals_direct_launches(ctx):
+    """Device frames replay a captured hipGraph of the frame's launch sequence while the launch key
+    (scene, parameters, buffers, fan count, flags) is unchanged. Replayed frames, re-captured frames
+    after a rebind with other parameters, and direct launches (ART_CTX_NO_GRAPH) must all equal the
+    oracle byte for byte; multi-bounce (per-bounce echo forks) and permeation (side stream) included."""
+    torch = pytest.importorskip("torch")
+    cfg = art.CONFIGS[5]
+    scene, org, params = art.synth(cfg, S=12, R=128, C_scale=0.2)
+    d_org = torch.from_numpy(org.copy()).cuda()
+    st = torch.cuda.current_stream()
+    for life in (125.0, 40.0):
+        params.max_ray_life = life
+        fr = art.Frame(scene, params, org, art.FanOutputs(12, 128, cfg.H, cfg.T, 1, dsp=True, hits=True))
+        ref = art.FanOutputs(12, 128, cfg.H, cfg.T, 1, dsp=True, hits=True)
+        oracle.run_frame(art.Frame(scene, params, org, ref), threads=16)
+        lay = art.fan_layout(fr, abi.ART_OUT_HIT_RESULTS)
+        ctx.bind(fr)
+        for flags in (0, 0, abi.ART_CTX_NO_GRAPH, 0):
+            ctx.set_flags(flags)
+            d_blk = torch.zeros(12 * lay["stride"], dtype=torch.uint8, device="cuda")
+            for _ in range(3):  # replays write the same block
+                ctx.launch_device(d_org.data_ptr(), 12, d_blk.data_ptr(), abi.ART_OUT_HIT_RESULTS, st.cuda_stream)
+            st.synchronize()
+            got = art.unpack_block(d_blk.cpu().numpy(), lay, 12, 128, cfg.H, cfg.T, 1, hits=True, dsp=True)
+            assert all(got.equal(ref).values()), (life, flags, got.equal(ref))
+    ctx.set_flags(0)
