@@ -109,11 +109,15 @@ struct GraphKey {
 
 struct Device {
   int id = 0;
-  // frame graph (enqueue_kernels): capture stream, instantiated graph and its key
+  // frame graphs (enqueue_kernels): capture stream and a small cache of instantiated graphs
+  struct Graph {
+    GraphKey key;
+    hipGraphExec_t exec = nullptr;
+    uint64_t used = 0;
+  };
   hipStream_t cap = nullptr;
-  hipGraphExec_t gexec = nullptr;
-  GraphKey gkey{};
-  uint64_t graph_captures = 0;
+  std::vector<Graph> graphs;
+  uint64_t graph_clock = 0, graph_captures = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
@@ -549,6 +553,8 @@ hipEvent_t pool_event(Device& dv, size_t i) {
   return dv.ev_pool[i];
 }
 
+constexpr size_t kGraphCache = 4;  // instantiated frame graphs kept per device
+
 bool graphs_enabled() {
   static const bool on = [] {
     const char* e = getenv("ART_GRAPH");
@@ -705,11 +711,23 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   key.sc = dv.sc; key.fp = fp; key.L = f.L;
   key.org = d_origins; key.blk = d_block; key.acc = dv.acc.p; key.pairs = dv.pairs.p; key.raw = dv.raw.p;
   key.exec = exec_ctr; key.flags = c->flags; key.fans = fan_count; key.count = count;
-  if (dv.gexec && memcmp(&key, &dv.gkey, sizeof key) == 0) {
-    HIP_TRY(c, hipGraphLaunch(dv.gexec, st));
-    return ART_OK;
+  for (Device::Graph& gr : dv.graphs)
+    if (memcmp(&key, &gr.key, sizeof key) == 0) {
+      gr.used = ++dv.graph_clock;
+      HIP_TRY(c, hipGraphLaunch(gr.exec, st));
+      return ART_OK;
+    }
+  if (dv.graphs.size() >= kGraphCache) {  // evict the least recently used graph
+    size_t v = 0;
+    for (size_t i = 1; i < dv.graphs.size(); ++i)
+      if (dv.graphs[i].used < dv.graphs[v].used) v = i;
+    // it may still run: frames form one dependency chain (launch_common / wait_launch), so the last
+    // frame's event and the context stream cover every earlier launch
+    if (dv.launch_done) HIP_TRY(c, hipEventSynchronize(dv.launch_done));
+    HIP_TRY(c, hipStreamSynchronize(dv.stream));
+    (void)hipGraphExecDestroy(dv.graphs[v].exec);
+    dv.graphs.erase(dv.graphs.begin() + (long)v);
   }
-  if (dv.gexec) { (void)hipGraphExecDestroy(dv.gexec); dv.gexec = nullptr; }
   if (!dv.cap) HIP_TRY(c, hipStreamCreateWithFlags(&dv.cap, hipStreamNonBlocking));
   HIP_TRY(c, hipStreamBeginCapture(dv.cap, hipStreamCaptureModeRelaxed));
   const int rc = launch(dv.cap);
@@ -719,12 +737,15 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     if (g) (void)hipGraphDestroy(g);
     return rc ? rc : fail(c, ART_E_DEVICE, "hipStreamEndCapture failed: %s", hipGetErrorString(ee));
   }
-  const hipError_t ei = hipGraphInstantiate(&dv.gexec, g, nullptr, nullptr, 0);
+  Device::Graph gr;
+  gr.key = key;
+  const hipError_t ei = hipGraphInstantiate(&gr.exec, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
-  if (ei != hipSuccess) { dv.gexec = nullptr; return fail(c, ART_E_DEVICE, "hipGraphInstantiate failed: %s", hipGetErrorString(ei)); }
-  dv.gkey = key;
+  if (ei != hipSuccess) return fail(c, ART_E_DEVICE, "hipGraphInstantiate failed: %s", hipGetErrorString(ei));
+  gr.used = ++dv.graph_clock;
+  dv.graphs.push_back(gr);
   dv.graph_captures++;
-  HIP_TRY(c, hipGraphLaunch(dv.gexec, st));
+  HIP_TRY(c, hipGraphLaunch(gr.exec, st));
   return ART_OK;
 }
 
@@ -852,7 +873,8 @@ ART_API void art_destroy(art_ctx* c) {
   for (Device& dv : c->devs) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    if (dv.gexec) (void)hipGraphExecDestroy(dv.gexec);
+    if (dv.launch_done) (void)hipEventSynchronize(dv.launch_done);  // a device frame on the caller's stream
+    for (Device::Graph& gr : dv.graphs) (void)hipGraphExecDestroy(gr.exec);
     if (dv.cap) (void)hipStreamDestroy(dv.cap);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.exec.release(); dv.pairs.release(); dv.dsp.release();
