@@ -94,6 +94,9 @@ struct Frame {
   size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_cull = 0, soa_bytes = 0;
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
   size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
+  // muffle candidate lists (art_cells.hip)
+  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_com = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, cells_temp = 0;
+  uint32_t cells_cap = 0;
 };
 
 // Everything a captured frame graph bakes in: a replay is valid only for an identical key.
@@ -122,6 +125,8 @@ struct Device {
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
   DevBuf exec;  // executed-work counters (ART_CTX_COUNT_EXECUTED)
+  DevBuf cones; // the cell cone table (art_cells.hip), uploaded once
+  CellBufs cb{};  // muffle candidate list buffers of the current scene (upload_scene)
   DevBuf pairs; // global visibility pairs of the split raytrace path
   DevBuf dsp;   // per-sample DSP batch (art_dsp_process): samples, offsets, frames, params, states
   // resident collider store (art_colliders.h): AoS lists, decoded records + bounds, sync upload
@@ -312,6 +317,50 @@ void coherent_order(const art_half3* dirs, int R, std::vector<int>& order) {
   for (int i = 0; i < R; ++i) order[(size_t)i] = keys[(size_t)i].second;
 }
 
+// Cube-map direction cells around a target (art_cells.hip): face f = 2 m + (negative), cell (i, j)
+// covers u = v[(m+1)%3] / |v[m]| in [-1 + 2i/G, -1 + 2(i+1)/G] and w = v[(m+2)%3] / |v[m]| likewise
+// (art_trace.hip cube_cell). Each cell's cone: the normalised sum of its corner directions and the
+// largest angle to a corner (the farthest point of a convex spherical quadrilateral from an inner
+// point), plus 1e-4 rad for the rounding of the cell lookup and of this float table.
+struct ConeTable {
+  CellCone cone[kCells];
+  float alpha_max = 0.0f;
+  ConeTable() {
+    for (int f = 0; f < 6; ++f) {
+      const int m = f >> 1;
+      const double sg = (f & 1) ? -1.0 : 1.0;
+      for (int j = 0; j < kCellG; ++j)
+        for (int i = 0; i < kCellG; ++i) {
+          double corner[4][3], sum[3] = {0, 0, 0};
+          for (int k = 0; k < 4; ++k) {
+            const double u = -1.0 + 2.0 * (i + (k & 1)) / kCellG, w = -1.0 + 2.0 * (j + (k >> 1)) / kCellG;
+            double d[3];
+            d[m] = sg; d[(m + 1) % 3] = u; d[(m + 2) % 3] = w;
+            const double nrm = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+            for (int a = 0; a < 3; ++a) { corner[k][a] = d[a] / nrm; sum[a] += corner[k][a]; }
+          }
+          const double sn = std::sqrt(sum[0] * sum[0] + sum[1] * sum[1] + sum[2] * sum[2]);
+          for (int a = 0; a < 3; ++a) sum[a] /= sn;
+          double alpha = 0.0;
+          for (int k = 0; k < 4; ++k) {
+            const double c = sum[0] * corner[k][0] + sum[1] * corner[k][1] + sum[2] * corner[k][2];
+            alpha = std::max(alpha, std::acos(std::min(1.0, c)));
+          }
+          alpha += 1e-4;
+          CellCone& cc = cone[(f * kCellG + j) * kCellG + i];
+          cc.ax = (float)sum[0]; cc.ay = (float)sum[1]; cc.az = (float)sum[2];
+          cc.cos_a = (float)std::cos(alpha); cc.sin_a = (float)std::sin(alpha);
+          cc.pad0 = cc.pad1 = cc.pad2 = 0.0f;
+          alpha_max = std::max(alpha_max, (float)alpha);
+        }
+    }
+  }
+};
+const ConeTable& cone_table() {
+  static const ConeTable t;
+  return t;
+}
+
 // Frame scalars + batch tables (Audio/AudioRayTracer.cs:161, Jobs/*:63-64, :36-37).
 void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int* resident_counts = nullptr) {
   f = Frame();
@@ -398,6 +447,18 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_bvh = s; s = align_up(s + bvh_node_count((int)n) * sizeof(CullRec), 256);
     f.soa_bvh_ref = s; s = align_up(s + n * 4, 256);
     f.soa_bvh_leaf = s; s = align_up(s + bvh_slot_count((int)n) * 64, 256);
+  }
+  {  // muffle candidate lists
+    const size_t cells = (size_t)f.T * kCells;
+    f.cells_temp = cells_scan_temp_bytes(f.T);
+    f.cells_cap = (uint32_t)cells_entry_cap(f.T, f.ns + f.na + f.no);
+    f.soa_ccount = s; s = align_up(s + (cells + 1) * 4, 256);
+    f.soa_cstart = s; s = align_up(s + (cells + 1) * 4, 256);
+    f.soa_ccur = s; s = align_up(s + cells * 4, 256);
+    f.soa_com = s; s = align_up(s + (size_t)f.T * 4, 256);
+    f.soa_cok = s; s = align_up(s + (size_t)f.T * 4, 256);
+    f.soa_ctemp = s; s = align_up(s + f.cells_temp, 256);
+    f.soa_cent = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
   }
   f.soa_bytes = s;
 }
@@ -497,6 +558,24 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     dv.sorted_gen = f.resident ? c->sync_gen : ~0ull;
     dv.sorted_soa = dv.soa.p;
     dv.sorted_n[0] = f.ns; dv.sorted_n[1] = f.na; dv.sorted_n[2] = f.no;
+  }
+  {  // muffle candidate lists for these colliders and targets
+    if (!dv.cones.p) {
+      if (!dv.cones.reserve(sizeof(CellCone) * kCells)) return fail(c, ART_E_NOMEM, "device allocation failed");
+      HIP_TRY(c, hipMemcpyAsync(dv.cones.p, cone_table().cone, sizeof(CellCone) * kCells, hipMemcpyHostToDevice, dv.stream));
+    }
+    CellBufs& cb = dv.cb;
+    cb.cones = static_cast<const CellCone*>(dv.cones.p);
+    cb.alpha_max = cone_table().alpha_max;
+    cb.count = reinterpret_cast<uint32_t*>(soa + f.soa_ccount);
+    cb.start = reinterpret_cast<uint32_t*>(soa + f.soa_cstart);
+    cb.cursor = reinterpret_cast<uint32_t*>(soa + f.soa_ccur);
+    cb.om = reinterpret_cast<float*>(soa + f.soa_com);
+    cb.ok = reinterpret_cast<uint32_t*>(soa + f.soa_cok);
+    cb.temp = soa + f.soa_ctemp; cb.temp_bytes = f.cells_temp;
+    cb.ent = reinterpret_cast<uint2*>(soa + f.soa_cent);
+    cb.cap = f.cells_cap;
+    if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
     dv.sorted_sc = sc;
   }
   HIP_TRY(c, hipGetLastError());
@@ -603,7 +682,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // Everything the stages allocate or create comes first: once the permeation job is forked to the
   // side stream, an early error return would leave it writing the caller's block unjoined.
   const bool fast = (f.stages & ART_STAGE_RAYTRACE) && !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
-  const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.L.stride);
+  const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.TC, f.L.stride);
   if (fast) {
     if ((c->flags & ART_CTX_COUNT_EXECUTED) && !dv.exec.p) {
       if (!dv.exec.reserve(64)) return fail(c, ART_E_NOMEM, "device allocation failed");
@@ -877,7 +956,7 @@ ART_API void art_destroy(art_ctx* c) {
     for (Device::Graph& gr : dv.graphs) (void)hipGraphExecDestroy(gr.exec);
     if (dv.cap) (void)hipStreamDestroy(dv.cap);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
-    dv.exec.release(); dv.pairs.release(); dv.dsp.release();
+    dv.exec.release(); dv.pairs.release(); dv.dsp.release(); dv.cones.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
     if (dv.st_done) (void)hipEventDestroy(dv.st_done);
     if (dv.launch_done) (void)hipEventDestroy(dv.launch_done);
@@ -1437,6 +1516,7 @@ ART_API int art_colliders_sync(art_ctx* c) {
         // moved colliders: refit the sorted copies and the BVH in place (device only, no H2D)
         if (nd) {
           if (launch_refit_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider refit failed");
+          if (launch_build_cells(dv.sc, dv.cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
           if (dv.sorted_gen != ~0ull) dv.sorted_gen = c->sync_gen;
           HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));  // device-path launches wait for the sort too
         }

@@ -1,0 +1,175 @@
+// art_cells.hip — muffle candidate lists: per audio target, a cube map of direction cells around
+// the target, each listing the colliders that can block a muffle ray arriving through it.
+//
+// A muffle ray (CanRaySeeAudioTarget, Jobs/AudioRaytracerJobBatched.cs:405-449, cast at :150-173)
+// runs from an offset hit point `off` to target t and is blocked by a collider not owned by t
+// (:413, :426, :439) whose test reports a hit closer than distance(off, target) (:165). Every such
+// segment ends at the target, so the colliders that can block it are exactly those met by the
+// target's ray through `off`. Cell lists make that a lookup: muffle_kernel (art_trace.hip) tests
+// only the entries of the segment's cell, instead of sorting per-(hit, target) pair records and
+// sweeping collider chunks.
+//
+// Exactness. A collider whose float test blocks the segment contains, in its
+// widened box (margin factor * (scale + om), the broad-phase margins of §5 item 8, with om >= |off|_1
+// + maxd), the exact point at the reported parameter of the float ray (off, normalize(t - off)).
+// That ray deviates from the exact segment [off, target] by at most eta = 2e-6 om, so the
+// collider's widened bounding sphere (+ 2 eta) meets the exact ray from the target towards `off`:
+// either it contains the target (entered in every cell) or the direction from the target to
+// `off` lies within the angular radius asin(rho / D) of the sphere, and that direction lies in
+// the segment's cell (up to the rounding of the cell lookup, covered by the cones' 1e-4 rad
+// slack). Entries also carry D - rho, a lower bound of the target distance of any blocking point;
+// muffle_kernel skips entries beyond maxd. A segment whose om exceeds the bound the lists were
+// built for, a degenerate segment, or a target whose lists overflowed tests every collider.
+#include <algorithm>
+
+#include <hipcub/hipcub.hpp>
+
+#include "art_device_fns.hpp"
+
+namespace art {
+
+constexpr float kCellEta = 2e-6f;  // relative deviation of a float muffle ray from its exact segment
+
+// |x|_1 bound of the scene and the largest target distance: the margin term om of target t.
+__device__ __forceinline__ float cells_om_of(const CullRec& root, vec3 tg) {
+  const float b1 = fmaxf(fabsf(root.lox), fabsf(root.hix)) + fmaxf(fabsf(root.loy), fabsf(root.hiy)) +
+                   fmaxf(fabsf(root.loz), fabsf(root.hiz));
+  const float dx = fmaxf(fabsf(root.lox - tg.x), fabsf(root.hix - tg.x));
+  const float dy = fmaxf(fabsf(root.loy - tg.y), fabsf(root.hiy - tg.y));
+  const float dz = fmaxf(fabsf(root.loz - tg.z), fabsf(root.hiz - tg.z));
+  const float far = sqrtf(dx * dx + dy * dy + dz * dz);
+  return (b1 + far) * 1.01f + 1.0f;
+}
+
+__global__ void cells_prep_kernel(DevScene sc, int T, float* __restrict__ om, uint32_t* __restrict__ ok) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  float v = INFINITY;
+  if (sc.bvh_levels > 0) v = cells_om_of(sc.bvh[0], load3(sc.targets, t));
+  om[t] = v;
+  ok[t] = isfinite(v) ? 1u : 0u;  // non-finite colliders: every muffle ray tests every collider
+}
+
+// Global collider g (spheres, AABBs, OBBs): its order code and AudioTargetId.
+__device__ __forceinline__ void collider_code(const DevScene& sc, int g, uint32_t& code, int& tid) {
+  if (g < sc.ns) { code = (uint32_t)g; tid = sc.sph[g].tid; return; }
+  g -= sc.ns;
+  if (g < sc.na) { code = (1u << 28) | (uint32_t)g; tid = sc.aabb[g].tid; return; }
+  g -= sc.na;
+  code = (2u << 28) | (uint32_t)g;
+  tid = sc.obb[g].tid;
+}
+
+// Cell range [i0, i1] of one face axis: the gnomonic coordinate u = (p . e_u) / (p . n) over the
+// cone of half-angle gamma around a (components a_u, a_n; s = sin^2 gamma) is bounded by the roots
+// of (a_n^2 - s) u^2 - 2 a_u a_n u + (a_u^2 - s) = 0 (the tangents of the cone's conic section).
+__device__ __forceinline__ void face_range(float a_u, float a_n, float s, int& i0, int& i1) {
+  const float den = a_n * a_n - s;
+  const float disc = s * (a_u * a_u + a_n * a_n - s);
+  if (!(den > 1e-3f) || !(disc >= 0.0f)) { i0 = 0; i1 = kCellG - 1; return; }
+  const float sq = sqrtf(disc);
+  const float r0 = (a_u * a_n - sq) / den, r1 = (a_u * a_n + sq) / den;
+  const float lo = fminf(r0, r1), hi = fmaxf(r0, r1);
+  i0 = (int)floorf((fmaxf(lo, -1.0f) + 1.0f) * (0.5f * kCellG)) - 1;
+  i1 = (int)floorf((fminf(hi, 1.0f) + 1.0f) * (0.5f * kCellG)) + 1;
+  i0 = max(i0, 0);
+  i1 = min(i1, kCellG - 1);
+  if (!(lo <= 1.0f && hi >= -1.0f)) { i0 = 1; i1 = 0; }  // outside the face
+}
+
+// One thread per (target, collider): enumerate the cells whose cone meets the collider's widened
+// bounding sphere. FILL = false counts per cell; FILL = true writes the entries.
+template <bool FILL>
+__global__ __launch_bounds__(256) void cells_collider_kernel(DevScene sc, CellBufs cb, int T) {
+  const int n = sc.ns + sc.na + sc.no;
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (long long)n * T) return;
+  const int t = (int)(k / n), g = (int)(k - (long long)t * n);
+  if (!cb.ok[t]) return;
+  uint32_t code;
+  int tid;
+  collider_code(sc, g, code, tid);
+  if (tid == t) return;  // owned by the target: its muffle rays skip it (:413, :426, :439)
+  const float om = cb.om[t];
+  const vec3 tg = load3(sc.targets, t);
+  const CullRec cr = sc.cull[g];
+  const float m = cr.factor * (cr.scale + om);
+  const float rho = 0.5f * ((cr.hix - cr.lox) + (cr.hiy - cr.loy) + (cr.hiz - cr.loz)) * 1.001f + 1.75f * m +
+                    2.0f * (kCellEta * om + 1e-6f);
+  const vec3 w = mk3(0.5f * (cr.lox + cr.hix) - tg.x, 0.5f * (cr.loy + cr.hiy) - tg.y, 0.5f * (cr.loz + cr.hiz) - tg.z);
+  const float D = sqrtf(w.x * w.x + w.y * w.y + w.z * w.z);
+  const bool all = !(D > rho * 1.0001f) || !isfinite(D) || !isfinite(rho);  // the sphere holds the target
+  const float sb = all ? 1.0f : rho / D;
+  const float cb_ = sqrtf(fmaxf(0.0f, 1.0f - sb * sb));
+  const float near = all ? 0.0f : fmaxf(0.0f, (D - rho) * 0.99999f - 1e-5f);
+  const vec3 u = all ? mk3(1.0f, 0.0f, 0.0f) : mk3(w.x / D, w.y / D, w.z / D);
+  const float gamma = cb.alpha_max + asinf(fminf(sb, 1.0f)) + 1e-3f;
+  const bool wide = all || gamma >= 1.5f;
+  const float sg = sinf(fminf(gamma, 1.5707963f)), s2 = sg * sg;
+  uint32_t* cnt = cb.count + (size_t)t * kCells;
+  uint32_t* cur = cb.cursor + (size_t)t * kCells;
+  const float uc[3] = {u.x, u.y, u.z};
+  for (int f = 0; f < 6; ++f) {
+    const int ax = f >> 1;
+    const float sgn = (f & 1) ? -1.0f : 1.0f;
+    const float a_n = sgn * uc[ax], a_u = uc[(ax + 1) % 3], a_v = uc[(ax + 2) % 3];
+    int i0 = 0, i1 = kCellG - 1, j0 = 0, j1 = kCellG - 1;
+    if (!wide) {
+      if (a_n <= -sg) continue;  // the cone stays in the opposite half-space
+      face_range(a_u, a_n, s2, i0, i1);
+      face_range(a_v, a_n, s2, j0, j1);
+    }
+    for (int j = j0; j <= j1; ++j)
+      for (int i = i0; i <= i1; ++i) {
+        const int c = (f * kCellG + j) * kCellG + i;
+        const CellCone cc = cb.cones[c];
+        // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
+        const bool hit = all || (u.x * cc.ax + u.y * cc.ay + u.z * cc.az >= (cc.cos_a * cb_ - cc.sin_a * sb) - 1e-5f);
+        if (!hit) continue;
+        if (!FILL) {
+          atomicAdd(cnt + c, 1u);
+        } else {
+          const uint32_t pos = atomicAdd(cur + c, 1u);
+          if (pos < cb.cap) cb.ent[pos] = make_uint2(code, __float_as_uint(near));
+          else cb.ok[t] = 0u;  // overflow: this target's muffle rays test every collider
+        }
+      }
+  }
+}
+
+size_t cells_scan_temp_bytes(int T) {
+  size_t bytes = 0;
+  const int n = T * kCells + 1;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, n);
+  return bytes;
+}
+
+// Entry capacity: 64 cells per (target, collider) on average (a collider near its target spans
+// hundreds, a far one a few); a target whose lists do not fit falls back to testing every collider.
+size_t cells_entry_cap(int T, int C) {
+  const size_t want = (size_t)64 * (size_t)T * (size_t)(C > 0 ? C : 1);
+  return std::min<size_t>(std::max<size_t>(want, (size_t)1 << 16), (size_t)1 << 26);
+}
+
+int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
+  const int T = sc.T, n = sc.ns + sc.na + sc.no;
+  const int cells = T * kCells;
+  hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.om, cb.ok);
+  if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
+  const long long work = (long long)n * T;
+  const unsigned blocks = (unsigned)((work + 255) / 256);
+  if (work > 0) hipLaunchKernelGGL(cells_collider_kernel<false>, dim3(blocks), dim3(256), 0, st, sc, cb, T);
+  size_t bytes = cb.temp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(cb.temp, bytes, cb.count, cb.start, cells + 1, st) != hipSuccess) return -1;
+  if (hipMemcpyAsync(cb.cursor, cb.start, (size_t)cells * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return -1;
+  if (work > 0) hipLaunchKernelGGL(cells_collider_kernel<true>, dim3(blocks), dim3(256), 0, st, sc, cb, T);
+  sc.cell_start = cb.start;
+  sc.cell_ent = cb.ent;
+  sc.cell_om = cb.om;
+  sc.cell_ok = cb.ok;
+  sc.cell_cap = cb.cap;
+  return 0;
+}
+
+}  // namespace art

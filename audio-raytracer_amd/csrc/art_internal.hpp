@@ -88,6 +88,23 @@ struct DevScene {
                                   // index; -1: empty slot) in the first 32 B (bvh_leaf_kernel)
   int bvh_levels;                 // 0: no BVH
   int bvh_leaf0;
+  // Muffle candidate lists (art_cells.hip): for target t and direction cell c (a
+  // cube map of kCellG x kCellG cells per face around the target), the colliders not owned by t
+  // whose widened bounding sphere meets cell c's cone; entries (order code, distance from the
+  // target to the sphere) at cell_ent[cell_start[t * kCells + c] ..). A target whose bound or list
+  // overflowed (cell_ok[t] == 0) is tested against every collider instead.
+  const uint32_t* cell_start;     // [T * kCells + 1]
+  const uint2* cell_ent;          // [cell_cap]: (code, near bits)
+  const float* cell_om;           // [T]: the margin term the lists were built for
+  const uint32_t* cell_ok;        // [T]
+  uint32_t cell_cap;
+};
+constexpr int kCellG = 32;                   // cells per cube-face axis
+constexpr int kCells = 6 * kCellG * kCellG;  // cells per target
+// Cell cone (host table, art_capi.cpp): unit axis and cos / sin of the half-angle plus slack.
+struct alignas(16) CellCone {
+  float ax, ay, az, cos_a;
+  float sin_a, pad0, pad1, pad2;
 };
 constexpr int kBvhLeaf = 4;        // colliders per leaf
 constexpr int kBvhMaxLevels = 12;  // up to kBvhLeaf * 4^11 = 2^24 colliders per scene
@@ -119,6 +136,23 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
 // Colliders moved, counts unchanged: recompute the sorted copies' records, chunk bounds and the
 // BVH's bounds and leaf slots in place, keeping every order.
 int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
+
+// Muffle candidate lists (art_cells.hip): built after every scene upload / refit on stream st.
+struct CellBufs {
+  const CellCone* cones;          // [kCells]
+  float alpha_max;                // largest cone half-angle (with slack)
+  uint32_t* count;                // [T * kCells + 1] entries per cell
+  uint32_t* start;                // [T * kCells + 1] exclusive scan of count (DevScene::cell_start)
+  uint32_t* cursor;               // [T * kCells] fill positions
+  uint2* ent;                     // [cap]
+  float* om;                      // [T]
+  uint32_t* ok;                   // [T]
+  uint32_t cap;
+  void* temp; size_t temp_bytes;  // hipcub scan storage
+};
+size_t cells_scan_temp_bytes(int T);
+size_t cells_entry_cap(int T, int C);
+int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st);
 
 // Per-fan output block (byte offsets inside one fan's record; fan f starts at f * stride).
 struct FanLayout {
@@ -161,12 +195,12 @@ void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout&
                      uint8_t* block, uint32_t* muffle_acc, DevCounts* counts, hipStream_t st);
 // Bytes of the visibility pair buffer of launch_raytrace_fast for this frame (fp.S fans).
 size_t fast_pair_bytes(const FrameParams& fp);
-// Fans per launch_raytrace_fast call (32-bit pair slots and block offsets).
-int fast_fans_per_launch(int R, int H, int T, uint32_t stride);
-// The throughput raytrace stage (art_trace.hip): per bounce nearest_first_kernel + path_kernel,
-// then the pair sort, vis_kernel and vis_finalize. Any target count, every DevScene with a BVH.
-// echo_st (optional, with two events): the echo visibility runs there, beside the pair sort and the
-// muffle sweep on st, joined before vis_finalize.
+// Fans per launch_raytrace_fast call (32-bit pair slots, accumulator indices and block offsets).
+int fast_fans_per_launch(int R, int H, int T, int TC, uint32_t stride);
+// The throughput raytrace stage (art_trace.hip): per bounce nearest_first_kernel + path_kernel
+// (+ the bounce's echo vis_kernel), then muffle_kernel. Any target count, every DevScene with a BVH
+// and cell lists. echo_st (optional, with two events): the echo traversals run there, beside the
+// next bounces and the muffle kernel on st, joined at the end.
 struct SideStream {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;

@@ -4,16 +4,16 @@
 // One frame of S fans x R rays is, per bounce k = 0 .. H-1:
 //   nearest_first_kernel  nearest hit of every live ray segment (ShootRayCast :225-280) by a
 //                         quad-per-ray traversal of the collider BVH (art_bvh.hip);
-//   path_kernel           the exact re-evaluation of the winner, the hit point, the echo and
-//                         muffle visibility pairs (:121-173) and, for multi-hit frames, the
-//                         reflection / termination (:179-193, ReflectRay :456-532) and the ray
-//                         state of the next bounce;
+//   path_kernel           the exact re-evaluation of the winner, the hit point, the echo pair
+//                         (:121-145) and the hit record of the muffle rays (:150-173) and, for
+//                         multi-hit frames, the reflection / termination (:179-193, ReflectRay
+//                         :456-532) and the ray state of the next bounce;
+//   vis_kernel            (side stream) the bounce's echo rays (CanRaySeePoint :365-397) by quad
+//                         BVH any-hit traversal; a visible echo is stored at once;
 // then, once for the frame:
-//   pair sort (3 kernels) muffle pairs counting-sorted by (target, direction seen from it);
-//   vis_kernel            every pair's any-hit verdict (CanRaySeePoint :365-397,
-//                         CanRaySeeAudioTarget :405-449): echo batches by quad BVH traversal,
-//                         muffle batches by a box + apex-cone sweep over sorted collider chunks;
-//   vis_finalize          visible echoes stored, visible muffle rays counted.
+//   muffle_kernel         every hit's muffle rays (CanRaySeeAudioTarget :405-449) against the
+//                         target's direction-cell candidate lists (art_cells.hip), visible rays
+//                         counted into the muffle accumulators.
 // Every output equals the reference's bit for bit: the broad phases are exact, the
 // nearest hit is the (distance, reference order) minimum, any-hit verdicts are ORs.
 #include <algorithm>
@@ -25,8 +25,6 @@ namespace art {
 
 constexpr int kNoHit = 0x7fffffff;
 constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
-constexpr int kMaxQueries = 8;        // pair-emission round: echo + 7 targets, then 8 targets per round
-constexpr int kChunk = 64;            // colliders per sorted chunk (art_bvh.hip chunk_bounds_kernel)
 
 // Sphere test split so the common miss costs no branch: the square root and the two IEEE
 // divisions run only for lanes whose discriminant is non-negative (RayIntersectsSphere :323-355).
@@ -47,54 +45,11 @@ __device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c
   return hit;
 }
 
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ float dpp_mov(float v, float ident) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
-}
-
-// Wave-wide IEEE min / max (NaN lanes ignored), result wave-uniform. row_shr 1,2,4,8 within each
-// row of 16, then row_bcast 15 / 31 fold the rows into lane 63.
-__device__ __forceinline__ float wave_min(float v) {
-  v = fminf(v, dpp_mov<0x111, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x112, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x114, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x118, 0xf>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x142, 0xa>(v, INFINITY));
-  v = fminf(v, dpp_mov<0x143, 0xc>(v, INFINITY));
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ float wave_max(float v) {
-  v = fmaxf(v, dpp_mov<0x111, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x112, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x114, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x118, 0xf>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x142, 0xa>(v, -INFINITY));
-  v = fmaxf(v, dpp_mov<0x143, 0xc>(v, -INFINITY));
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-
 // Executed-work accounting (ART_CTX_COUNT_EXECUTED): one atomic per call from lane 0, off when
 // `ex` is null (a uniform branch).
 __device__ __forceinline__ void exec_add(unsigned long long* ex, int slot, unsigned long long v) {
   if (ex && v && (threadIdx.x & 63) == 0) atomicAdd(ex + slot, v);
 }
-
-// Candidate colliders of one 64-collider chunk: bit i = member i (wave-uniform mask).
-struct CandSet {
-  unsigned long long m;
-  int left;
-  __device__ __forceinline__ int pop() {  // next candidate offset (wave-uniform)
-    const int k = (int)__builtin_ctzll(m);
-    m &= m - 1;
-    --left;
-    return k;
-  }
-};
 
 // A ray whose direction or origin is non-finite, or whose direction is zero, makes every box test
 // inconclusive: its traversals visit every node (the exact tests alone decide).
@@ -385,77 +340,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
 }
 
 // ------------------------------------------------------------------------------------------
-// Visibility pairs. The path kernel emits every (hit, query) pair with its output destination;
-// visibility never feeds back into ray paths (echo :124-145 and muffle :150-173 only write
-// outputs), so the verdicts can be computed after all bounces.
-// Pair arrays (struct of arrays). Echo pairs i in [0, echo_cap), emission order (the 64 rays of a
-// wave share the fan origin, one batch each):
-//   seg[2 i], seg[2 i + 1]  (o.xyz, maxd), (d.xyz, kNoOwner)  32 B, read by the echo traversal;
-//                           1/d and dot(d, d) are recomputed there by make_seg (same operations)
-//   out[i]                  (u16 index of the echo in the fan blocks, echo half)  8 B, vis_finalize
-// Muffle pairs e in [0, S R H T), emission order:
-//   mrec[e]                 (off.xyz, e << tbits | t)  16 B: the segment's start and its target
-//                           (bit 31 of w: blocked, set in the sorted copy by the sweep);
-//                           maxd and the direction to the target are recomputed by the sweep with
-//                           the path kernel's operations
-//   mdest[e]                muffle_acc index  4 B, read by vis_finalize
-//   msorted[]               mrec counting-sorted by key (pair_scatter_kernel): the sweep reads its
-//                           batches of 64 coalesced, 16 B per pair
-// flag[i] / flag[echo_cap + e]: 0 = no blocker found yet, 1 = blocked. counts[0] / counts[1] = echo /
-// muffle pairs emitted.
+// Visibility work. The path kernel emits every echo ray and one hit record per hit; visibility
+// never feeds back into ray paths (echo :124-145 and muffle :150-173 only write outputs), so the
+// verdicts can be computed beside the next bounces. Struct of arrays:
+//   seg[2 i], seg[2 i + 1]  echo pair i, emission order: (o.xyz, maxd), (d.xyz, kNoOwner) 32 B, read by
+//                           the echo traversal (1/d and dot(d, d) recomputed by make_seg)
+//   out[i]                  (u16 index of the echo in the fan blocks, echo half) 8 B: the traversal
+//                           stores the half when no collider blocks the ray
+//   hrec[j]                 hit record j: (off.xyz, dest) 16 B — the muffle rays' common start
+//                           (:158) and the muffle accumulator index (fan * TC + batch slot) * T of
+//                           target 0; muffle_kernel casts its T rays
+// counts[0] / counts[1] = echo pairs / hit records emitted.
 // ------------------------------------------------------------------------------------------
 struct VisPairs {
   float4* seg;
   uint2* out;
-  uint32_t* flag;
-  float4* mrec;
-  float4* msorted;
-  uint32_t* mdest;
+  float4* hrec;
   uint32_t echo_cap;  // multiple of 64
-  int tbits;          // target bits of a muffle record's w
 };
-
-// Bits of a target index (T targets): the muffle records pack (e << bits | t) into 32 bits.
-__host__ __device__ inline int target_bits(int T) {
-  int b = 0;
-  while ((1 << b) < T) ++b;
-  return b;
-}
 
 __device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Seg& s, float& maxd, int& owner) {
   const float4 q0 = vp.seg[2 * (size_t)i], q1 = vp.seg[2 * (size_t)i + 1];
   s = make_seg(mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z));
   maxd = q0.w;
   owner = __float_as_int(q1.w);
-}
-
-// Sort key of a muffle pair: target t and the octahedral Morton cell (32 x 32) of the ray's
-// direction seen from the target, so 64 consecutive sorted pairs form a thin cone with apex t
-// (1024 cells per target: 1.8 % broad-phase candidates in simulation, 4096: 1.6 %). Above 8
-// targets the low Morton bits are dropped so that T << bits stays within the LDS histogram.
-constexpr int kSortDirBits = 10, kSortBins = 8 << kSortDirBits;
-__host__ __device__ inline int sort_dir_bits(int T) {
-  int b = kSortDirBits;
-  while (b > 1 && (T << b) > kSortBins) --b;
-  return b;
-}
-__device__ __forceinline__ uint16_t vis_sort_key(int t, int T, vec3 u) {
-  const float n = fabsf(u.x) + fabsf(u.y) + fabsf(u.z);
-  float a = 0.0f, c = 0.0f;
-  if (n > 0.0f && isfinite(n)) {
-    const float x = u.x / n, y = u.y / n, z = u.z / n;
-    a = z < 0.0f ? (1.0f - fabsf(y)) * (x >= 0.0f ? 1.0f : -1.0f) : x;
-    c = z < 0.0f ? (1.0f - fabsf(x)) * (y >= 0.0f ? 1.0f : -1.0f) : y;
-  }
-  constexpr float kCells = (float)(1 << (kSortDirBits / 2));  // cells per octahedral axis
-  auto q5 = [](float v) { return (uint32_t)fminf(fmaxf((v + 1.0f) * (0.5f * kCells), 0.0f), kCells - 1.0f); };
-  auto sp = [](uint32_t v) {  // 5 bits -> even bit positions
-    v = (v | (v << 4)) & 0x0F0Fu; v = (v | (v << 2)) & 0x3333u; v = (v | (v << 1)) & 0x5555u;
-    return v;
-  };
-  const int bits = sort_dir_bits(T);
-  const uint32_t cell = (sp(q5(a)) | (sp(q5(c)) << 1)) >> (kSortDirBits - bits);
-  return (uint16_t)(((uint32_t)t << bits) | cell);
 }
 
 __device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
@@ -475,7 +383,7 @@ constexpr int kPathWaves = 8;
 template <bool HITS, bool MULTI>
 __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu(4))) void path_kernel(
     DevScene sc, FrameParams fp, FanLayout L, const float* __restrict__ origins, uint8_t* __restrict__ block,
-    const int* __restrict__ ray_order, VisPairs vp, uint32_t* __restrict__ pair_count, uint16_t* __restrict__ pkeys,
+    const int* __restrict__ ray_order, VisPairs vp, uint32_t* __restrict__ pair_count,
     const int2* __restrict__ pre_hits, float4* __restrict__ state, int step) {
   constexpr int K = kPathWaves;
   __shared__ uint32_t s_agg[2][K][2];
@@ -585,57 +493,28 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       hid[ray * H + k] = ART_HIT_ID(type, idx);  // ShootRayCast's (hitColliderType, collider) :225-280
     }
 
-    // visibility pairs: q = 0 echo ray to the origin (:124-145), q = 1..T muffle rays (:150-173),
-    // in rounds of kMaxQueries queries (the ballot masks stay in registers), one reservation each
+    // the echo ray to the fan origin (:124-145), emitted into a live slot only (:118), and the hit
+    // record the T muffle rays start from (:150-173); one reservation for the workgroup
     const vec3 off = o - d * kEps;                 // :124, :158
     const float dist0 = distance(O, o);            // :130 (un-offset hit point)
-    for (int q0 = 0; q0 <= T; q0 += kMaxQueries) {  // block-uniform
-      unsigned long long mq[kMaxQueries];
-      uint32_t actbits = 0, np = 0;
-#pragma unroll
-      for (int qq = 0; qq < kMaxQueries; ++qq) {
-        const int q = q0 + qq;
-        bool act = false;
-        if (q <= T) {
-          if (q == 0) act = live_slot;  // the echo is written only into a live slot (:118)
-          else act = hit && distance(off, load3(sc.targets, q - 1)) < fp.max_muffle;  // :165-168
-        }
-        mq[qq] = __ballot(act);
-        actbits |= act ? (1u << qq) : 0u;
-        np += (uint32_t)__popcll(mq[qq]);
+    {
+      const unsigned long long me = __ballot(live_slot), mr = __ballot(hit);
+      uint32_t eb, rb;
+      reserve((uint32_t)__popcll(me), (uint32_t)__popcll(mr), pair_count, eb, rb);
+      if (live_slot) {
+        const uint32_t at = eb + (uint32_t)__popcll(me & lt);
+        const vec3 qdir = normalize(O - off);
+        vp.seg[2 * (size_t)at] = make_float4(off.x, off.y, off.z, dist0);
+        vp.seg[2 * (size_t)at + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(kNoOwner));
+        vp.out[at] = make_uint2((uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k),
+                                f32tof16(dist0 * echo_of(sc, type, idx)));  // :142-144
       }
-      const uint32_t ne = q0 == 0 ? (uint32_t)__popcll(mq[0]) : 0u, nm = np - ne;
-      uint32_t eb, mb;
-      reserve(ne, nm, pair_count, eb, mb);
-      if (np) {
-        uint32_t pos = mb;  // muffle position (region-relative)
-#pragma unroll
-        for (int qq = 0; qq < kMaxQueries; ++qq) {
-          const int q = q0 + qq;
-          if (q <= T && ((actbits >> qq) & 1u)) {
-            const uint32_t rank = (uint32_t)__popcll(mq[qq] & lt);
-            if (q == 0) {  // the echo ray to the fan origin (:124-145): its segment in full
-              const uint32_t at = eb + rank;
-              const vec3 qdir = normalize(O - off);
-              vp.seg[2 * (size_t)at] = make_float4(off.x, off.y, off.z, dist0);
-              vp.seg[2 * (size_t)at + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(kNoOwner));
-              vp.out[at] = make_uint2((uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + k),
-                                      f32tof16(dist0 * echo_of(sc, type, idx)));  // :142-144
-              vp.flag[at] = 0u;
-            } else {  // a muffle ray to target q - 1 (:150-173): its start, target and counter
-              const uint32_t e = pos + rank;
-              const vec3 qdir = normalize(load3(sc.targets, q - 1) - off);  // :158-160
-              vp.mrec[e] = make_float4(off.x, off.y, off.z, __uint_as_float((e << vp.tbits) | (uint32_t)(q - 1)));
-              vp.mdest[e] = (uint32_t)(((size_t)fan * fp.TC + my_slot) * T + (q - 1));
-              vp.flag[vp.echo_cap + e] = 0u;
-              pkeys[e] = vis_sort_key(q - 1, T, mk3(-qdir.x, -qdir.y, -qdir.z));
-            }
-          }
-          if (q > 0 && q <= T) pos += (uint32_t)__popcll(mq[qq]);
-        }
+      if (hit) {
+        const uint32_t at = rb + (uint32_t)__popcll(mr & lt);
+        vp.hrec[at] = make_float4(off.x, off.y, off.z, __uint_as_float((uint32_t)(((size_t)fan * fp.TC + my_slot) * T)));
       }
     }
-    // a blocked echo leaves the reset value (:76); vis_finalize overwrites the visible ones
+    // a blocked echo leaves the reset value (:76); the echo traversal overwrites the visible ones
     if (live_slot && single_slot) echo[ray * H + k] = 0;
 
     // termination / reflection — :179-193, ReflectRay :456-532
@@ -717,397 +596,18 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
 }
 
 // ------------------------------------------------------------------------------------------
-// Counting sort of the muffle pairs by key (T << bits buckets; the order inside a bucket is free:
-// the any-hit verdicts do not depend on it). Block j of kSortBlock pairs: LDS histogram -> row j
-// of hist[block][bucket]; a column prefix per bucket and the buckets' totals; each scatter block
-// scans the totals and hands out positions with LDS atomics.
-// ------------------------------------------------------------------------------------------
-constexpr int kSortThreads = 256, kSortBlock = 16 * kSortThreads;
-
-// The 16 keys of one thread with two 16-B loads (one memory latency). i0 is a multiple of 16 below
-// the key count and the key array is 256-B aligned and padded, so a read past the last key stays
-// in the buffer; those keys are ignored.
-__device__ __forceinline__ void load_keys16(const uint16_t* keys, uint32_t i0, uint16_t* kk) {
-  const uint4* p = reinterpret_cast<const uint4*>(keys + i0);
-  const uint4 a = p[0], b = p[1];
-  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { kk[2 * j] = (uint16_t)(w[j] & 0xffffu); kk[2 * j + 1] = (uint16_t)(w[j] >> 16); }
-}
-
-__global__ __launch_bounds__(kSortThreads) void pair_hist_kernel(const uint16_t* __restrict__ keys,
-                                                                 const uint32_t* __restrict__ count,
-                                                                 uint32_t* __restrict__ hist, int nblk, int nbins) {
-  __shared__ uint32_t h[kSortBins];
-  for (int i = threadIdx.x; i < nbins; i += kSortThreads) h[i] = 0u;
-  __syncthreads();
-  // each thread counts 16 consecutive keys, one LDS atomic per run of equal keys (the keys of a
-  // wave's rays are coherent, so per-key atomics would serialize on a few bins)
-  const uint32_t n = ldc(count, 1), i0 = blockIdx.x * (uint32_t)kSortBlock + threadIdx.x * 16u;
-  const uint32_t e = min(n, i0 + 16u);
-  uint16_t kk[16];
-  if (i0 < n) load_keys16(keys, i0, kk);
-  uint32_t run = 0, rk = 0;
-  for (uint32_t j = 0; j < 16u; ++j) {
-    if (i0 + j >= e) break;
-    const uint32_t k = kk[j];
-    if (run && k != rk) { atomicAdd(&h[rk], run); run = 0; }
-    rk = k;
-    ++run;
-  }
-  if (run) atomicAdd(&h[rk], run);
-  __syncthreads();
-  for (int i = threadIdx.x; i < nbins; i += kSortThreads) hist[(size_t)blockIdx.x * nbins + i] = h[i];  // row = block
-}
-
-// Column prefix: thread = bucket; hist[block][bucket] becomes the count of the bucket's keys in
-// earlier blocks, and tot[bucket] the bucket's total (rows are read and written coalesced).
-__global__ __launch_bounds__(64) void pair_colscan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ prefix,
-                                                          uint32_t* __restrict__ tot, int nblk, int nbins) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= nbins) return;
-  uint32_t run = 0;
-  int b = 0;
-  for (; b + 8 <= nblk; b += 8) {  // 8 independent loads in flight per step
-    uint32_t c[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) c[j] = hist[(size_t)(b + j) * nbins + k];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { prefix[(size_t)(b + j) * nbins + k] = run; run += c[j]; }
-  }
-  for (; b < nblk; ++b) {
-    const uint32_t c = hist[(size_t)b * nbins + k];
-    prefix[(size_t)b * nbins + k] = run;
-    run += c;
-  }
-  tot[k] = run;
-}
-
-// Each block scans the bucket totals itself (nbins <= kSortBins, 32 per thread) and adds its row
-// of column prefixes: cur[bucket] = first position of this block's keys of that bucket.
-__global__ __launch_bounds__(kSortThreads) void pair_scatter_kernel(const uint16_t* __restrict__ keys,
-                                                                    const uint32_t* __restrict__ count,
-                                                                    const uint32_t* __restrict__ prefix,
-                                                                    const uint32_t* __restrict__ tot,
-                                                                    const float4* __restrict__ mrec,
-                                                                    float4* __restrict__ msorted, int nblk, int nbins) {
-  __shared__ uint32_t cur[kSortBins];
-  __shared__ uint32_t s_part[kSortThreads];
-  __builtin_amdgcn_s_setprio(3);  // on the critical path; issues ahead of the echo traversal beside it
-  constexpr int kPer = kSortBins / kSortThreads;
-  const int t = threadIdx.x;
-  uint32_t v[kPer], sum = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = t * kPer + j;
-    v[j] = k < nbins ? tot[k] : 0u;
-    sum += v[j];
-  }
-  s_part[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < kSortThreads; off <<= 1) {  // inclusive scan of the per-thread sums
-    const uint32_t x = t >= off ? s_part[t - off] : 0u;
-    __syncthreads();
-    s_part[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = s_part[t] - sum;  // exclusive
-  const uint32_t* row = prefix + (size_t)blockIdx.x * nbins;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = t * kPer + j;
-    if (k < nbins) cur[k] = run + row[k];
-    run += v[j];
-  }
-  __syncthreads();
-  const uint32_t n = ldc(count, 1), i0 = blockIdx.x * (uint32_t)kSortBlock + threadIdx.x * 16u;
-  const uint32_t e = min(n, i0 + 16u);
-  uint16_t kk[16];
-  if (i0 < n) load_keys16(keys, i0, kk);
-#pragma unroll
-  for (uint32_t j = 0; j < 16u; ++j) {
-    if (i0 + j >= e) break;
-    msorted[atomicAdd(&cur[kk[j]], 1u)] = mrec[i0 + j];
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Broad phase of the muffle sweep. A batch of 64 sorted pairs (one target, nearby directions seen
-// from it) is reduced to the box of its segments [o, o + maxd d] and an apex cone: all its
-// segments end at (nearly) the same point, the target (:165); echo segments of one wave end at the
-// fan origin (:130). A collider whose widened bounds miss the box or the cone cannot block any
-// lane's segment, so every verdict equals the brute-force OR.
-// ------------------------------------------------------------------------------------------
-struct WaveBox {
-  float lx, ly, lz, hx, hy, hz, om;
-};
-
-// The box of a wave's segments [o, o + maxd d] (valid lanes) and the margin term max |o|_1 + maxd.
-__device__ __forceinline__ WaveBox make_wave_box(const Seg& s, float maxd, bool valid) {
-  WaveBox wb;
-  const vec3 e = s.o + s.d * maxd;
-  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
-  wb.lx = wave_min(valid ? fminf(s.o.x, e.x) : INFINITY);
-  wb.ly = wave_min(valid ? fminf(s.o.y, e.y) : INFINITY);
-  wb.lz = wave_min(valid ? fminf(s.o.z, e.z) : INFINITY);
-  wb.hx = wave_max(valid ? fmaxf(s.o.x, e.x) : -INFINITY);
-  wb.hy = wave_max(valid ? fmaxf(s.o.y, e.y) : -INFINITY);
-  wb.hz = wave_max(valid ? fmaxf(s.o.z, e.z) : -INFINITY);
-  wb.om = wave_max(valid ? om : 0.0f);
-  return wb;
-}
-
-// Apex cone of a wave of segments that (nearly) share their END point. Apex A = the first valid
-// lane's computed end point; every lane's end point lies within `extra` of A (its computed
-// distance, widened for the rounding of o + maxd d), so each segment lies in the hull of its
-// start o and the ball (A, extra), and that hull lies in cone(A, axis, theta) (+) ball(extra) once
-// o is inside the cone. Starts inside the ball need no cone. A wave with a non-finite segment,
-// whose starts all lie in the ball, or whose cone is wider than a half-space, is not cone-culled
-// (on = false). theta carries a 2e-3 rad slack for the rounding of the normalisations.
-struct VisCone {
-  float ax, ay, az;       // apex
-  float nx, ny, nz;       // unit axis
-  float cos2, sin_t;      // cos^2 and sin of the half-angle
-  float extra;            // apex ball radius
-  bool on;
-};
-
-__device__ __forceinline__ VisCone make_vis_cone(const Seg& s, float maxd, bool valid, float om) {
-  VisCone vc;
-  const vec3 e = s.o + s.d * maxd;
-  const unsigned long long vm = __ballot(valid);
-  const int first = vm ? (int)__builtin_ctzll(vm) : 0;
-  vc.ax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.x), first));
-  vc.ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.y), first));
-  vc.az = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.z), first));
-  const float ex = e.x - vc.ax, ey = e.y - vc.ay, ez = e.z - vc.az;
-  const float re = sqrtf(ex * ex + ey * ey + ez * ez);
-  vc.extra = wave_max(valid ? re : 0.0f) * 1.001f + 1e-6f * om + 1e-6f;
-  const float vx = s.o.x - vc.ax, vy = s.o.y - vc.ay, vz = s.o.z - vc.az;
-  const float l2 = vx * vx + vy * vy + vz * vz;
-  const float l = sqrtf(l2);
-  const bool fin = isfinite(l2) && isfinite(re) && isfinite(maxd) && isfinite(s.d.x) && isfinite(s.d.y) && isfinite(s.d.z);
-  const bool use = valid && fin && l > vc.extra;
-  const float inv = use ? 1.0f / l : 0.0f;
-  const float ux = vx * inv, uy = vy * inv, uz = vz * inv;
-  const float sx = wave_sum(ux), sy = wave_sum(uy), sz = wave_sum(uz);
-  const float sn = sqrtf(sx * sx + sy * sy + sz * sz);
-  vc.nx = 1.0f; vc.ny = 0.0f; vc.nz = 0.0f; vc.cos2 = 0.0f; vc.sin_t = 1.0f; vc.on = false;
-  if (!(sn > 0.0f) || __any(valid && !fin) || !isfinite(vc.extra)) return vc;
-  vc.nx = sx / sn; vc.ny = sy / sn; vc.nz = sz / sn;
-  float c = wave_min(use ? ux * vc.nx + uy * vc.ny + uz * vc.nz : INFINITY);
-  c = fminf(c, 1.0f);
-  const float s0 = sqrtf(fmaxf(0.0f, 1.0f - c * c));
-  constexpr float ce = 0.999998f, se = 0.002f;  // cos / sin of the slack angle
-  const float cos_t = c * ce - s0 * se;
-  vc.sin_t = s0 * ce + c * se;
-  vc.cos2 = cos_t * cos_t;
-  vc.on = cos_t > 0.0f;
-  return vc;
-}
-
-// Does the collider's widened bounding sphere (centre c, radius rho) meet cone (+) ball(extra)?
-// Distance from c to the cone's lateral surface is perp cos(theta) - proj sin(theta) (negative
-// inside; for c behind the apex it is at most |c - A|, so the test only over-admits there):
-// candidate iff perp cos <= rho' + proj sin =: rhs, evaluated squared (no sqrt or division) with
-// an absolute slack of 1e-6 |c - A|^2 for the cancellation in perp^2 = |v|^2 - proj^2. Non-finite
-// bounds give NaN/inf terms, which every comparison below admits.
-__device__ __forceinline__ bool vis_cone_cand(const VisCone& vc, const CullRec& cr, float om) {
-  const float cx = 0.5f * (cr.lox + cr.hix), cy = 0.5f * (cr.loy + cr.hiy), cz = 0.5f * (cr.loz + cr.hiz);
-  const float rho = 0.5f * ((cr.hix - cr.lox) + (cr.hiy - cr.loy) + (cr.hiz - cr.loz)) * 1.001f +
-                    cr.factor * (cr.scale + om) + vc.extra;
-  const float vx = cx - vc.ax, vy = cy - vc.ay, vz = cz - vc.az;
-  const float l2 = vx * vx + vy * vy + vz * vz;
-  const float pj = vx * vc.nx + vy * vc.ny + vz * vc.nz;
-  const float rhs = rho + pj * vc.sin_t;
-  const float perp2 = l2 - pj * pj;
-  return !(rhs < 0.0f) && !(perp2 * vc.cos2 > rhs * rhs + 1e-6f * l2);
-}
-
-constexpr int kCullU = 4;  // candidate tests per scalar-load group
-
-template <int U, typename Rec, typename Test>
-__device__ __forceinline__ bool test_candidates(const Rec* recs, int b, CandSet& cs, bool blocked, bool done, Test test,
-                                                unsigned& nt) {
-  while (cs.left >= U) {
-    nt += U;
-    int idx[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) idx[u] = b + cs.pop();
-    Rec r[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) r[u] = ldc(recs, wave_uniform(idx[u]));
-#pragma unroll
-    for (int u = 0; u < U; ++u) blocked |= test(r[u]);
-    if (__all(blocked || done)) return blocked;
-  }
-  while (cs.left > 0) {
-    const Rec r = ldc(recs, wave_uniform(b + cs.pop()));
-    blocked |= test(r);
-    ++nt;
-  }
-  return blocked;
-}
-
-// Any-hit sweep of one lane's segment (s, maxd, owner) over the sorted chunks [c_lo, c_hi) for a
-// wave of up to 64 segments (`valid` lanes): the chunks' union bounds first (lane = chunk), then
-// the members of the candidate chunks (lane = collider), then exact wave-uniform tests of the
-// candidates. Any-hit is an OR over the colliders, so the order is free. Returns the lane's
-// verdict (true = blocked).
-template <bool OBB>
-__device__ __forceinline__ bool cull_sweep(const DevScene& sc, const Seg& s, float maxd, int owner, bool valid, int lane,
-                                           unsigned long long* ex, int c_lo, int c_hi, const VisCone& vc) {
-  const int cs_n = (sc.ns + kChunk - 1) / kChunk, ca_n = (sc.na + kChunk - 1) / kChunk;
-  const int nchunks = min(sc.nchunks, c_hi);
-  if (c_lo >= nchunks) return false;
-  const WaveBox wb = make_wave_box(s, maxd, valid);
-  bool blocked = false;
-  const bool done = !valid;
-  if (__all(done)) return false;
-  unsigned nt[3] = {0u, 0u, 0u}, nchk = 0u;
-  // broad-phase candidate: widened bounds meet the wave box and the cone
-  auto candidate = [&](const CullRec& cr) {
-    const float m = cr.factor * (cr.scale + wb.om);
-    bool c = (cr.lox - m <= wb.hx) & (cr.hix + m >= wb.lx) & (cr.loy - m <= wb.hy) & (cr.hiy + m >= wb.ly) &
-             (cr.loz - m <= wb.hz) & (cr.hiz + m >= wb.lz);
-    if (vc.on && __any(c)) c = c && vis_cone_cand(vc, cr, wb.om);
-    return c;
-  };
-  const float oml = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
-  const bool force = force_all(s, oml);
-  for (int pb = c_lo; pb < nchunks; pb += 64) {
-    const int pc = pb + lane;
-    bool ccand = false;
-    if (pc < nchunks) ccand = candidate(sc.chunks[pc]);
-    unsigned long long cm_mask = __ballot(ccand);
-    ++nchk;
-    while (cm_mask) {
-      const int c = pb + (int)__builtin_ctzll(cm_mask);
-      cm_mask &= cm_mask - 1;
-      int type, b, n, g;
-      if (c < cs_n) { type = 0; b = c * kChunk; n = min(kChunk, sc.ns - b); g = b; }
-      else if (c < cs_n + ca_n) { type = 1; b = (c - cs_n) * kChunk; n = min(kChunk, sc.na - b); g = sc.ns + b; }
-      else { type = 2; b = (c - cs_n - ca_n) * kChunk; n = min(kChunk, sc.no - b); g = sc.ns + sc.na + b; }
-      bool cand = false;
-      if (lane < n) cand = candidate(sc.cull_s[g + lane]);
-      CandSet cs;
-      cs.m = __ballot(cand);
-      cs.left = __popcll(cs.m);
-      ++nchk;
-      if (cs.left == 0) continue;
-      if (type == 0) {
-        blocked = test_candidates<kCullU>(sc.sph_s, b, cs, blocked, done, [&](const SphereRec& r) {
-          float d;
-          return sphere_hit_dist(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[0]);
-      } else if (type == 1) {
-        blocked = test_candidates<kCullU>(sc.aabb_s, b, cs, blocked, done, [&](const AabbRec& r) {
-          float d;
-          return aabb_test<false>(s, r, d) && d < maxd && r.tid != owner;
-        }, nt[1]);
-      } else if (OBB) {
-        // OBB candidates (118-op exact test): first each lane's slab test against the collider's own
-        // widened bounds (a blocker's segment enters them before maxd); the
-        // exact test runs only where a live lane passes
-        const CullRec* cb = sc.cull_s + sc.ns + sc.na;
-        while (cs.left > 0) {
-          const int i = wave_uniform(b + cs.pop());
-          const CullRec cr = ldc(cb, i);
-          float tn;
-          const bool h = node_entry(s, cr, oml, tn);
-          const bool near = force || (h && tn <= maxd);
-          if (!__any(near && !blocked && !done)) continue;
-          const ObbRec r = ldc(sc.obb_s, i);
-          ++nt[2];
-          if (near && !blocked) {
-            float d;
-            blocked = obb_test<false>(s, r, stored_q(r), d) && d < maxd && r.tid != owner;
-          }
-          if (__all(blocked || done)) break;
-        }
-      }
-      if (__all(blocked || done)) break;
-    }
-    if (__all(blocked || done)) break;
-  }
-  exec_add(ex, kExecSphere, 64ull * nt[0]);
-  exec_add(ex, kExecAabb, 64ull * nt[1]);
-  exec_add(ex, kExecObb, 64ull * nt[2]);
-  exec_add(ex, kExecCullBox, 64ull * nchk);
-  return blocked;
-}
-
-// Chunk ranges per 64-pair batch (work items of the muffle sweep), by scene kind: each range
-// repeats the batch's setup, while OBB tests are long and balance better over more items.
-// Measured (raytrace stage): no OBBs 2 ranges (config 2: 218 vs 231 us at 4, 274 at 1); OBB
-// majority 8 (config 3: 0.98 vs 1.01 ms at 4); some OBBs 4 (config 4: 5.73 vs 5.84 ms at 8,
-// config 5: 2.69 vs 2.81).
-__host__ __device__ __forceinline__ int vis_ranges(const DevScene& sc) {
-  return 2 * sc.no > sc.ns + sc.na + sc.no ? 8 : (sc.no > 0 ? 4 : 2);
-}
-
-// Work item i of the muffle sweep = (chunk range r, sorted batch b), range-major: r = i / nbm,
-// b = i % nbm. Lane = sorted position 64 b + lane: its record gives the segment's start, its target
-// t and its emission index e; maxd and the direction to the target are recomputed with the path
-// kernel's operations (:158-168), so the segment is the one the reference tests. A batch's later
-// ranges usually start after its earlier ones finished and skip the pairs those already blocked:
-// a blocker sets bit 31 of the sorted record (coalesced, read with the record; a stale read only
-// costs work) and the pair's flag[echo_cap + e] for vis_finalize, both by relaxed device-scope
-// atomicOr (no fences: an agent-scope release writes back the XCD's L2); vis_finalize writes the
-// outputs after the kernel boundary.
-template <bool OBB>
-__device__ __forceinline__ void vis_sweep_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                               uint32_t nbm, unsigned long long* ex, uint32_t blk) {
-  const int lane = threadIdx.x & 63;
-  __builtin_amdgcn_s_setprio(1);  // the sweep ends the frame's critical path; the echo waves beside it have slack
-  const uint32_t item = blk * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t r = item / nbm, b = item - r * nbm;
-  const int nranges = vis_ranges(sc);
-  const uint32_t base = b * 64u, n = ldc(count, 1);
-  if (r >= (uint32_t)nranges || base >= n) return;
-  const uint32_t n_in = min(64u, n - base);
-  const uint32_t p = base + ((uint32_t)lane < n_in ? (uint32_t)lane : 0u);
-  const float4 rec = vp.msorted[p];
-  const uint32_t wv = __float_as_uint(rec.w), e = (wv & 0x7fffffffu) >> vp.tbits;
-  const int t = (int)(wv & ((1u << vp.tbits) - 1u));
-  // pairs an earlier range already blocked (bit 31 of the sorted record) are skipped (out of the
-  // wave's box)
-  const bool valid = (uint32_t)lane < n_in && (wv >> 31) == 0u;
-  if (!__any(valid)) return;
-  Seg s;
-  float maxd = 0.0f;
-  s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
-  s.a2 = 0.0f;
-  if (valid) {
-    const vec3 off = mk3(rec.x, rec.y, rec.z), tp = load3(sc.targets, t);
-    maxd = distance(off, tp);                // :165
-    s = make_seg(off, normalize(tp - off));  // :158-160
-  }
-  const int nch = sc.nchunks;
-  const int c_lo = (int)(((long long)nch * r) / nranges), c_hi = (int)(((long long)nch * (r + 1)) / nranges);
-  const float om = wave_max(valid ? fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd : 0.0f);
-  const VisCone vc = make_vis_cone(s, maxd, valid, om);
-  const bool blocked = cull_sweep<OBB>(sc, s, maxd, t, valid, lane, ex, c_lo, c_hi, vc);  // owner = t (:413, :426, :439)
-  if (valid && blocked) {
-    __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(vp.msorted + p) + 3, 0x80000000u, __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_or(vp.flag + vp.echo_cap + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // Echo visibility by quad-per-segment BVH traversal. An echo batch is one wave's rays of one fan
 // traced back to the fan origin: 64 segments fanning over an eighth of the sphere, whose box and
 // cone admit ~10 % of the colliders, so a sweep would spend most of its time there. Per segment
 // the BVH visits only the nodes along it: a segment enters a node when its widened box is entered
 // before maxd (a blocker's computed distance d < maxd lies strictly after every ancestor's
 // entry), 4 lanes per segment (lane q: child q / leaf slot q; the quad agrees through ballots),
-// the first blocker ends the segment.
+// the first blocker ends the segment; a segment no collider blocks stores its echo.
 // ------------------------------------------------------------------------------------------
 template <bool OBB>
 __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
                                               unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
-                                              const uint32_t* ecnt, int bounce) {
+                                              const uint32_t* ecnt, int bounce, uint8_t* block) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
   const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64-pair batch
   // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
@@ -1171,7 +671,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       }
     }
   }
-  if (valid && blocked && qd == 0) vp.flag[p] = 1u;
+  if (valid && !blocked && qd == 0) {  // visible: the echo is stored (:142-144)
+    const uint2 o = vp.out[p];
+    reinterpret_cast<uint16_t*>(block)[o.x] = (uint16_t)(o.y & 0xffffu);
+  }
   if (ex) {
     exec_add(ex, kExecSphere, wave_sum_u32(nt[0]));
     exec_add(ex, kExecAabb, wave_sum_u32(nt[1]));
@@ -1180,112 +683,170 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   }
 }
 
-// One launch for both visibility halves, so they overlap on the chip: blocks [0, n_echo) trace
-// the echo batches by quad BVH traversal (longer jobs first), the others run the sweep's items.
-// EX: count the executed tests (fp.exec); without it the counters compile out. 8 waves per SIMD
-// (a few VGPRs spill; measured faster than 6 or 7).
+// The echo traversal: one 64-pair batch per workgroup. EX: count the executed tests (fp.exec);
+// without it the counters compile out. 8 waves per SIMD.
 template <bool EX, bool OBB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, uint32_t nbm, unsigned long long* ex,
-                uint32_t n_echo, const uint32_t* __restrict__ ecnt, int bounce) {
+void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, unsigned long long* ex,
+                const uint32_t* __restrict__ ecnt, int bounce, uint8_t* __restrict__ block) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
-  unsigned long long* e = EX ? ex : nullptr;
-  if (blockIdx.x < n_echo) vis_quad_body<OBB>(sc, vp, count, e, blockIdx.x, s_stk, ecnt, bounce);
-  else vis_sweep_body<OBB>(sc, vp, count, nbm, e, blockIdx.x - n_echo);
+  vis_quad_body<OBB>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, ecnt, bounce, block);
 }
 
-// Outputs of the visibility pairs once every range has run (the kernel boundary makes the verdicts
-// visible): visible echoes are stored, visible muffle rays counted.
-__global__ __launch_bounds__(256) void vis_finalize(VisPairs vp, const uint32_t* __restrict__ count,
-                                                    uint8_t* __restrict__ block, uint32_t* __restrict__ muffle_acc) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t p = blockIdx.x * 256u + threadIdx.x, wbase = __builtin_amdgcn_readfirstlane(p - lane);
-  const bool echo_region = wbase < vp.echo_cap;  // echo_cap is a multiple of 64: one region per wave
-  const uint32_t n = echo_region ? ldc(count, 0) : ldc(count, 1), rel = echo_region ? p : p - vp.echo_cap;
-  if (__builtin_amdgcn_readfirstlane(rel - lane) >= n) return;
-  const bool valid = rel < n;
-  uint32_t flag = 1u, dest = 0u, val = 0u;
-  const bool muf = !echo_region;
-  if (valid) {
-    flag = vp.flag[p];
-    if (muf) { dest = vp.mdest[rel]; } else { const uint2 o = vp.out[p]; dest = o.x; val = o.y; }
+// ------------------------------------------------------------------------------------------
+// Muffle rays (:150-173, CanRaySeeAudioTarget :405-449). One lane per hit record; for each target
+// t (wave-uniform) the lane's ray from `off` to the target (distance < MaxMuffleHitDistance,
+// :165-168) is tested against the colliders of its direction cell around the target
+// (art_cells.hip: not owned by t, widened bounding sphere on the ray) and stops at its first
+// blocker; the wave counts its visible rays into the muffle accumulators with one atomic per
+// distinct counter (its records come from one or two 64-ray groups). Any-hit is an OR over the
+// colliders, so the cell lists' order is free.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int cube_cell(vec3 v) {
+  const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z);
+  const int m = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+  const float c[3] = {v.x, v.y, v.z};
+  const float n = fabsf(c[m]);
+  const float u = c[(m + 1) % 3] / n, w = c[(m + 2) % 3] / n;
+  const int i = min(max((int)floorf((u + 1.0f) * (0.5f * kCellG)), 0), kCellG - 1);
+  const int j = min(max((int)floorf((w + 1.0f) * (0.5f * kCellG)), 0), kCellG - 1);
+  const int f = 2 * m + (c[m] < 0.0f ? 1 : 0);
+  return (f * kCellG + j) * kCellG + i;
+}
+
+// Exact test of collider `code` (rank << 28 | index, reference records) against segment s.
+template <bool OBB>
+__device__ __forceinline__ bool muffle_test(const DevScene& sc, const Seg& s, uint32_t code, float maxd, unsigned* nt) {
+  const uint32_t type = code >> 28, idx = code & 0x0fffffffu;
+  float d;
+  bool h;
+  if (type == 0) {
+    const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
+    SphereRec r;
+    r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
+    ++nt[0];
+    h = sphere_hit_dist(s, r, d);
+  } else if (type == 1 || !OBB) {
+    const AabbRec r = sc.aabb[idx];
+    ++nt[1];
+    h = aabb_test<false>(s, r, d);
+  } else {
+    const ObbRec r = sc.obb[idx];
+    ++nt[2];
+    h = obb_test<false>(s, r, stored_q(r), d);
   }
-  const bool vis = valid && flag == 0u;
-  if (vis && !muf) reinterpret_cast<uint16_t*>(block)[dest] = (uint16_t)(val & 0xffffu);  // :142-144
-  // muffle counts (:171): one atomic per distinct counter of the wave (its pairs come from one or
-  // two (fan, target) groups of the emission order)
-  unsigned long long mv = __ballot(vis && muf);
-  while (mv) {
-    const uint32_t d0 = __builtin_amdgcn_readlane(dest, __builtin_ctzll(mv));
-    const unsigned long long eq = __ballot(vis && muf && dest == d0);
-    if (lane == 0) atomicAdd(&muffle_acc[d0], (uint32_t)__popcll(eq));
-    mv &= ~eq;
+  return h && d < maxd;
+}
+
+// Every collider not owned by target t, in reference order (lists unavailable or not applicable).
+template <bool OBB>
+__device__ bool muffle_brute(const DevScene& sc, const Seg& s, float maxd, int t, unsigned* nt) {
+  for (int i = 0; i < sc.ns; ++i)
+    if (sc.sph[i].tid != t && muffle_test<OBB>(sc, s, (uint32_t)i, maxd, nt)) return true;
+  for (int i = 0; i < sc.na; ++i)
+    if (sc.aabb[i].tid != t && muffle_test<OBB>(sc, s, (1u << 28) | (uint32_t)i, maxd, nt)) return true;
+  for (int i = 0; i < sc.no; ++i)
+    if (sc.obb[i].tid != t && muffle_test<true>(sc, s, (2u << 28) | (uint32_t)i, maxd, nt)) return true;
+  return false;
+}
+
+template <bool EX, bool OBB>
+__global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
+                                                     const uint32_t* __restrict__ count, uint32_t* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t n = ldc(count, 1);
+  if (__builtin_amdgcn_readfirstlane(i - (uint32_t)lane) >= n) return;
+  const bool valid = i < n;
+  const float4 r = vp.hrec[valid ? i : 0u];
+  const vec3 off = mk3(r.x, r.y, r.z);
+  const uint32_t dbase = __float_as_uint(r.w);
+  const float o1 = fabsf(off.x) + fabsf(off.y) + fabsf(off.z);
+  unsigned nt[3] = {0u, 0u, 0u};
+  for (int t = 0; t < fp.T; ++t) {  // wave-uniform
+    const vec3 tp = load3(sc.targets, t);
+    const float maxd = distance(off, tp);                             // :165
+    const bool act = valid && maxd < fp.max_muffle;                   // :168
+    bool blocked = false;
+    if (act) {
+      const Seg s = make_seg(off, normalize(tp - off));               // :158-160
+      const vec3 v = off - tp;                                        // the ray seen from the target
+      const bool lists = sc.cell_ok[t] != 0u && o1 + maxd <= sc.cell_om[t] && (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f) &&
+                         isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
+      if (lists) {
+        const uint32_t* st = sc.cell_start + (size_t)t * kCells + cube_cell(v);
+        const uint32_t b = st[0], e = st[1];
+        const float lim = maxd * 1.00001f + 1e-6f;
+        for (uint32_t k = b; k < e; ++k) {
+          const uint2 en = sc.cell_ent[k];
+          if (__uint_as_float(en.y) > lim) continue;  // the collider lies beyond the segment
+          if (muffle_test<OBB>(sc, s, en.x, maxd, nt)) { blocked = true; break; }
+        }
+      } else {
+        blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
+      }
+    }
+    const bool vis = act && !blocked;                                 // :171
+    unsigned long long mv = __ballot(vis);
+    const uint32_t dest = dbase + (uint32_t)t;
+    while (mv) {
+      const uint32_t d0 = __builtin_amdgcn_readlane(dest, __builtin_ctzll(mv));
+      const unsigned long long eq = __ballot(vis && dest == d0);
+      if (lane == 0) atomicAdd(&acc[d0], (uint32_t)__popcll(eq));
+      mv &= ~eq;
+    }
+  }
+  if (EX) {  // lane-tests executed (each lane's own tests; the loop is per lane)
+    exec_add(fp.exec, kExecSphere, wave_sum_u32(nt[0]));
+    exec_add(fp.exec, kExecAabb, wave_sum_u32(nt[1]));
+    exec_add(fp.exec, kExecObb, wave_sum_u32(nt[2]));
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
-// Pair buffer: VisPairs (echo seg | echo out | flag | muffle records | sorted records | muffle dest)
-// | first-segment hits | ray state + live list (multi-hit) | muffle keys u16 | hist, scanned hist
-// u32[bins x blocks] | bucket totals.
+// Pair buffer: echo segments | echo outputs | hit records | first-segment hits | ray state + live
+// list (multi-hit).
 struct PairBufs {
   VisPairs vp;
-  uint16_t* keys;
-  uint32_t *hist, *prefix, *tot;
   int2* pre;        // [groups * 64] nearest hits of the current bounce
   float4* state;    // [groups * 64][2] ray state between the bounce launches (multi-hit frames)
   size_t total;
-  int nblk, nbins;
 };
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static size_t echo_cap_of(const FrameParams& fp) { return ((size_t)fp.S * fp.R * fp.H + 63) & ~(size_t)63; }
-static size_t muffle_cap_of(const FrameParams& fp) { return (size_t)fp.S * fp.R * fp.H * fp.T; }
 
 static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   PairBufs b{};
-  const size_t ecap = echo_cap_of(fp), mcap = muffle_cap_of(fp), max_pairs = ecap + mcap;
+  const size_t ecap = echo_cap_of(fp), hcap = (size_t)fp.S * fp.R * fp.H;
   const size_t slots = (size_t)fp.S * ((fp.R + 63) / 64) * 64;
   uint8_t* p = static_cast<uint8_t*>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) { uint8_t* q = p ? p + off : nullptr; off += align256(bytes); return q; };
   b.vp.seg = reinterpret_cast<float4*>(take(ecap * 32));
   b.vp.out = reinterpret_cast<uint2*>(take(ecap * 8));
-  b.vp.flag = reinterpret_cast<uint32_t*>(take(max_pairs * 4));
-  b.vp.mrec = reinterpret_cast<float4*>(take(mcap * 16));
-  b.vp.msorted = reinterpret_cast<float4*>(take(mcap * 16));
-  b.vp.mdest = reinterpret_cast<uint32_t*>(take(mcap * 4));
+  b.vp.hrec = reinterpret_cast<float4*>(take(hcap * 16));
   b.vp.echo_cap = (uint32_t)ecap;
-  b.vp.tbits = target_bits(fp.T);
   b.pre = reinterpret_cast<int2*>(take(slots * sizeof(int2)));
   if (fp.H > 1) b.state = reinterpret_cast<float4*>(take(slots * (2 * sizeof(float4) + 4) + 2 * kLiveCounters * 4));
-  if (mcap) {
-    b.nblk = (int)((mcap + kSortBlock - 1) / kSortBlock);
-    b.nbins = fp.T << sort_dir_bits(fp.T);  // keys (target << bits | cell) < T << bits <= kSortBins
-    const size_t cells = (size_t)b.nbins * b.nblk;
-    b.keys = reinterpret_cast<uint16_t*>(take(mcap * 2 + 64));  // + padding for load_keys16 past the end
-    b.hist = reinterpret_cast<uint32_t*>(take(cells * 4));
-    b.prefix = reinterpret_cast<uint32_t*>(take(cells * 4));
-    b.tot = reinterpret_cast<uint32_t*>(take((size_t)b.nbins * 4));
-  }
   b.total = off;
   return b;
 }
 
 size_t fast_pair_bytes(const FrameParams& fp) { return pair_bufs(nullptr, fp).total; }
 
-// Fans per launch_raytrace_fast call: pair slots (echo + muffle, R*H*(T+1) per fan) stay below
-// 2^31 (u32 slots and sorted positions), muffle emission indices fit the records' 31 - tbits bits,
-// and a fan's echo halves stay addressable with a 32-bit half offset into the block
+// Fans per launch_raytrace_fast call: echo pairs and hit records (R*H per fan each) stay below
+// 2^31 (u32 indices), the muffle accumulator index (fan * TC + slot) * T + t fits 32 bits, and a
+// fan's echo halves stay addressable with a 32-bit half offset into the block
 // (fan * stride / 2 < 2^32).
-int fast_fans_per_launch(int R, int H, int T, uint32_t stride) {
-  const unsigned long long per_fan = (unsigned long long)R * H * (T + 1) + 64;
+int fast_fans_per_launch(int R, int H, int T, int TC, uint32_t stride) {
+  const unsigned long long per_fan = (unsigned long long)R * H + 64;
   const unsigned long long by_pairs = ((1ull << 31) - 64) / per_fan;
-  const unsigned long long mper_fan = (unsigned long long)R * H * (T > 0 ? T : 1);
-  const unsigned long long by_rec = ((1ull << (31 - target_bits(T))) - 1) / mper_fan;
+  const unsigned long long by_dest = ((1ull << 32) - 1) / ((unsigned long long)(TC > 0 ? TC : 1) * (T > 0 ? T : 1));
   const unsigned long long by_block = ((1ull << 33) - 1) / (stride ? stride : 1) - 1;
-  unsigned long long n = std::min(std::min(std::min(by_pairs, by_rec), by_block), (unsigned long long)(1 << 24));
+  unsigned long long n = std::min(std::min(std::min(by_pairs, by_dest), by_block), (unsigned long long)(1 << 24));
   if (const char* e = getenv("ART_FAST_CHUNK_FANS")) {  // test hook: force small chunks
     const long long v = atoll(e);
     if (v > 0) n = std::min(n, (unsigned long long)v);
@@ -1298,32 +859,28 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                           hipStream_t st, const SideStream& echo) {
   if (fp.S == 0) return;
   const PairBufs pb = pair_bufs(pair_buf, fp);
-  const size_t mcap = muffle_cap_of(fp), max_pairs = (size_t)pb.vp.echo_cap + mcap;
   const unsigned groups = (unsigned)((size_t)fp.S * ((fp.R + 63) / 64));
   const unsigned path_blocks = (groups + kPathWaves - 1) / kPathWaves;
   const bool multi = fp.H > 1;
   const bool obb = sc.no > 0;  // OBB-free scenes run instantiations without the OBB tests
   const uint32_t nacc = (uint32_t)((size_t)fp.S * fp.TC * fp.T);  // this chunk's muffle accumulators
-  const uint32_t nb_max = (uint32_t)(pb.vp.echo_cap / 64 + (mcap + 63) / 64);
-  const uint32_t eb = pb.vp.echo_cap / 64;  // echo batches (one workgroup each)
-  const uint32_t nbm = nb_max - eb;         // muffle batches (vis_ranges items each, 4 per workgroup)
-  const size_t mblocks = ((size_t)nbm * vis_ranges(sc) + 3) / 4;
+  const uint32_t eb = pb.vp.echo_cap / 64;                         // echo batches (one workgroup each)
+  const size_t hcap = (size_t)fp.S * fp.R * fp.H;
   uint32_t* ecnt = pb.state ? reinterpret_cast<uint32_t*>(pb.state + 2 * (size_t)groups * 64) + (size_t)groups * 64 + kLiveCounters
                             : nullptr;  // per-bounce echo counts (echo_counts)
-#define ART_VIS(S_, BLOCKS_, NECHO_, B_, EX_, OBB_)                                                                \
-  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, nbm, \
-                     EX_ ? fp.exec : nullptr, NECHO_, ecnt, B_)
-#define ART_VIS_ANY(S_, BLOCKS_, NECHO_, B_)                                                                      \
+#define ART_VIS(S_, BLOCKS_, B_, EX_, OBB_)                                                                     \
+  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, \
+                     EX_ ? fp.exec : nullptr, ecnt, B_, block)
+#define ART_VIS_ANY(S_, BLOCKS_, B_)                                                                              \
   do {                                                                                                           \
-    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, B_, true, true); else ART_VIS(S_, BLOCKS_, NECHO_, B_, true, false); } \
-    else { if (obb) ART_VIS(S_, BLOCKS_, NECHO_, B_, false, true); else ART_VIS(S_, BLOCKS_, NECHO_, B_, false, false); }    \
+    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, B_, true, true); else ART_VIS(S_, BLOCKS_, B_, true, false); } \
+    else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true); else ART_VIS(S_, BLOCKS_, B_, false, false); }       \
   } while (0)
   // The echo traversal (latency-bound) needs only the path kernel's pairs, so it runs on the side
   // stream: in multi-hit frames each bounce's echoes right after that bounce's path kernel, beside
-  // the next bounces' nearest traversals (their tails leave CUs idle) and then the pair sort; in
-  // one-hit frames beside the pair sort and the VALU-bound muffle sweep. Without a side stream both
-  // halves share one vis_kernel launch (echo workgroups first).
-  const bool split = echo.st && eb && mcap;
+  // the next bounces' nearest traversals (their tails leave CUs idle); in one-hit frames beside the
+  // muffle kernel. Without a side stream it runs on st.
+  const bool split = echo.st != nullptr;
   const bool per_bounce = split && multi && ecnt;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
 #define ART_NEAREST(EX_, OBB_)                                                                                      \
@@ -1334,41 +891,37 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
 #undef ART_NEAREST
 #define ART_PATH(H_, M_)                                                                                              \
   hipLaunchKernelGGL((path_kernel<H_, M_>), dim3(path_blocks), dim3(64 * kPathWaves), 0, st, sc, fp, L, origins, block, \
-                     ray_order, pb.vp, pair_count, pb.keys, pb.pre, pb.state, k)
+                     ray_order, pb.vp, pair_count, pb.pre, pb.state, k)
     if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
     else { if (multi) ART_PATH(false, true); else ART_PATH(false, false); }
 #undef ART_PATH
     if (per_bounce) {  // this bounce's echoes (at most one per ray slot: `groups` batches)
       (void)hipEventRecord(echo.fork, st);
       (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-      ART_VIS_ANY(echo.st, groups, groups, k);
+      ART_VIS_ANY(echo.st, groups, k);
     }
   }
-  if (!nb_max) return;
-  if (split && !per_bounce) {
-    (void)hipEventRecord(echo.fork, st);
-    (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-    ART_VIS_ANY(echo.st, eb, eb, -1);
+  if (!per_bounce) {
+    if (split) {
+      (void)hipEventRecord(echo.fork, st);
+      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+      ART_VIS_ANY(echo.st, eb, -1);
+    } else {
+      ART_VIS_ANY(st, eb, -1);
+    }
   }
-  if (split) (void)hipEventRecord(echo.join, echo.st);
-  if (mcap) {
-    hipLaunchKernelGGL(pair_hist_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.hist, pb.nblk,
-                       pb.nbins);
-    hipLaunchKernelGGL(pair_colscan_kernel, dim3((pb.nbins + 63) / 64), dim3(64), 0, st, pb.hist, pb.prefix, pb.tot, pb.nblk,
-                       pb.nbins);
-    hipLaunchKernelGGL(pair_scatter_kernel, dim3(pb.nblk), dim3(kSortThreads), 0, st, pb.keys, pair_count, pb.prefix, pb.tot,
-                       pb.vp.mrec, pb.vp.msorted, pb.nblk, pb.nbins);
-  }
-  if (split) {
-    ART_VIS_ANY(st, mblocks, 0u, -1);
-    (void)hipStreamWaitEvent(st, echo.join, 0);
-  } else if (eb + mblocks) {
-    ART_VIS_ANY(st, eb + mblocks, eb, -1);
-  }
+  const unsigned mblocks = (unsigned)((hcap + 255) / 256);  // hit records: at most one per ray and bounce
+#define ART_MUFFLE(EX_, OBB_) \
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_>), dim3(mblocks), dim3(256), 0, st, sc, fp, pb.vp, pair_count, muffle_acc)
+  if (fp.exec) { if (obb) ART_MUFFLE(true, true); else ART_MUFFLE(true, false); }
+  else { if (obb) ART_MUFFLE(false, true); else ART_MUFFLE(false, false); }
+#undef ART_MUFFLE
 #undef ART_VIS_ANY
 #undef ART_VIS
-  hipLaunchKernelGGL(vis_finalize, dim3((unsigned)((max_pairs + 255) / 256)), dim3(256), 0, st, pb.vp, pair_count, block,
-                     muffle_acc);
+  if (split) {
+    (void)hipEventRecord(echo.join, echo.st);
+    (void)hipStreamWaitEvent(st, echo.join, 0);
+  }
 }
 
 }  // namespace art
