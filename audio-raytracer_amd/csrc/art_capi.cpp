@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -28,7 +29,9 @@
 #include "unity_math.hpp"
 
 #include <cmath>
+#include <csignal>
 #include <cstdlib>
+#include <execinfo.h>
 
 using namespace art;
 
@@ -117,7 +120,9 @@ struct Device {
     GraphKey key;
     hipGraphExec_t exec = nullptr;
     uint64_t used = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // permeation fork / join, echo fork / join
   };
+  std::vector<hipEvent_t> graph_events;  // every graph's events (kept for the process's life)
   hipStream_t cap = nullptr;
   std::vector<Graph> graphs;
   uint64_t graph_clock = 0, graph_captures = 0;
@@ -632,7 +637,9 @@ hipEvent_t pool_event(Device& dv, size_t i) {
   return dv.ev_pool[i];
 }
 
-constexpr size_t kGraphCache = 4;  // instantiated frame graphs kept per device
+constexpr size_t kGraphCache = 16;         // instantiated frame graphs per device
+constexpr int kGraphsPerProcess = 512;     // and per process (they are released only at exit)
+std::atomic<int> g_graphs_alive{0};
 
 bool graphs_enabled() {
   static const bool on = [] {
@@ -715,7 +722,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
 
   // The frame's launch sequence on stream st: stage kernels, side-stream forks and joins. It
   // allocates nothing and reads no device state on the host, so it can be captured as a graph.
-  auto launch = [&](hipStream_t st) -> int {
+  auto launch = [&](hipStream_t st, hipEvent_t pfork, hipEvent_t pjoin, const SideStream& echo) -> int {
   // an error return after the fork drains the side stream first (the caller may free d_block)
   struct SideDrain {
     hipStream_t side = nullptr;
@@ -723,13 +730,13 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   } drain;
   if (overlap) {
     drain.side = dv.side;
-    HIP_TRY(c, hipEventRecord(dv.fork, st));
-    HIP_TRY(c, hipStreamWaitEvent(dv.side, dv.fork, 0));
+    HIP_TRY(c, hipEventRecord(pfork, st));
+    HIP_TRY(c, hipStreamWaitEvent(dv.side, pfork, 0));
     size_t ti = timing ? tstart(1, dv.side) : 0;
     launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, dv.side);
     if (timing) tstop(ti, dv.side);
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipEventRecord(dv.join, dv.side));
+    HIP_TRY(c, hipEventRecord(pjoin, dv.side));
   }
 
   if (f.stages & ART_STAGE_RAYTRACE) {
@@ -750,14 +757,14 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         FrameParams fpc = fpx;
         fpc.S = std::min(chunk, fan_count - b0);
         launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
-                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, dv.echo);
+                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, echo);
       }
     }
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
   }
   if (overlap) {
-    HIP_TRY(c, hipStreamWaitEvent(st, dv.join, 0));
+    HIP_TRY(c, hipStreamWaitEvent(st, pjoin, 0));
     drain.side = nullptr;  // joined: stream order covers it from here
   }
   if ((f.stages & ART_STAGE_PERMEATE) && !overlap) {
@@ -784,7 +791,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // caller's stream for every later frame with the same launch key (scene, frame parameters,
   // buffers, fan count, flags). One graph launch replaces ~10 launches and the host-side fork /
   // join gaps. Counting and timed frames, and ART_CTX_NO_GRAPH / ART_GRAPH=0, launch directly.
-  if (count || timing || (c->flags & ART_CTX_NO_GRAPH) || !graphs_enabled()) return launch(st);
+  if (count || timing || (c->flags & ART_CTX_NO_GRAPH) || !graphs_enabled()) return launch(st, dv.fork, dv.join, dv.echo);
   GraphKey key;
   memset(&key, 0, sizeof key);
   key.sc = dv.sc; key.fp = fp; key.L = f.L;
@@ -796,27 +803,28 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       HIP_TRY(c, hipGraphLaunch(gr.exec, st));
       return ART_OK;
     }
-  if (dv.graphs.size() >= kGraphCache) {  // evict the least recently used graph
-    size_t v = 0;
-    for (size_t i = 1; i < dv.graphs.size(); ++i)
-      if (dv.graphs[i].used < dv.graphs[v].used) v = i;
-    // it may still run: frames form one dependency chain (launch_common / wait_launch), so the last
-    // frame's event and the context stream cover every earlier launch
-    if (dv.launch_done) HIP_TRY(c, hipEventSynchronize(dv.launch_done));
-    HIP_TRY(c, hipStreamSynchronize(dv.stream));
-    (void)hipGraphExecDestroy(dv.graphs[v].exec);
-    dv.graphs.erase(dv.graphs.begin() + (long)v);
-  }
+  // Instantiated graphs are never destroyed while the process runs: on ROCm 7.2 a hipGraphLaunch
+  // of a newly instantiated graph crashed (host SIGSEGV inside libamdhip64) after an earlier graph
+  // sharing its kernels had been destroyed with hipGraphExecDestroy (tests/test_parity_gpu.py
+  // sequence). A full cache, or the process-wide cap, launches new keys directly.
+  if (dv.graphs.size() >= kGraphCache || g_graphs_alive.load() >= kGraphsPerProcess) return launch(st, dv.fork, dv.join, dv.echo);
   if (!dv.cap) HIP_TRY(c, hipStreamCreateWithFlags(&dv.cap, hipStreamNonBlocking));
+  // each graph records its own fork / join events (never shared between graphs or with direct launches)
+  Device::Graph gr;
+  for (hipEvent_t* e : {&gr.ev[0], &gr.ev[1], &gr.ev[2], &gr.ev[3]})
+    HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t e : gr.ev) dv.graph_events.push_back(e);
+  SideStream gecho = dv.echo;
+  gecho.fork = gr.ev[2];
+  gecho.join = gr.ev[3];
   HIP_TRY(c, hipStreamBeginCapture(dv.cap, hipStreamCaptureModeRelaxed));
-  const int rc = launch(dv.cap);
+  const int rc = launch(dv.cap, gr.ev[0], gr.ev[1], gecho);
   hipGraph_t g = nullptr;
   const hipError_t ee = hipStreamEndCapture(dv.cap, &g);
   if (rc || ee != hipSuccess || !g) {
     if (g) (void)hipGraphDestroy(g);
     return rc ? rc : fail(c, ART_E_DEVICE, "hipStreamEndCapture failed: %s", hipGetErrorString(ee));
   }
-  Device::Graph gr;
   gr.key = key;
   const hipError_t ei = hipGraphInstantiate(&gr.exec, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
@@ -824,6 +832,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   gr.used = ++dv.graph_clock;
   dv.graphs.push_back(gr);
   dv.graph_captures++;
+  g_graphs_alive.fetch_add(1);
   HIP_TRY(c, hipGraphLaunch(gr.exec, st));
   return ART_OK;
 }
@@ -897,7 +906,19 @@ ART_API int art_device_count(void) {
   return n;
 }
 
+// Diagnostics: ART_SEGV_TRACE=1 prints the native stack of a fatal signal (glibc backtrace).
+static void segv_trace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  fprintf(stderr, "libart: fatal signal %d, native stack:\n", sig);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 static int create_on(const int32_t* ids, int32_t count, art_ctx** out) {
+  if (const char* e = getenv("ART_SEGV_TRACE"))
+    if (e[0] == '1') { signal(SIGSEGV, segv_trace); signal(SIGABRT, segv_trace); }
   if (!out) return ART_E_INVALID;
   *out = nullptr;
   int n = 0;
@@ -953,7 +974,8 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     if (dv.launch_done) (void)hipEventSynchronize(dv.launch_done);  // a device frame on the caller's stream
-    for (Device::Graph& gr : dv.graphs) (void)hipGraphExecDestroy(gr.exec);
+    // the context's graphs and their events stay allocated until the process exits (see
+    // enqueue_kernels: destroying an instantiated graph broke later graph launches on ROCm 7.2)
     if (dv.cap) (void)hipStreamDestroy(dv.cap);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.exec.release(); dv.pairs.release(); dv.dsp.release(); dv.cones.release();
