@@ -50,7 +50,7 @@ ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
-ART_CTX_NO_GRAPH = 0x100
+ART_CTX_GRAPH = 0x100
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 # art_fan.ray_hit_ids: ColliderType (Enums/ColliderType.cs) << 30 | index in that type's array
@@ -120,7 +120,7 @@ class art_collider_sync_stats(C.Structure):
 
 class art_exec_counts(C.Structure):
     _fields_ = [("sphere", C.c_uint64), ("aabb", C.c_uint64), ("obb", C.c_uint64), ("cull_box", C.c_uint64),
-                ("cull_cone", C.c_uint64), ("launches", C.c_uint64)]
+                ("cell_entries", C.c_uint64), ("launches", C.c_uint64), ("muffle_fallback", C.c_uint64)]
 
 
 # include/art_dsp.h

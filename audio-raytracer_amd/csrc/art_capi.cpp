@@ -45,7 +45,7 @@ static_assert(sizeof(art_dsp_params) == 24, "art_dsp_params");
 
 namespace {
 
-constexpr uint32_t kAbiVersion = (2u << 16) | 0u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off
+constexpr uint32_t kAbiVersion = (2u << 16) | 1u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1: art_exec_counts.cell_entries / muffle_fallback, ART_CTX_GRAPH
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
@@ -98,7 +98,7 @@ struct Frame {
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
   size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
   // muffle candidate lists (art_cells.hip)
-  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_com = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, cells_temp = 0;
+  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, cells_temp = 0;
   uint32_t cells_cap = 0;
 };
 
@@ -460,7 +460,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_ccount = s; s = align_up(s + (cells + 1) * 4, 256);
     f.soa_cstart = s; s = align_up(s + (cells + 1) * 4, 256);
     f.soa_ccur = s; s = align_up(s + cells * 4, 256);
-    f.soa_com = s; s = align_up(s + (size_t)f.T * 4, 256);
+    f.soa_cfar = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_cok = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_ctemp = s; s = align_up(s + f.cells_temp, 256);
     f.soa_cent = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
@@ -575,7 +575,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.count = reinterpret_cast<uint32_t*>(soa + f.soa_ccount);
     cb.start = reinterpret_cast<uint32_t*>(soa + f.soa_cstart);
     cb.cursor = reinterpret_cast<uint32_t*>(soa + f.soa_ccur);
-    cb.om = reinterpret_cast<float*>(soa + f.soa_com);
+    cb.far = reinterpret_cast<float*>(soa + f.soa_cfar);
     cb.ok = reinterpret_cast<uint32_t*>(soa + f.soa_cok);
     cb.temp = soa + f.soa_ctemp; cb.temp_bytes = f.cells_temp;
     cb.ent = reinterpret_cast<uint2*>(soa + f.soa_cent);
@@ -641,10 +641,10 @@ constexpr size_t kGraphCache = 16;         // instantiated frame graphs per devi
 constexpr int kGraphsPerProcess = 512;     // and per process (they are released only at exit)
 std::atomic<int> g_graphs_alive{0};
 
-bool graphs_enabled() {
+bool graphs_forced() {
   static const bool on = [] {
     const char* e = getenv("ART_GRAPH");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -790,8 +790,8 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // side streams' event edges as graph edges, and the instantiated graph is launched on the
   // caller's stream for every later frame with the same launch key (scene, frame parameters,
   // buffers, fan count, flags). One graph launch replaces ~10 launches and the host-side fork /
-  // join gaps. Counting and timed frames, and ART_CTX_NO_GRAPH / ART_GRAPH=0, launch directly.
-  if (count || timing || (c->flags & ART_CTX_NO_GRAPH) || !graphs_enabled()) return launch(st, dv.fork, dv.join, dv.echo);
+  // join gaps. Opt-in (ART_CTX_GRAPH / ART_GRAPH=1); counting and timed frames launch directly.
+  if (count || timing || !((c->flags & ART_CTX_GRAPH) || graphs_forced())) return launch(st, dv.fork, dv.join, dv.echo);
   GraphKey key;
   memset(&key, 0, sizeof key);
   key.sc = dv.sc; key.fp = fp; key.L = f.L;
@@ -1287,10 +1287,11 @@ ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
     if (!dv.exec.p) continue;
     HIP_TRY(c, hipSetDevice(dv.id));
     HIP_TRY(c, hipDeviceSynchronize());
-    unsigned long long v[5] = {0, 0, 0, 0, 0};
+    unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
     HIP_TRY(c, hipMemcpy(v, dv.exec.p, sizeof v, hipMemcpyDeviceToHost));
     HIP_TRY(c, hipMemset(dv.exec.p, 0, 64));
-    out->sphere += v[0]; out->aabb += v[1]; out->obb += v[2]; out->cull_box += v[3]; out->cull_cone += v[4];
+    out->sphere += v[0]; out->aabb += v[1]; out->obb += v[2]; out->cull_box += v[3]; out->cell_entries += v[4];
+    out->muffle_fallback += v[5];
     out->launches += dv.exec_launches;
     dv.exec_launches = 0;
   }

@@ -10,16 +10,17 @@
 // sweeping collider chunks.
 //
 // Exactness. A collider whose float test blocks the segment contains, in its
-// widened box (margin factor * (scale + om), the broad-phase margins of §5 item 8, with om >= |off|_1
-// + maxd), the exact point at the reported parameter of the float ray (off, normalize(t - off)).
-// That ray deviates from the exact segment [off, target] by at most eta = 2e-6 om, so the
+// widened bounding sphere (margin factor * (far_t + |h| + 1), the broad-phase factors of §5 item 8
+// applied to the rounding scale |off - c| <= maxd + |h| <= far_t + |h|), the exact point at the
+// reported parameter of the float ray (off, normalize(t - off)). That ray deviates from the exact
+// segment [off, target] by at most eta = 2e-6 far_t, so the
 // collider's widened bounding sphere (+ 2 eta) meets the exact ray from the target towards `off`:
 // either it contains the target (entered in every cell) or the direction from the target to
 // `off` lies within the angular radius asin(rho / D) of the sphere, and that direction lies in
 // the segment's cell (up to the rounding of the cell lookup, covered by the cones' 1e-4 rad
 // slack). Entries also carry D - rho, a lower bound of the target distance of any blocking point;
-// muffle_kernel skips entries beyond maxd. A segment whose om exceeds the bound the lists were
-// built for, a degenerate segment, or a target whose lists overflowed tests every collider.
+// muffle_kernel skips entries beyond maxd. A segment longer than far_t (the bound the lists were
+// built for), a degenerate segment, or a target whose lists overflowed tests every collider.
 #include <algorithm>
 
 #include <hipcub/hipcub.hpp>
@@ -30,23 +31,22 @@ namespace art {
 
 constexpr float kCellEta = 2e-6f;  // relative deviation of a float muffle ray from its exact segment
 
-// |x|_1 bound of the scene and the largest target distance: the margin term om of target t.
-__device__ __forceinline__ float cells_om_of(const CullRec& root, vec3 tg) {
-  const float b1 = fmaxf(fabsf(root.lox), fabsf(root.hix)) + fmaxf(fabsf(root.loy), fabsf(root.hiy)) +
-                   fmaxf(fabsf(root.loz), fabsf(root.hiz));
+// far_t: the largest distance from target t to the scene's bounds (every muffle segment of t
+// starts on a collider, so maxd <= far_t; muffle_kernel tests a longer segment against every
+// collider).
+__device__ __forceinline__ float cells_far_of(const CullRec& root, vec3 tg) {
   const float dx = fmaxf(fabsf(root.lox - tg.x), fabsf(root.hix - tg.x));
   const float dy = fmaxf(fabsf(root.loy - tg.y), fabsf(root.hiy - tg.y));
   const float dz = fmaxf(fabsf(root.loz - tg.z), fabsf(root.hiz - tg.z));
-  const float far = sqrtf(dx * dx + dy * dy + dz * dz);
-  return (b1 + far) * 1.01f + 1.0f;
+  return sqrtf(dx * dx + dy * dy + dz * dz) * 1.001f + 1e-3f;
 }
 
-__global__ void cells_prep_kernel(DevScene sc, int T, float* __restrict__ om, uint32_t* __restrict__ ok) {
+__global__ void cells_prep_kernel(DevScene sc, int T, float* __restrict__ far, uint32_t* __restrict__ ok) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
   float v = INFINITY;
-  if (sc.bvh_levels > 0) v = cells_om_of(sc.bvh[0], load3(sc.targets, t));
-  om[t] = v;
+  if (sc.bvh_levels > 0) v = cells_far_of(sc.bvh[0], load3(sc.targets, t));
+  far[t] = v;
   ok[t] = isfinite(v) ? 1u : 0u;  // non-finite colliders: every muffle ray tests every collider
 }
 
@@ -90,13 +90,40 @@ __global__ __launch_bounds__(256) void cells_collider_kernel(DevScene sc, CellBu
   int tid;
   collider_code(sc, g, code, tid);
   if (tid == t) return;  // owned by the target: its muffle rays skip it (:413, :426, :439)
-  const float om = cb.om[t];
+  // The collider's bounding sphere and its error margin. Every test's rounding is relative to the
+  // segment-start-to-collider vector (the operands o and the record are exact floats): a reported
+  // blocking point lies within factor * (|o - c| + |h|_1) of the shape,
+  // and |o - c| <= maxd + rho <= far_t + rho for a collider the segment meets.
+  const float far = cb.far[t];
   const vec3 tg = load3(sc.targets, t);
   const CullRec cr = sc.cull[g];
-  const float m = cr.factor * (cr.scale + om);
-  const float rho = 0.5f * ((cr.hix - cr.lox) + (cr.hiy - cr.loy) + (cr.hiz - cr.loz)) * 1.001f + 1.75f * m +
-                    2.0f * (kCellEta * om + 1e-6f);
-  const vec3 w = mk3(0.5f * (cr.lox + cr.hix) - tg.x, 0.5f * (cr.loy + cr.hiy) - tg.y, 0.5f * (cr.loz + cr.hiz) - tg.z);
+  vec3 cc0;
+  float r, h1, widen;
+  const uint32_t ty = code >> 28, ix = code & 0x0fffffffu;
+  if (ty == 0) {
+    const SphereRec q = sc.sph[ix];
+    cc0 = mk3(q.cx, q.cy, q.cz);
+    r = sqrtf(q.r2) * 1.000001f;
+    h1 = 3.0f * r;
+    widen = 1.0f;
+  } else {
+    vec3 hh;
+    if (ty == 1) {
+      const AabbRec q = sc.aabb[ix];
+      cc0 = mk3(0.5f * (q.mnx + q.mxx), 0.5f * (q.mny + q.mxy), 0.5f * (q.mnz + q.mxz));
+      hh = mk3(0.5f * fabsf(q.mxx - q.mnx), 0.5f * fabsf(q.mxy - q.mny), 0.5f * fabsf(q.mxz - q.mnz));
+    } else {
+      const ObbRec q = sc.obb[ix];
+      cc0 = mk3(q.cx, q.cy, q.cz);
+      hh = mk3(0.5f * fabsf(q.lmxx - q.lmnx), 0.5f * fabsf(q.lmxy - q.lmny), 0.5f * fabsf(q.lmxz - q.lmnz));
+    }
+    r = sqrtf(hh.x * hh.x + hh.y * hh.y + hh.z * hh.z) * 1.00001f;
+    h1 = hh.x + hh.y + hh.z;
+    widen = 1.7321f;  // a box widened by m per axis: its half-diagonal grows by sqrt(3) m
+  }
+  const float m = cr.factor * (far + r + h1 + 1.0f);
+  const float rho = r + widen * m + 2.0f * (kCellEta * far + 1e-6f) + 1e-6f * (fabsf(cc0.x) + fabsf(cc0.y) + fabsf(cc0.z));
+  const vec3 w = mk3(cc0.x - tg.x, cc0.y - tg.y, cc0.z - tg.z);
   const float D = sqrtf(w.x * w.x + w.y * w.y + w.z * w.z);
   const bool all = !(D > rho * 1.0001f) || !isfinite(D) || !isfinite(rho);  // the sphere holds the target
   const float sb = all ? 1.0f : rho / D;
@@ -144,17 +171,17 @@ size_t cells_scan_temp_bytes(int T) {
   return bytes;
 }
 
-// Entry capacity: 64 cells per (target, collider) on average (a collider near its target spans
+// Entry capacity: 128 cells per (target, collider) on average (a collider near its target spans
 // hundreds, a far one a few); a target whose lists do not fit falls back to testing every collider.
 size_t cells_entry_cap(int T, int C) {
-  const size_t want = (size_t)64 * (size_t)T * (size_t)(C > 0 ? C : 1);
+  const size_t want = (size_t)128 * (size_t)T * (size_t)(C > 0 ? C : 1);
   return std::min<size_t>(std::max<size_t>(want, (size_t)1 << 16), (size_t)1 << 26);
 }
 
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   const int T = sc.T, n = sc.ns + sc.na + sc.no;
   const int cells = T * kCells;
-  hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.om, cb.ok);
+  hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.far, cb.ok);
   if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
   const long long work = (long long)n * T;
   const unsigned blocks = (unsigned)((work + 255) / 256);
@@ -166,7 +193,7 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   if (work > 0) hipLaunchKernelGGL(cells_collider_kernel<true>, dim3(blocks), dim3(256), 0, st, sc, cb, T);
   sc.cell_start = cb.start;
   sc.cell_ent = cb.ent;
-  sc.cell_om = cb.om;
+  sc.cell_far = cb.far;
   sc.cell_ok = cb.ok;
   sc.cell_cap = cb.cap;
   return 0;

@@ -95,7 +95,7 @@ struct DevScene {
   // overflowed (cell_ok[t] == 0) is tested against every collider instead.
   const uint32_t* cell_start;     // [T * kCells + 1]
   const uint2* cell_ent;          // [cell_cap]: (code, near bits)
-  const float* cell_om;           // [T]: the margin term the lists were built for
+  const float* cell_far;          // [T]: the segment length the lists were built for
   const uint32_t* cell_ok;        // [T]
   uint32_t cell_cap;
 };
@@ -145,7 +145,7 @@ struct CellBufs {
   uint32_t* start;                // [T * kCells + 1] exclusive scan of count (DevScene::cell_start)
   uint32_t* cursor;               // [T * kCells] fill positions
   uint2* ent;                     // [cap]
-  float* om;                      // [T]
+  float* far;                     // [T]: distance bound of t's segments
   uint32_t* ok;                   // [T]
   uint32_t cap;
   void* temp; size_t temp_bytes;  // hipcub scan storage
@@ -176,7 +176,7 @@ struct FrameParams {
 };
 
 // Slots of FrameParams::exec (art_exec_counts order).
-enum ExecSlot { kExecSphere = 0, kExecAabb = 1, kExecObb = 2, kExecCullBox = 3, kExecCullCone = 4 };
+enum ExecSlot { kExecSphere = 0, kExecAabb = 1, kExecObb = 2, kExecCullBox = 3, kExecCellEntries = 4, kExecMuffleFallback = 5 };
 
 // Device counters for the counting variant, in art_test_counts order.
 struct DevCounts { unsigned long long v[9]; };

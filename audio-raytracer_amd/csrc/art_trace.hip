@@ -761,8 +761,7 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
   const float4 r = vp.hrec[valid ? i : 0u];
   const vec3 off = mk3(r.x, r.y, r.z);
   const uint32_t dbase = __float_as_uint(r.w);
-  const float o1 = fabsf(off.x) + fabsf(off.y) + fabsf(off.z);
-  unsigned nt[3] = {0u, 0u, 0u};
+  unsigned nt[3] = {0u, 0u, 0u}, ne = 0u, nfb = 0u;  // tests, list entries scanned, fallback rays
   for (int t = 0; t < fp.T; ++t) {  // wave-uniform
     const vec3 tp = load3(sc.targets, t);
     const float maxd = distance(off, tp);                             // :165
@@ -771,18 +770,20 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
     if (act) {
       const Seg s = make_seg(off, normalize(tp - off));               // :158-160
       const vec3 v = off - tp;                                        // the ray seen from the target
-      const bool lists = sc.cell_ok[t] != 0u && o1 + maxd <= sc.cell_om[t] && (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f) &&
+      const bool lists = sc.cell_ok[t] != 0u && maxd <= sc.cell_far[t] && (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f) &&
                          isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
       if (lists) {
         const uint32_t* st = sc.cell_start + (size_t)t * kCells + cube_cell(v);
         const uint32_t b = st[0], e = st[1];
         const float lim = maxd * 1.00001f + 1e-6f;
+        if (EX) ne += e - b;
         for (uint32_t k = b; k < e; ++k) {
           const uint2 en = sc.cell_ent[k];
           if (__uint_as_float(en.y) > lim) continue;  // the collider lies beyond the segment
           if (muffle_test<OBB>(sc, s, en.x, maxd, nt)) { blocked = true; break; }
         }
       } else {
+        if (EX) ++nfb;
         blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
       }
     }
@@ -800,6 +801,8 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
     exec_add(fp.exec, kExecSphere, wave_sum_u32(nt[0]));
     exec_add(fp.exec, kExecAabb, wave_sum_u32(nt[1]));
     exec_add(fp.exec, kExecObb, wave_sum_u32(nt[2]));
+    exec_add(fp.exec, kExecCellEntries, wave_sum_u32(ne));
+    exec_add(fp.exec, kExecMuffleFallback, wave_sum_u32(nfb));
   }
 }
 

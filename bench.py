@@ -33,10 +33,9 @@ import torch  # noqa: E402
 import art  # noqa: E402
 from art import abi  # noqa: E402
 
-# Broad-phase bound tests, same counting rule: segment box vs collider bounds (margin 2, 6 widened
-# bounds, 6 compares) and shared-origin cone vs bounding sphere (centre 6, radius 8, distance 9,
-# angle terms 10, compare 2).
-CULL_OPS = {"cull_box": 14, "cull_cone": 35}
+# Broad-phase work, same counting rule: BVH node box vs segment (margin 2, 6 widened bounds, 6
+# compares) and muffle cell-list entries scanned (a load and a distance compare: 2).
+CULL_OPS = {"cull_box": 14, "cell_entries": 2}
 # Algorithmic FP32 ops per test (SURVEY.md §8 d; miss path, IEEE add/sub/mul/div/sqrt/min/max/cmp = 1).
 OPS = {"rt_sphere": 26, "rt_aabb": 34, "rt_obb": 118, "perm_hit_sphere": 26, "perm_hit_aabb": 34, "perm_hit_obb": 134,
        "perm_loss_sphere": 18, "perm_loss_aabb": 33, "perm_loss_obb": 117}
@@ -657,7 +656,7 @@ def main():
     bf_tflops = bf_ops / (rt_ms * 1e-3) / 1e12
     ex_launches = max(1, executed["launches"])
     ex_ops = (executed["sphere"] * OPS["rt_sphere"] + executed["aabb"] * OPS["rt_aabb"] + executed["obb"] * OPS["rt_obb"] +
-              executed["cull_box"] * CULL_OPS["cull_box"] + executed["cull_cone"] * CULL_OPS["cull_cone"]) / ex_launches
+              executed["cull_box"] * CULL_OPS["cull_box"] + executed["cell_entries"] * CULL_OPS["cell_entries"]) / ex_launches
     ex_tests = (executed["sphere"] + executed["aabb"] + executed["obb"]) / ex_launches
     ex_tflops = ex_ops / (rt_ms * 1e-3) / 1e12
     # algorithmic HBM bytes of one raytrace launch: the decoded collider records, directions,

@@ -47,10 +47,11 @@ typedef struct {
 /* (0x8, 0x40 and 0x80 selected round-1 alternative raytrace implementations; they are gone and
  * the bits are reserved.) */
 
-/* Launch every frame's kernels directly instead of replaying the captured frame graph (a frame's
- * launch sequence is captured as a hipGraph on first use and replayed while the scene, buffers,
- * fan count and flags stay the same; ART_GRAPH=0 in the environment also disables it). */
-#define ART_CTX_NO_GRAPH 0x100u
+/* Replay each frame's launch sequence as a captured hipGraph (captured on first use, replayed while
+ * the scene, buffers, fan count and flags stay the same; ART_GRAPH=1 in the environment turns it on
+ * for every context). Off by default: on ROCm 7.2 the replay measured slower than direct launches
+ * and graph lifetimes interact badly with hipGraphExecDestroy. */
+#define ART_CTX_GRAPH 0x100u
 
 ART_API int art_fan_layout_get(const art_frame_desc* desc, uint32_t out_flags, art_fan_layout* out);
 
@@ -87,8 +88,10 @@ ART_API int art_count_device(art_ctx* ctx, const float* d_origins, int32_t fan_c
 #define ART_CTX_COUNT_EXECUTED 0x10u
 typedef struct {
     uint64_t sphere, aabb, obb;      /* exact lane-tests executed */
-    uint64_t cull_box, cull_cone;    /* broad-phase lane-evaluations (segment box / shared-origin cone) */
+    uint64_t cull_box;               /* BVH node box tests (lane-evaluations) */
+    uint64_t cell_entries;           /* muffle candidate-list entries scanned (lane-evaluations) */
     uint64_t launches;               /* frames counted */
+    uint64_t muffle_fallback;        /* muffle rays tested against every collider (no usable cell list) */
 } art_exec_counts;
 /* Executed-work counters since the last call (needs ART_CTX_COUNT_EXECUTED); synchronizes. */
 ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);

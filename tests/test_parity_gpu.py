@@ -396,9 +396,9 @@ def test_launch_device_then_schedule_and_bind_without_sync(ctx):
 
 
 def test_graph_replay_equals_direct_launches(ctx):
-    """Device frames replay a captured hipGraph of the frame's launch sequence while the launch key
-    (scene, parameters, buffers, fan count, flags) is unchanged. Replayed frames, re-captured frames
-    after a rebind with other parameters, and direct launches (ART_CTX_NO_GRAPH) must all equal the
+    """With ART_CTX_GRAPH, device frames replay a captured hipGraph of the frame's launch sequence while
+    the launch key (scene, parameters, buffers, fan count, flags) is unchanged. Replayed frames,
+    re-captured frames after a rebind with other parameters, and direct launches must all equal the
     oracle byte for byte; multi-bounce (per-bounce echo forks) and permeation (side stream) included."""
     torch = pytest.importorskip("torch")
     cfg = art.CONFIGS[5]
@@ -412,7 +412,7 @@ def test_graph_replay_equals_direct_launches(ctx):
         oracle.run_frame(art.Frame(scene, params, org, ref), threads=16)
         lay = art.fan_layout(fr, abi.ART_OUT_HIT_RESULTS)
         ctx.bind(fr)
-        for flags in (0, 0, abi.ART_CTX_NO_GRAPH, 0):
+        for flags in (abi.ART_CTX_GRAPH, abi.ART_CTX_GRAPH, 0, abi.ART_CTX_GRAPH):
             ctx.set_flags(flags)
             d_blk = torch.zeros(12 * lay["stride"], dtype=torch.uint8, device="cuda")
             for _ in range(3):  # replays write the same block
