@@ -98,7 +98,8 @@ struct Frame {
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
   size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
   // muffle candidate lists (art_cells.hip)
-  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, cells_temp = 0;
+  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, cells_temp = 0,
+         soa_cgeo = 0;
   uint32_t cells_cap = 0;
 };
 
@@ -464,6 +465,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_cok = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_ctemp = s; s = align_up(s + f.cells_temp, 256);
     f.soa_cent = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
+    f.soa_cgeo = s; s = align_up(s + cells_geo_bytes(f.T, f.ns + f.na + f.no), 256);
   }
   f.soa_bytes = s;
 }
@@ -580,6 +582,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.temp = soa + f.soa_ctemp; cb.temp_bytes = f.cells_temp;
     cb.ent = reinterpret_cast<uint2*>(soa + f.soa_cent);
     cb.cap = f.cells_cap;
+    cb.geo = soa + f.soa_cgeo;
     if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
     dv.sorted_sc = sc;
   }

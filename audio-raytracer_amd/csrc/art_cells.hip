@@ -77,19 +77,34 @@ __device__ __forceinline__ void face_range(float a_u, float a_n, float s, int& i
   if (!(lo <= 1.0f && hi >= -1.0f)) { i0 = 1; i1 = 0; }  // outside the face
 }
 
-// One thread per (target, collider): enumerate the cells whose cone meets the collider's widened
-// bounding sphere. FILL = false counts per cell; FILL = true writes the entries.
-template <bool FILL>
-__global__ __launch_bounds__(256) void cells_collider_kernel(DevScene sc, CellBufs cb, int T) {
+// Geometry of one (target, collider) pair for the enumeration: the unit direction to the widened
+// bounding sphere, sin / cos of its angular radius, the entry (code, near) and per face the cell
+// rectangle its cone can touch (i0, i1, j0, j1; empty when i0 > i1).
+struct alignas(16) CellGeo {
+  float ux, uy, uz, sb;
+  float cb, near;
+  uint32_t code, all;      // all: the sphere holds the target (every cell)
+  uint8_t rect[6][4];
+  uint32_t pad[2];
+};
+
+// One thread per (target, collider).
+__global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb, int T, CellGeo* __restrict__ geo) {
   const int n = sc.ns + sc.na + sc.no;
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (long long)n * T) return;
   const int t = (int)(k / n), g = (int)(k - (long long)t * n);
-  if (!cb.ok[t]) return;
+  CellGeo G;
+  for (int f = 0; f < 6; ++f) { G.rect[f][0] = 1; G.rect[f][1] = 0; G.rect[f][2] = 1; G.rect[f][3] = 0; }
+  G.pad[0] = G.pad[1] = 0u;
   uint32_t code;
   int tid;
   collider_code(sc, g, code, tid);
-  if (tid == t) return;  // owned by the target: its muffle rays skip it (:413, :426, :439)
+  G.code = code;
+  G.all = 0u;
+  G.ux = G.uy = G.uz = G.sb = G.cb = G.near = 0.0f;
+  // owned by the target (its muffle rays skip it, :413, :426, :439) or no lists: no cells
+  if (!cb.ok[t] || tid == t) { geo[k] = G; return; }
   // The collider's bounding sphere and its error margin. Every test's rounding is relative to the
   // segment-start-to-collider vector (the operands o and the record are exact floats): a reported
   // blocking point lies within factor * (|o - c| + |h|_1) of the shape,
@@ -133,9 +148,8 @@ __global__ __launch_bounds__(256) void cells_collider_kernel(DevScene sc, CellBu
   const float gamma = cb.alpha_max + asinf(fminf(sb, 1.0f)) + 1e-3f;
   const bool wide = all || gamma >= 1.5f;
   const float sg = sinf(fminf(gamma, 1.5707963f)), s2 = sg * sg;
-  uint32_t* cnt = cb.count + (size_t)t * kCells;
-  uint32_t* cur = cb.cursor + (size_t)t * kCells;
   const float uc[3] = {u.x, u.y, u.z};
+  G.ux = u.x; G.uy = u.y; G.uz = u.z; G.sb = sb; G.cb = cb_; G.near = near; G.all = all ? 1u : 0u;
   for (int f = 0; f < 6; ++f) {
     const int ax = f >> 1;
     const float sgn = (f & 1) ? -1.0f : 1.0f;
@@ -146,21 +160,38 @@ __global__ __launch_bounds__(256) void cells_collider_kernel(DevScene sc, CellBu
       face_range(a_u, a_n, s2, i0, i1);
       face_range(a_v, a_n, s2, j0, j1);
     }
-    for (int j = j0; j <= j1; ++j)
-      for (int i = i0; i <= i1; ++i) {
-        const int c = (f * kCellG + j) * kCellG + i;
-        const CellCone cc = cb.cones[c];
-        // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
-        const bool hit = all || (u.x * cc.ax + u.y * cc.ay + u.z * cc.az >= (cc.cos_a * cb_ - cc.sin_a * sb) - 1e-5f);
-        if (!hit) continue;
-        if (!FILL) {
-          atomicAdd(cnt + c, 1u);
-        } else {
-          const uint32_t pos = atomicAdd(cur + c, 1u);
-          if (pos < cb.cap) cb.ent[pos] = make_uint2(code, __float_as_uint(near));
-          else cb.ok[t] = 0u;  // overflow: this target's muffle rays test every collider
-        }
-      }
+    G.rect[f][0] = (uint8_t)i0; G.rect[f][1] = (uint8_t)i1; G.rect[f][2] = (uint8_t)j0; G.rect[f][3] = (uint8_t)j1;
+  }
+  geo[k] = G;
+}
+
+// One thread per (target, collider, face, cell row): tests the row's cells of the pair's face
+// rectangle. FILL = false counts per cell; FILL = true writes the entries.
+template <bool FILL>
+__global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restrict__ geo, long long pairs, CellBufs cb, int n) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long p = k / (6 * kCellG);
+  if (p >= pairs) return;
+  const int fr = (int)(k - p * (6 * kCellG)), f = fr / kCellG, j = fr - f * kCellG;
+  const CellGeo G = geo[p];
+  const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
+  if (j < j0 || j > j1 || i0 > i1) return;
+  const int t = (int)(p / n);
+  uint32_t* cnt = cb.count + (size_t)t * kCells;
+  uint32_t* cur = cb.cursor + (size_t)t * kCells;
+  for (int i = i0; i <= i1; ++i) {
+    const int c = (f * kCellG + j) * kCellG + i;
+    const CellCone cc = cb.cones[c];
+    // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
+    const bool hit = G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
+    if (!hit) continue;
+    if (!FILL) {
+      atomicAdd(cnt + c, 1u);
+    } else {
+      const uint32_t pos = atomicAdd(cur + c, 1u);
+      if (pos < cb.cap) cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
+      else cb.ok[t] = 0u;  // overflow: this target's muffle rays test every collider
+    }
   }
 }
 
@@ -183,14 +214,21 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   const int cells = T * kCells;
   hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.far, cb.ok);
   if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
-  const long long work = (long long)n * T;
-  const unsigned blocks = (unsigned)((work + 255) / 256);
-  if (work > 0) hipLaunchKernelGGL(cells_collider_kernel<false>, dim3(blocks), dim3(256), 0, st, sc, cb, T);
+  const long long pairs = (long long)n * T;
+  CellGeo* geo = reinterpret_cast<CellGeo*>(cb.geo);
+  if (pairs > 0) {
+    hipLaunchKernelGGL(cells_geo_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, st, sc, cb, T, geo);
+    const unsigned rb = (unsigned)((pairs * 6 * kCellG + 255) / 256);
+    hipLaunchKernelGGL(cells_row_kernel<false>, dim3(rb), dim3(256), 0, st, geo, pairs, cb, n);
+  }
   size_t bytes = cb.temp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(cb.temp, bytes, cb.count, cb.start, cells + 1, st) != hipSuccess) return -1;
   if (hipMemcpyAsync(cb.cursor, cb.start, (size_t)cells * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
     return -1;
-  if (work > 0) hipLaunchKernelGGL(cells_collider_kernel<true>, dim3(blocks), dim3(256), 0, st, sc, cb, T);
+  if (pairs > 0) {
+    const unsigned rb = (unsigned)((pairs * 6 * kCellG + 255) / 256);
+    hipLaunchKernelGGL(cells_row_kernel<true>, dim3(rb), dim3(256), 0, st, geo, pairs, cb, n);
+  }
   sc.cell_start = cb.start;
   sc.cell_ent = cb.ent;
   sc.cell_far = cb.far;
@@ -198,5 +236,7 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   sc.cell_cap = cb.cap;
   return 0;
 }
+
+size_t cells_geo_bytes(int T, int C) { return (size_t)T * (size_t)(C > 0 ? C : 1) * sizeof(CellGeo); }
 
 }  // namespace art

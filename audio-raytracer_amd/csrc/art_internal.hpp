@@ -149,8 +149,10 @@ struct CellBufs {
   uint32_t* ok;                   // [T]
   uint32_t cap;
   void* temp; size_t temp_bytes;  // hipcub scan storage
+  void* geo;                      // [T * C] per-(target, collider) geometry (cells_geo_bytes)
 };
 size_t cells_scan_temp_bytes(int T);
+size_t cells_geo_bytes(int T, int C);
 size_t cells_entry_cap(int T, int C);
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st);
 

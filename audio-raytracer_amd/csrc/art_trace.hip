@@ -694,8 +694,9 @@ void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, un
 }
 
 // ------------------------------------------------------------------------------------------
-// Muffle rays (:150-173, CanRaySeeAudioTarget :405-449). One lane per hit record; for each target
-// t (wave-uniform) the lane's ray from `off` to the target (distance < MaxMuffleHitDistance,
+// Muffle rays (:150-173, CanRaySeeAudioTarget :405-449). One lane per hit record and target (grid
+// y = target; more waves in flight for the latency-bound list walks): the lane's ray from `off` to
+// the target (distance < MaxMuffleHitDistance,
 // :165-168) is tested against the colliders of its direction cell around the target
 // (art_cells.hip: not owned by t, widened bounding sphere on the ray) and stops at its first
 // blocker; the wave counts its visible rays into the muffle accumulators with one atomic per
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
   const vec3 off = mk3(r.x, r.y, r.z);
   const uint32_t dbase = __float_as_uint(r.w);
   unsigned nt[3] = {0u, 0u, 0u}, ne = 0u, nfb = 0u;  // tests, list entries scanned, fallback rays
-  for (int t = 0; t < fp.T; ++t) {  // wave-uniform
+  for (int t = blockIdx.y; t < fp.T; t += gridDim.y) {  // workgroup-uniform
     const vec3 tp = load3(sc.targets, t);
     const float maxd = distance(off, tp);                             // :165
     const bool act = valid && maxd < fp.max_muffle;                   // :168
@@ -914,8 +915,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     }
   }
   const unsigned mblocks = (unsigned)((hcap + 255) / 256);  // hit records: at most one per ray and bounce
+  const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
 #define ART_MUFFLE(EX_, OBB_) \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_>), dim3(mblocks), dim3(256), 0, st, sc, fp, pb.vp, pair_count, muffle_acc)
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_>), dim3(mblocks, mt), dim3(256), 0, st, sc, fp, pb.vp, pair_count, muffle_acc)
   if (fp.exec) { if (obb) ART_MUFFLE(true, true); else ART_MUFFLE(true, false); }
   else { if (obb) ART_MUFFLE(false, true); else ART_MUFFLE(false, false); }
 #undef ART_MUFFLE
