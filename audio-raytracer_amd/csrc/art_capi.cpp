@@ -1290,11 +1290,11 @@ ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
     if (!dv.exec.p) continue;
     HIP_TRY(c, hipSetDevice(dv.id));
     HIP_TRY(c, hipDeviceSynchronize());
-    unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(c, hipMemcpy(v, dv.exec.p, sizeof v, hipMemcpyDeviceToHost));
     HIP_TRY(c, hipMemset(dv.exec.p, 0, 64));
     out->sphere += v[0]; out->aabb += v[1]; out->obb += v[2]; out->cull_box += v[3]; out->cell_entries += v[4];
-    out->muffle_fallback += v[5];
+    out->muffle_fallback += v[5]; out->echo_pairs += v[6];
     out->launches += dv.exec_launches;
     dv.exec_launches = 0;
   }

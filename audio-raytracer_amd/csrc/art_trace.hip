@@ -499,6 +499,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
     const float dist0 = distance(O, o);            // :130 (un-offset hit point)
     {
       const unsigned long long me = __ballot(live_slot), mr = __ballot(hit);
+      exec_add(fp.exec, kExecEchoPairs, (unsigned long long)__popcll(me));
       uint32_t eb, rb;
       reserve((uint32_t)__popcll(me), (uint32_t)__popcll(mr), pair_count, eb, rb);
       if (live_slot) {

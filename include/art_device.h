@@ -92,6 +92,7 @@ typedef struct {
     uint64_t cell_entries;           /* muffle candidate-list entries scanned (lane-evaluations) */
     uint64_t launches;               /* frames counted */
     uint64_t muffle_fallback;        /* muffle rays tested against every collider (no usable cell list) */
+    uint64_t echo_pairs;             /* echo rays left to the BVH echo traversal (not decided by the nearest pass) */
 } art_exec_counts;
 /* Executed-work counters since the last call (needs ART_CTX_COUNT_EXECUTED); synchronizes. */
 ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);

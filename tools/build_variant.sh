@@ -9,13 +9,13 @@ pkg=$root/audio-raytracer_amd
 tmp=$(mktemp -d)
 mkdir -p "$root/variants"
 flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden "$@")
-for f in art_kernels art_trace art_bvh art_dsp; do
+for f in art_kernels art_trace art_bvh art_cells art_dsp; do
   hipcc "${flags[@]}" -c "$pkg/csrc/$f.hip" -o "$tmp/$f.o" &
 done
 hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_capi.cpp" -o "$tmp/art_capi.o" &
 hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_synth.cpp" -o "$tmp/art_synth.o" &
 hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_cpu.cpp" -o "$tmp/art_cpu.o" &
 wait
-hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/variants/libart_$name.so" "$tmp"/*.o
+hipcc --offload-arch=gfx950 -shared -fPIC -rdynamic -o "$root/variants/libart_$name.so" "$tmp"/*.o
 rm -rf "$tmp"
 echo "variants/libart_$name.so"
