@@ -195,29 +195,70 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
   return obb_test<false>(s, r, stored_q(r), dist);
 }
 
+// Work sharing inside a wave (nearest and echo traversals): a wave lasts as long as its longest
+// traversal, so a quad whose traversal has ended takes over the bottom entry of a busy quad's
+// stack (the largest pending subtree) together with that quad's ray, and traverses it for the
+// ray's home quad. (ART_*_STEAL=0 builds the plain traversals, for A/B runs.)
+#ifndef ART_VIS_STEAL
+#define ART_VIS_STEAL 1
+#endif
+#ifndef ART_NEAREST_STEAL
+#define ART_NEAREST_STEAL 1
+#endif
+constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
+// k-th (0-based) set bit of m, k < popcount(m).
+__device__ __forceinline__ int select_bit(unsigned long long m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll((m >> pos) & ((1ull << w) - 1ull));
+    if (k >= c) { k -= c; pos += w; }
+  }
+  return pos;
+}
+
+// (distance, order) as one ordered 64-bit key; distances are >= 0 or -0, the two zeros equal
+__device__ __forceinline__ unsigned long long nearest_key(float d, int code) {
+  return ((unsigned long long)(d == 0.0f ? 0u : __float_as_uint(d)) << 32) | (uint32_t)code;
+}
+
 // Nearest hit of the quad's ray s (identical in the 4 lanes; `my` = the ray's kBvhStack-entry
-// stack): (distance, order) minimum in best / code of every lane of the quad.
+// stack inside the wave's 16 stacks; s_bound / s_key = the wave's 16 shared pruning bounds and
+// result keys): (distance, order) minimum in best / code of every lane of the quad.
+// With work sharing, the quads that traverse parts of one ray's tree prune against the smallest
+// distance any of them found (s_bound, published once the wave has shared work), and the ray's
+// result is the (distance, order) minimum of their results (a 64-bit LDS minimum of (distance
+// bits, order); the two zeros compare equal, as in the reference's `<`, and the path kernel
+// re-evaluates a zero distance).
 template <bool EX, bool OBB>
-__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg& s, bool alive, int lane, uint32_t* my,
-                                                  float& best, int& code, unsigned long long* ex) {
-  const int qd = lane & 3;
+__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint32_t* my,
+                                                  int* s_bound, unsigned long long* s_key, float& best, int& code,
+                                                  unsigned long long* ex) {
+  const int qd = lane & 3, wq = lane >> 2;
+  uint32_t* const s_wave = my - wq * kBvhStack;
   best = FLT_MAX;
   code = kNoHit;
   if (sc.bvh_levels == 0) return;  // no colliders: every ray misses
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
-  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
-  const bool force = force_all(s, om);
+  float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
+  bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
-  int g = alive ? 0 : -1, sp = 0;
-  // branch-free pop: the stack slot is read unconditionally (clamped), the select picks -1 when empty
+  int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
+  float lim = FLT_MAX;   // pruning bound: best, and (shared work) the other quads' results for the ray
+  bool shared = false;   // wave-uniform: work was shared in this wave
+  float mybest = FLT_MAX;  // this quad's own (distance, order) minimum over the leaves it tested
+  int mycode = kNoHit;
+  // branch-free pop of entries [bp, sp): the slot is read unconditionally (clamped), -1 when empty
   auto pop = [&]() {
-    const int t = (int)my[sp > 0 ? sp - 1 : 0];
-    g = sp > 0 ? t : -1;
-    sp = sp > 0 ? sp - 1 : 0;
+    const bool has = sp > bp;
+    const int t = (int)my[has ? sp - 1 : 0];
+    g = has ? t : -1;
+    sp = has ? sp - 1 : sp;
+    if (sp == bp) sp = bp = 0;
   };
-  // A child is entered when its widened box is entered at or before the best distance (a winner or
-  // tie lies strictly after every ancestor's entry); quad_descend orders the entered ones.
+  // A child is entered when its widened box is entered at or before the bound (a winner or tie
+  // lies strictly after every ancestor's entry); quad_descend orders the entered ones.
   auto inner_step = [&]() {
     const int c0 = 4 * g + 1;
     if (EX && qd == 0) ++nnode;
@@ -225,8 +266,9 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
     float tn;
     const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
-    const bool enter = (r.lox <= r.hix) & (force | (h & (en <= best)));  // bitwise: no branch
+    const bool enter = (r.lox <= r.hix) & (force | (h & (en <= lim)));  // bitwise: no branch
     quad_descend(enter, en, force, qd, c0, my, g, sp);
+    if (sp == bp) sp = bp = 0;
   };
   auto leaf_step = [&](int leaf) {
     int cc, tid;
@@ -237,20 +279,58 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
     int dc = kNoHit;
     if (h && dd < FLT_MAX) { d = dd; dc = cc; }
     quad_min(d, dc);
-    if (d < best || (d == best && dc < code)) { best = d; code = dc; }
+    if (d < mybest || (d == mybest && dc < mycode)) {
+      mybest = d;
+      mycode = dc;
+      lim = fminf(lim, d);
+      if (ART_NEAREST_STEAL && shared && qd == 0) atomicMin(s_bound + home, __float_as_int(d));
+    }
   };
   // Speculative while-while (Aila & Laine): a quad that reaches a leaf parks it and keeps
   // descending; the wave tests leaves once every quad with work holds one, so both kinds of step
   // run with most quads busy. The order in which leaves are tested does not change the minimum.
   int pend = -1;
-  while (__any(g >= 0 || pend >= 0)) {
+  for (;;) {
+    const unsigned long long act = __ballot(g >= 0 || pend >= 0) & kQuad0;
+    if (!act) break;
     {  // Wave priority by unfinished rays: the waves with the most rays left (the ones that set the
        // kernel's length) issue first, the nearly finished ones fill the gaps (s_setprio, 0..3)
-      const int act = __popcll(__ballot((g >= 0 || pend >= 0) && qd == 0));
-      if (act > 12) __builtin_amdgcn_s_setprio(3);
-      else if (act > 8) __builtin_amdgcn_s_setprio(2);
-      else if (act > 4) __builtin_amdgcn_s_setprio(1);
+      const int na = __popcll(act);
+      if (na > 12) __builtin_amdgcn_s_setprio(3);
+      else if (na > 8) __builtin_amdgcn_s_setprio(2);
+      else if (na > 4) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
+    }
+    if (ART_NEAREST_STEAL) {
+      const unsigned long long donors = __ballot(sp > bp) & kQuad0, idle = ~act & kQuad0;
+      if (donors && idle) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
+        if (!shared) {       // publish every ray's bound once, open its result key
+          shared = true;
+          if (qd == 0) { s_bound[wq] = __float_as_int(lim); s_key[wq] = ~0ull; }
+        }
+        const unsigned long long below = (1ull << (lane & ~3)) - 1ull;
+        const int ir = __popcll(idle & below), dr = __popcll(donors & below);
+        const bool thief = (act >> (lane & ~3) & 1ull) == 0ull && ir < __popcll(donors);
+        const bool robbed = sp > bp && dr < __popcll(idle);
+        const int src = (thief ? select_bit(donors, ir) : (lane & ~3)) + qd;
+        const int dbp = __shfl(bp, src), dhome = __shfl(home, src);
+        const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
+        const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
+        const float dlim = __shfl(lim, src);
+        if (thief && mycode != kNoHit && qd == 0) atomicMin(s_key + home, nearest_key(mybest, mycode));
+        if (thief) {  // the ray's derived values are recomputed as the home computed them
+          g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
+          sp = bp = 0;
+          home = dhome;
+          s = make_seg(mk3(ox, oy, oz), mk3(dx, dy, dz));
+          om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
+          force = force_all(s, om);
+          lim = dlim;
+          mybest = FLT_MAX; mycode = kNoHit;  // (the finished ray's result went to its key above)
+        }
+        if (robbed && ++bp == sp) sp = bp = 0;
+      }
+      if (shared) lim = fminf(lim, __int_as_float(s_bound[home]));
     }
     for (;;) {
       if (g >= leaf0 && pend < 0) { pend = g; pop(); }
@@ -259,6 +339,14 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, const Seg&
       if (inner) inner_step();
     }
     if (pend >= 0) { leaf_step(pend); pend = -1; }
+  }
+  best = mybest;
+  code = mycode;
+  if (ART_NEAREST_STEAL && shared) {  // the ray's result: the minimum over the quads that traversed it
+    if (mycode != kNoHit && qd == 0) atomicMin(s_key + home, nearest_key(mybest, mycode));
+    const unsigned long long k = s_key[wq];
+    best = k == ~0ull ? FLT_MAX : __uint_as_float((uint32_t)(k >> 32));
+    code = k == ~0ull ? kNoHit : (int)(uint32_t)k;
   }
   if (ex) {
     exec_add(ex, kExecSphere, wave_sum_u32(nt[0]));
@@ -294,6 +382,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
     uint32_t* __restrict__ counters) {
   __shared__ uint32_t s_stk[kBvhStack * 64];
+  __shared__ int s_bound[64];
+  __shared__ unsigned long long s_key[64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
   const int ngroups = fp.S * nrb;
@@ -335,7 +425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
     write = true;
     out = (uint32_t)g * 64u + (uint32_t)rr;
   }
-  quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, best, code, ex);
+  quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code, ex);
   if ((lane & 3) == 0 && write) hits[out] = make_int2(__float_as_int(best), code);
 }
 
@@ -477,6 +567,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       // exact (Unity min/max) re-evaluation of a zero distance: IEEE and Unity min/max differ only
       // in the sign of an equal-magnitude zero pair, so only a zero result can differ (its sign)
       if (dist == 0.0f) {
+        if (type == kSphere) sphere_hit_dist(s, sc.sph[idx], dist);  // (a -0 the result key made +0)
         if (type == kAabb) aabb_test<true>(s, sc.aabb[idx], dist);
         if (type == kObb) { const ObbRec r = sc.obb[idx]; obb_test<true>(s, r, stored_q(r), dist); }
       }
@@ -604,13 +695,19 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
 // before maxd (a blocker's computed distance d < maxd lies strictly after every ancestor's
 // entry), 4 lanes per segment (lane q: child q / leaf slot q; the quad agrees through ballots),
 // the first blocker ends the segment; a segment no collider blocks stores its echo.
+// Work sharing inside the wave: a wave lasts as long as its longest traversal, so a quad whose
+// traversal has ended takes over the bottom entry of a busy quad's stack (the largest pending
+// subtree) together with that quad's segment, and traverses it for the segment's home quad. The
+// subtrees of a segment are then split between quads; any of them finding a blocker marks the home
+// blocked (wave-uniform mask), which ends every traversal of that segment. Any-hit is an OR over
+// the subtrees, so the split does not change a verdict.
 // ------------------------------------------------------------------------------------------
 template <bool OBB>
 __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
                                               unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
                                               const uint32_t* ecnt, int bounce, uint8_t* block) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
-  const int slot = w * 16 + (lane >> 2);                       // segment of the block's 64-pair batch
+  const int wq = lane >> 2, slot = w * 16 + wq;                // segment of the block's 64-pair batch
   // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
   uint32_t start = 0u, n;
   if (bounce < 0) {
@@ -630,15 +727,48 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
   s.a2 = 0.0f;
   if (valid) load_pair_seg(vp, p, s, maxd, owner);
-  const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
-  const bool force = force_all(s, om);
+  float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+  bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
   const BvhRes br = bvh_res(sc);
-  uint32_t* my = s_stk + slot * kBvhStack;
+  uint32_t* const s_wave = s_stk + w * 16 * kBvhStack;
+  uint32_t* const my = s_wave + wq * kBvhStack;                // entries [bp, sp) pending
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
-  bool blocked = false;
-  int g = valid ? 0 : -1, sp = 0;
-  while (__any(g >= 0)) {
+  uint32_t wblocked = 0u;                                      // wave-uniform: home quads found blocked
+  int home = wq;
+  int g = valid ? 0 : -1, sp = 0, bp = 0;
+  auto pop = [&]() {
+    const bool has = sp > bp;
+    const int t = (int)my[has ? sp - 1 : 0];
+    g = has ? t : -1;
+    sp = has ? sp - 1 : sp;
+    if (sp == bp) sp = bp = 0;
+  };
+  constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
+  for (;;) {
+    const unsigned long long act = __ballot(g >= 0) & kQuad0;
+    if (!act) break;
+    const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
+    if (ART_VIS_STEAL && donors && idle) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
+      const unsigned long long below = (1ull << (lane & ~3)) - 1ull;
+      const int ir = __popcll(idle & below), dr = __popcll(donors & below);
+      const bool thief = g < 0 && ir < __popcll(donors);
+      const bool robbed = g >= 0 && sp > bp && dr < __popcll(idle);
+      const int src = (thief ? select_bit(donors, ir) : (lane & ~3)) + qd;
+      const int dbp = __shfl(bp, src), dhome = __shfl(home, src), downer = __shfl(owner, src);
+      const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
+      const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
+      const float dmaxd = __shfl(maxd, src);
+      if (thief) {  // the segment's derived values are recomputed as the home computed them
+        g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
+        sp = bp = 0;
+        home = dhome; owner = downer; maxd = dmaxd;
+        s = make_seg(mk3(ox, oy, oz), mk3(dx, dy, dz));
+        om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
+        force = force_all(s, om);
+      }
+      if (robbed && ++bp == sp) sp = bp = 0;
+    }
     while (g >= 0 && g < leaf0) {  // quad-uniform
       const int c0 = 4 * g + 1;
       if (qd == 0) ++nnode;
@@ -654,25 +784,23 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
         sp += __popc(rest);
         g = c0 + first;
       } else {
-        g = sp ? (int)my[sp - 1] : -1;
-        sp = sp ? sp - 1 : 0;
+        pop();
       }
     }
+    bool hit_quad = false;
     if (g >= leaf0) {
       int cc, tid;
       float d;
       const bool hh = leaf_slot_test<OBB>(s, br, (g - leaf0) * kBvhLeaf + qd, cc, d, tid, nt);
       const bool blk_here = hh && d < maxd && tid != owner;  // :373-394, :411-447
-      if ((uint32_t)(__ballot(blk_here) >> qshift) & 0xFu) {
-        blocked = true;
-        g = -1;
-      } else {
-        g = sp ? (int)my[sp - 1] : -1;
-        sp = sp ? sp - 1 : 0;
-      }
+      hit_quad = ((uint32_t)(__ballot(blk_here) >> qshift) & 0xFu) != 0u;
+      if (!hit_quad) pop();
     }
+    for (unsigned long long bq = __ballot(hit_quad) & kQuad0; bq; bq &= bq - 1ull)
+      wblocked |= 1u << __builtin_amdgcn_readlane(home, __builtin_ctzll(bq));
+    if ((wblocked >> home) & 1u) { g = -1; sp = bp = 0; }  // the segment is decided: every quad on it stops
   }
-  if (valid && !blocked && qd == 0) {  // visible: the echo is stored (:142-144)
+  if (valid && !((wblocked >> wq) & 1u) && qd == 0) {  // visible: the echo is stored (:142-144)
     const uint2 o = vp.out[p];
     reinterpret_cast<uint16_t*>(block)[o.x] = (uint16_t)(o.y & 0xffffu);
   }

@@ -698,7 +698,7 @@ def main():
                           "ranks; the step time includes it" if world > 1 else None,
         "roofline": {"bound": "valu", "achieved": ex_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic, "traffic_note": traffic_note,
-                     "kernel": "raytrace stage: nearest_first_kernel + path_kernel + pair sort + vis_kernel + vis_finalize",
+                     "kernel": "raytrace stage: nearest_first_kernel + path_kernel per bounce, echo vis_kernel (side stream) + muffle_kernel",
                      "kernel_ms": rt_ms,
                      "note": "FP32 VALU roof (no MFMA-shaped work). achieved = ops the kernels executed per launch (exact "
                              "tests x SURVEY.md 8(d) ops per test, lane-tests = wave-level tests x 64, plus broad-phase "
