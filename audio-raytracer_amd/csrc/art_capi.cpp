@@ -169,7 +169,16 @@ struct Device {
   // the two jobs independently, AudioRayTracer.cs:191,213), joined before the reduce job (:237)
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
-  SideStream echo;  // the echo visibility beside the pair sort and the muffle sweep
+  SideStream echo;  // the echo visibility beside the muffle kernel
+  // fan lanes: lane j > 0 runs its share of the frame's fans on its own stream (and echo side
+  // stream), forked from and joined to the launch stream, so one lane's traversal tails overlap
+  // the other lane's kernels; lane 0 is the launch stream with `echo`
+  struct Lane {
+    hipStream_t st = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    SideStream echo;
+  };
+  Lane lanes[kMaxFanLanes];
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
   std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
 };
@@ -640,6 +649,16 @@ hipEvent_t pool_event(Device& dv, size_t i) {
   return dv.ev_pool[i];
 }
 
+// Fan lanes per frame (ART_FAN_LANES, 1..kMaxFanLanes; graph-replayed and counting frames use 1).
+int fan_lanes() {
+  static const int n = [] {
+    const char* e = getenv("ART_FAN_LANES");
+    const int v = e ? atoi(e) : kDefaultFanLanes;
+    return std::max(1, std::min(v, kMaxFanLanes));
+  }();
+  return n;
+}
+
 constexpr size_t kGraphCache = 16;         // instantiated frame graphs per device
 constexpr int kGraphsPerProcess = 512;     // and per process (they are released only at exit)
 std::atomic<int> g_graphs_alive{0};
@@ -667,7 +686,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // muffle accumulators, then (16-B aligned) the visibility pair counters: cleared by the first
   // nearest_first_kernel of each fast-path chunk, by one memset before the reference-order kernel
   const size_t acc_words = ((size_t)fan_count * f.TC * f.T + 3) & ~(size_t)3;
-  const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16;
+  const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16 * kMaxFanLanes;  // + 4 pair counters per lane
   if (!dv.acc.reserve(acc_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   uint32_t* acc = static_cast<uint32_t*>(dv.acc.p);
   uint32_t* pair_count = acc + acc_words;
@@ -703,9 +722,26 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.fork, hipEventDisableTiming));
       HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.join, hipEventDisableTiming));
     }
+  }
+  const bool graph = !count && !timing && ((c->flags & ART_CTX_GRAPH) || graphs_forced());
+  const int nlanes = fast && !graph ? std::min(fan_lanes(), fan_count) : 1;
+  const int lane_fans = (fan_count + nlanes - 1) / nlanes;
+  size_t lane_pair_bytes = 0;
+  if (fast) {
+    for (int j = 1; j < nlanes; ++j) {
+      Device::Lane& ln = dv.lanes[j];
+      if (ln.st) continue;
+      HIP_TRY(c, hipStreamCreateWithFlags(&ln.st, hipStreamNonBlocking));
+      HIP_TRY(c, hipEventCreateWithFlags(&ln.fork, hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&ln.join, hipEventDisableTiming));
+      HIP_TRY(c, hipStreamCreateWithFlags(&ln.echo.st, hipStreamNonBlocking));
+      HIP_TRY(c, hipEventCreateWithFlags(&ln.echo.fork, hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&ln.echo.join, hipEventDisableTiming));
+    }
     FrameParams fps = fp;
-    fps.S = std::min(fan_count, chunk);
-    if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
+    fps.S = std::min(lane_fans, chunk);
+    lane_pair_bytes = (fast_pair_bytes(fps) + 255) & ~(size_t)255;
+    if (!dv.pairs.reserve(lane_pair_bytes * nlanes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   }
   // The permeation job (read-only scene and origins, writes only the fans' permeation sections)
   // runs on the side stream concurrently with the raytrace stage, whose kernels leave CUs idle in
@@ -753,14 +789,30 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     } else {
       FrameParams fpx = fp;
       fpx.exec = exec_ctr;
-      // The pair arrays index pairs with 32-bit slots (sorted below 2^31) and the echo outputs with
-      // 32-bit half offsets into the block: larger frames run as consecutive fan chunks on the
-      // stream (the pair buffer and counter are reused, the muffle accumulators offset per chunk).
-      for (int b0 = 0; b0 < fan_count; b0 += chunk) {
-        FrameParams fpc = fpx;
-        fpc.S = std::min(chunk, fan_count - b0);
-        launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
-                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, echo);
+      // The pair arrays index pairs with 32-bit slots (below 2^31) and the echo outputs with 32-bit
+      // half offsets into the block: larger frames run as consecutive fan chunks on a lane's
+      // stream (the lane's pair buffer and counters are reused, the muffle accumulators offset per
+      // chunk). Lanes > 0 fork from st before any lane's kernels and join back before the reduce job.
+      for (int j = 1; j < nlanes; ++j) {
+        HIP_TRY(c, hipEventRecord(dv.lanes[j].fork, st));
+        HIP_TRY(c, hipStreamWaitEvent(dv.lanes[j].st, dv.lanes[j].fork, 0));
+      }
+      for (int j = 0; j < nlanes; ++j) {
+        const int l0 = std::min(fan_count, j * lane_fans), l1 = std::min(fan_count, l0 + lane_fans);
+        Device::Lane& ln = dv.lanes[j];
+        hipStream_t ls = j == 0 ? st : ln.st;
+        void* pairs = static_cast<uint8_t*>(dv.pairs.p) + (size_t)j * lane_pair_bytes;
+        for (int b0 = l0; b0 < l1; b0 += chunk) {
+          FrameParams fpc = fpx;
+          fpc.S = std::min(chunk, l1 - b0);
+          launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
+                               acc + (size_t)b0 * f.TC * f.T, order, pairs, pair_count + 4 * j, ls,
+                               j == 0 ? echo : ln.echo);
+        }
+        if (j > 0) {
+          HIP_TRY(c, hipEventRecord(ln.join, ls));
+          HIP_TRY(c, hipStreamWaitEvent(st, ln.join, 0));
+        }
       }
     }
     if (timing) tstop(ti, st);
@@ -794,7 +846,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // caller's stream for every later frame with the same launch key (scene, frame parameters,
   // buffers, fan count, flags). One graph launch replaces ~10 launches and the host-side fork /
   // join gaps. Opt-in (ART_CTX_GRAPH / ART_GRAPH=1); counting and timed frames launch directly.
-  if (count || timing || !((c->flags & ART_CTX_GRAPH) || graphs_forced())) return launch(st, dv.fork, dv.join, dv.echo);
+  if (!graph) return launch(st, dv.fork, dv.join, dv.echo);
   GraphKey key;
   memset(&key, 0, sizeof key);
   key.sc = dv.sc; key.fp = fp; key.L = f.L;
@@ -995,6 +1047,14 @@ ART_API void art_destroy(art_ctx* c) {
     if (dv.echo.fork) (void)hipEventDestroy(dv.echo.fork);
     if (dv.echo.join) (void)hipEventDestroy(dv.echo.join);
     if (dv.echo.st) (void)hipStreamDestroy(dv.echo.st);
+    for (Device::Lane& ln : dv.lanes) {
+      for (hipStream_t q : {ln.st, ln.echo.st})
+        if (q) (void)hipStreamSynchronize(q);
+      for (hipEvent_t e : {ln.fork, ln.join, ln.echo.fork, ln.echo.join})
+        if (e) (void)hipEventDestroy(e);
+      for (hipStream_t q : {ln.st, ln.echo.st})
+        if (q) (void)hipStreamDestroy(q);
+    }
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
   }
   c->h_in.release();
@@ -1115,6 +1175,9 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
         (void)hipStreamSynchronize(e.stream);
         if (e.side) (void)hipStreamSynchronize(e.side);  // a forked stage may not have joined
         if (e.echo.st) (void)hipStreamSynchronize(e.echo.st);
+        for (Device::Lane& ln : e.lanes)
+          for (hipStream_t q : {ln.st, ln.echo.st})
+            if (q) (void)hipStreamSynchronize(q);
       }
       return rc;
     }

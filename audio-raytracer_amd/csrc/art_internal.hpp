@@ -204,6 +204,8 @@ int fast_fans_per_launch(int R, int H, int T, int TC, uint32_t stride);
 // (+ the bounce's echo vis_kernel), then muffle_kernel. Any target count, every DevScene with a BVH
 // and cell lists. echo_st (optional, with two events): the echo traversals run there, beside the
 // next bounces and the muffle kernel on st, joined at the end.
+constexpr int kMaxFanLanes = 4;      // fan lanes per device (art_capi.cpp)
+constexpr int kDefaultFanLanes = 1;
 struct SideStream {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
