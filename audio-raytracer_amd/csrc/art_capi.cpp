@@ -1019,7 +1019,13 @@ ART_API int art_create_on(const int32_t* device_ids, int32_t count, art_ctx** ou
   return create_on(device_ids, count, out);
 }
 
+#ifdef ART_DIAG
+void art_diag_dump_impl();
+#endif
 ART_API void art_destroy(art_ctx* c) {
+#ifdef ART_DIAG
+  if (c && !c->devs.empty()) art_diag_dump_impl();
+#endif
   if (!c) return;
   if (c->cpu) {
     if (c->inflight) art::cpu_complete(c->cpu, nullptr);

@@ -17,6 +17,7 @@
 // Every output equals the reference's bit for bit: the broad phases are exact, the
 // nearest hit is the (distance, reference order) minimum, any-hit verdicts are ORs.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "art_device_fns.hpp"
@@ -50,6 +51,19 @@ __device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c
 __device__ __forceinline__ void exec_add(unsigned long long* ex, int slot, unsigned long long v) {
   if (ex && v && (threadIdx.x & 63) == 0) atomicAdd(ex + slot, v);
 }
+
+#ifdef ART_DIAG
+// Diagnostic build only (tools/build_variant.sh diag -DART_DIAG): log2 histograms of per-wave
+// cycles (0 nearest, 1 echo) and per-ray traversal steps (2 nearest, 3 echo), printed by
+// art_destroy.
+__device__ unsigned long long g_diag[4][64];
+__device__ __forceinline__ void diag_add(int k, unsigned long long v) {
+  atomicAdd(&g_diag[k][v ? 64 - __builtin_clzll(v) : 0], 1ull);
+}
+#define ART_DIAG_STEP(x) (++(x))
+#else
+#define ART_DIAG_STEP(x) ((void)0)
+#endif
 
 // A ray whose direction or origin is non-finite, or whose direction is zero, makes every box test
 // inconclusive: its traversals visit every node (the exact tests alone decide).
@@ -249,6 +263,8 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   bool shared = false;   // wave-uniform: work was shared in this wave
   float mybest = FLT_MAX;  // this quad's own (distance, order) minimum over the leaves it tested
   int mycode = kNoHit;
+  unsigned nsteps = 0;
+  (void)nsteps;
   // branch-free pop of entries [bp, sp): the slot is read unconditionally (clamped), -1 when empty
   auto pop = [&]() {
     const bool has = sp > bp;
@@ -262,6 +278,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   auto inner_step = [&]() {
     const int c0 = 4 * g + 1;
     if (EX && qd == 0) ++nnode;
+    ART_DIAG_STEP(nsteps);
     const CullRec r = load_node(br, c0 + qd);
     float tn;
     const bool h = node_entry(s, r, om, tn);
@@ -271,6 +288,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     if (sp == bp) sp = bp = 0;
   };
   auto leaf_step = [&](int leaf) {
+    ART_DIAG_STEP(nsteps);
     int cc, tid;
     float dd;
     const bool h = leaf_slot_test<OBB>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, dd, tid, nt);
@@ -340,6 +358,9 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     }
     if (pend >= 0) { leaf_step(pend); pend = -1; }
   }
+#ifdef ART_DIAG
+  if (qd == 0 && alive) diag_add(2, nsteps);
+#endif
   best = mybest;
   code = mycode;
   if (ART_NEAREST_STEAL && shared) {  // the ray's result: the minimum over the quads that traversed it
@@ -425,8 +446,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void n
     write = true;
     out = (uint32_t)g * 64u + (uint32_t)rr;
   }
+#ifdef ART_DIAG
+  const unsigned long long t0 = clock64();
+#endif
   quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code, ex);
   if ((lane & 3) == 0 && write) hits[out] = make_int2(__float_as_int(best), code);
+#ifdef ART_DIAG
+  if (lane == 0) diag_add(0, clock64() - t0);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -737,6 +764,11 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   uint32_t wblocked = 0u;                                      // wave-uniform: home quads found blocked
   int home = wq;
   int g = valid ? 0 : -1, sp = 0, bp = 0;
+  unsigned nsteps = 0;
+  (void)nsteps;
+#ifdef ART_DIAG
+  const unsigned long long t0 = clock64();
+#endif
   auto pop = [&]() {
     const bool has = sp > bp;
     const int t = (int)my[has ? sp - 1 : 0];
@@ -772,6 +804,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     while (g >= 0 && g < leaf0) {  // quad-uniform
       const int c0 = 4 * g + 1;
       if (qd == 0) ++nnode;
+      ART_DIAG_STEP(nsteps);
       const CullRec r = load_node(br, c0 + qd);
       float tn;
       const bool h = node_entry(s, r, om, tn);
@@ -789,6 +822,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     }
     bool hit_quad = false;
     if (g >= leaf0) {
+      ART_DIAG_STEP(nsteps);
       int cc, tid;
       float d;
       const bool hh = leaf_slot_test<OBB>(s, br, (g - leaf0) * kBvhLeaf + qd, cc, d, tid, nt);
@@ -800,6 +834,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       wblocked |= 1u << __builtin_amdgcn_readlane(home, __builtin_ctzll(bq));
     if ((wblocked >> home) & 1u) { g = -1; sp = bp = 0; }  // the segment is decided: every quad on it stops
   }
+#ifdef ART_DIAG
+  if (qd == 0 && valid) diag_add(3, nsteps);
+  if (lane == 0) diag_add(1, clock64() - t0);
+#endif
   if (valid && !((wblocked >> wq) & 1u) && qd == 0) {  // visible: the echo is stored (:142-144)
     const uint2 o = vp.out[p];
     reinterpret_cast<uint16_t*>(block)[o.x] = (uint16_t)(o.y & 0xffffu);
@@ -1058,4 +1096,17 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   }
 }
 
+#ifdef ART_DIAG
+extern "C" void art_diag_dump_impl() {
+  unsigned long long h[4][64];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof h) != hipSuccess) return;
+  const char* names[4] = {"nearest wave cycles", "echo wave cycles", "nearest ray steps", "echo ray steps"};
+  for (int k = 0; k < 4; ++k) {
+    fprintf(stderr, "[diag] %s (log2 bucket: count)", names[k]);
+    for (int b = 0; b < 64; ++b)
+      if (h[k][b]) fprintf(stderr, " %d:%llu", b, h[k][b]);
+    fprintf(stderr, "\n");
+  }
+}
+#endif
 }  // namespace art
