@@ -98,7 +98,7 @@ struct Frame {
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
   size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
   // muffle candidate lists (art_cells.hip)
-  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, cells_temp = 0,
+  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, cells_temp = 0,
          soa_cgeo = 0;
   uint32_t cells_cap = 0;
 };
@@ -459,17 +459,19 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_obb_s = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
     f.soa_cull_s = s; s = align_up(s + n * sizeof(CullRec), 256);
     f.soa_chunks = s; s = align_up(s + nch * sizeof(CullRec), 256);
-    f.soa_bvh = s; s = align_up(s + bvh_node_count((int)n) * sizeof(CullRec), 256);
+    f.soa_bvh = s; s = align_up(s + 2 * bvh_node_count((int)n) * sizeof(CullRec), 256);  // nodes + pre-widened boxes
     f.soa_bvh_ref = s; s = align_up(s + n * 4, 256);
     f.soa_bvh_leaf = s; s = align_up(s + bvh_slot_count((int)n) * 64, 256);
   }
   {  // muffle candidate lists
-    const size_t cells = (size_t)f.T * kCells;
-    f.cells_temp = cells_scan_temp_bytes(f.T);
+    const size_t cells = (size_t)f.T * kCells * 3;  // lists per (target, cell, collider type)
     f.cells_cap = (uint32_t)cells_entry_cap(f.T, f.ns + f.na + f.no);
+    f.cells_temp = cells_scan_temp_bytes(f.T, f.cells_cap);
     f.soa_ccount = s; s = align_up(s + (cells + 1) * 4, 256);
     f.soa_cstart = s; s = align_up(s + (cells + 1) * 4, 256);
-    f.soa_ccur = s; s = align_up(s + cells * 4, 256);
+    f.soa_ccur = s; s = align_up(s + (cells + 1) * 4, 256);
+    f.soa_ckeys = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
+    f.soa_cent_s = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
     f.soa_cfar = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_cok = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_ctemp = s; s = align_up(s + f.cells_temp, 256);
@@ -590,6 +592,8 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.ok = reinterpret_cast<uint32_t*>(soa + f.soa_cok);
     cb.temp = soa + f.soa_ctemp; cb.temp_bytes = f.cells_temp;
     cb.ent = reinterpret_cast<uint2*>(soa + f.soa_cent);
+    cb.ent_s = reinterpret_cast<uint2*>(soa + f.soa_cent_s);
+    cb.keys = reinterpret_cast<uint32_t*>(soa + f.soa_ckeys);
     cb.cap = f.cells_cap;
     cb.geo = soa + f.soa_cgeo;
     if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");

@@ -177,8 +177,9 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
   const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
   if (j < j0 || j > j1 || i0 > i1) return;
   const int t = (int)(p / n);
-  uint32_t* cnt = cb.count + (size_t)t * kCells;
-  uint32_t* cur = cb.cursor + (size_t)t * kCells;
+  const uint32_t ty = G.code >> 28;  // one list per collider type
+  uint32_t* cnt = cb.count + (size_t)t * kCells * 3 + ty;
+  uint32_t* cur = cb.cursor + (size_t)t * kCells * 3 + ty;
   for (int i = i0; i <= i1; ++i) {
     const int c = (f * kCellG + j) * kCellG + i;
     const CellCone cc = cb.cones[c];
@@ -186,20 +187,32 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
     const bool hit = G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
     if (!hit) continue;
     if (!FILL) {
-      atomicAdd(cnt + c, 1u);
+      atomicAdd(cnt + 3 * c, 1u);
     } else {
-      const uint32_t pos = atomicAdd(cur + c, 1u);
+      const uint32_t pos = atomicAdd(cur + 3 * c, 1u);
       if (pos < cb.cap) cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
       else cb.ok[t] = 0u;  // overflow: this target's muffle rays test every collider
     }
   }
 }
 
-size_t cells_scan_temp_bytes(int T) {
-  size_t bytes = 0;
-  const int n = T * kCells + 1;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, n);
-  return bytes;
+size_t cells_scan_temp_bytes(int T, uint32_t cap) {
+  size_t scan = 0, sort = 0;
+  const int n = T * kCells * 3 + 1;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, n);
+  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, sort, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                    (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                                    (int)cap, n - 1, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                                    0, 16);
+  return std::max(scan, sort);
+}
+
+// Sort keys of the filled entries, and the segment offsets clamped to the capacity (a target
+// whose lists overflowed is tested against every collider; its segments are sorted harmlessly).
+__global__ void cells_key_kernel(CellBufs cb, uint32_t total_cells) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cb.cap) cb.keys[i] = near_key(cb.ent[i].y);
+  if (i <= total_cells) cb.cursor[i] = min(cb.start[i], cb.cap);
 }
 
 // Entry capacity: 128 cells per (target, collider) on average (a collider near its target spans
@@ -211,7 +224,7 @@ size_t cells_entry_cap(int T, int C) {
 
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   const int T = sc.T, n = sc.ns + sc.na + sc.no;
-  const int cells = T * kCells;
+  const int cells = T * kCells * 3;  // lists: (target, cell, collider type)
   hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.far, cb.ok);
   if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
   const long long pairs = (long long)n * T;
@@ -229,8 +242,19 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
     const unsigned rb = (unsigned)((pairs * 6 * kCellG + 255) / 256);
     hipLaunchKernelGGL(cells_row_kernel<true>, dim3(rb), dim3(256), 0, st, geo, pairs, cb, n);
   }
+  // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its segment
+  {
+    const uint32_t span = std::max<uint32_t>(cb.cap, (uint32_t)cells + 1);
+    hipLaunchKernelGGL(cells_key_kernel, dim3((span + 255) / 256), dim3(256), 0, st, cb, (uint32_t)cells);
+    size_t sbytes = cb.temp_bytes;
+    if (hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
+                                                    reinterpret_cast<const unsigned long long*>(cb.ent),
+                                                    reinterpret_cast<unsigned long long*>(cb.ent_s), (int)cb.cap, cells,
+                                                    cb.cursor, cb.cursor + 1, 0, 16, st) != hipSuccess)
+      return -1;
+  }
   sc.cell_start = cb.start;
-  sc.cell_ent = cb.ent;
+  sc.cell_ent = cb.ent_s;
   sc.cell_far = cb.far;
   sc.cell_ok = cb.ok;
   sc.cell_cap = cb.cap;

@@ -80,7 +80,8 @@ struct DevScene {
   // of node g at 4g + 1 .. 4g + 4) over the Morton order of the bounds' centres, kBvhLeaf colliders
   // per leaf; the leaves are nodes bvh_leaf0 .. bvh_leaf0 + 4^(levels - 1) - 1 (those past the
   // last collider are empty). A node's CullRec is the union of its colliders' bounds with their
-  // largest margin scale and factor; an empty node has lo > hi.
+  // largest margin scale and factor; an empty node has lo > hi. The node array is followed by the
+  // nodes' pre-widened boxes (bvh_wide_kernel, art_bvh.hip): 2 float4 per node.
   const CullRec* bvh;
   const uint32_t* bvh_ref;        // [ns + na + no] in Morton order: type rank << 30 | in-type index
   const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] 64-B slots in Morton order: the
@@ -91,10 +92,12 @@ struct DevScene {
   // Muffle candidate lists (art_cells.hip): for target t and direction cell c (a
   // cube map of kCellG x kCellG cells per face around the target), the colliders not owned by t
   // whose widened bounding sphere meets cell c's cone; entries (order code, distance from the
-  // target to the sphere) at cell_ent[cell_start[t * kCells + c] ..). A target whose bound or list
+  // target to the sphere) at cell_ent[cell_start[(t * kCells + c) * 3 + type] ..), one list per
+  // collider type (Sphere, AABB, OBB: muffle_kernel walks them with type-uniform tests), each by
+  // ascending near bound. A target whose bound or list
   // overflowed (cell_ok[t] == 0) is tested against every collider instead.
-  const uint32_t* cell_start;     // [T * kCells + 1]
-  const uint2* cell_ent;          // [cell_cap]: (code, near bits)
+  const uint32_t* cell_start;     // [T * kCells * 3 + 1]
+  const uint2* cell_ent;          // [cell_cap]: (code, near bits), each cell's entries by ascending near_key
   const float* cell_far;          // [T]: the segment length the lists were built for
   const uint32_t* cell_ok;        // [T]
   uint32_t cell_cap;
@@ -116,7 +119,7 @@ struct SortBufs {
   uint32_t* keys; uint32_t* keys_s; int* vals; int* perm;
   void* temp; size_t temp_bytes;
   SphereRec* sph_s; AabbRec* aabb_s; ObbRec* obb_s; CullRec* cull_s; CullRec* chunks;
-  CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count) and leaf references
+  CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count, then as many pre-widened boxes) and leaf references
   float4* bvh_leaf;                 // leaf slots (bvh_slot_count)
 };
 // per-sample spatializer DSP (art_dsp.hip)
@@ -138,20 +141,28 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
 int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
 
 // Muffle candidate lists (art_cells.hip): built after every scene upload / refit on stream st.
+// Sort key of a cell entry's near bound (bits of a float): the top 16 bits of its non-negative
+// value (0 for a bound <= 0), monotone in the bound, so a list sorted by it can stop at the first
+// key above the segment's key.
+__host__ __device__ inline uint32_t near_key(uint32_t near_bits) {
+  return (int32_t)near_bits <= 0 ? 0u : near_bits >> 16;
+}
 struct CellBufs {
   const CellCone* cones;          // [kCells]
   float alpha_max;                // largest cone half-angle (with slack)
-  uint32_t* count;                // [T * kCells + 1] entries per cell
-  uint32_t* start;                // [T * kCells + 1] exclusive scan of count (DevScene::cell_start)
-  uint32_t* cursor;               // [T * kCells] fill positions
-  uint2* ent;                     // [cap]
+  uint32_t* count;                // [T * kCells * 3 + 1] entries per (cell, collider type)
+  uint32_t* start;                // [T * kCells * 3 + 1] exclusive scan of count (DevScene::cell_start)
+  uint32_t* cursor;               // [T * kCells * 3 + 1] fill positions, then the sort's segment offsets
+  uint2* ent;                     // [cap] in fill order
+  uint2* ent_s;                   // [cap] each cell's entries by ascending near bound (DevScene::cell_ent)
+  uint32_t* keys;                 // [2 * cap] sort keys (near_key) and their sorted copy
   float* far;                     // [T]: distance bound of t's segments
   uint32_t* ok;                   // [T]
   uint32_t cap;
-  void* temp; size_t temp_bytes;  // hipcub scan storage
+  void* temp; size_t temp_bytes;  // hipcub scan / segmented sort storage
   void* geo;                      // [T * C] per-(target, collider) geometry (cells_geo_bytes)
 };
-size_t cells_scan_temp_bytes(int T);
+size_t cells_scan_temp_bytes(int T, uint32_t cap);
 size_t cells_geo_bytes(int T, int C);
 size_t cells_entry_cap(int T, int C);
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st);

@@ -27,23 +27,16 @@ namespace art {
 constexpr int kNoHit = 0x7fffffff;
 constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
 
-// Sphere test split so the common miss costs no branch: the square root and the two IEEE
-// divisions run only for lanes whose discriminant is non-negative (RayIntersectsSphere :323-355).
+// Sphere test of the traversals and visibility kernels: RayIntersectsSphere (:323-355) with one
+// IEEE division (sphere_test_1div: the same verdict and distance bits; the square root and the
+// division run only for lanes whose discriminant is non-negative).
 __device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c, float& dist) {
-  vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
-  float b = 2.0f * dot(oc, s.d);
-  float cc = dot(oc, oc) - c.r2;
-  float disc = b * b - (2.0f * s.a2) * cc;  // 4 * a * c (:329)
-  bool hit = false;
+#if ART_SPHERE_2DIV
   dist = 0.0f;
-  if (disc >= 0.0f) {
-    float sq = sqrtf(disc);
-    float t0 = (-b - sq) / s.a2;
-    float t1 = (-b + sq) / s.a2;
-    hit = (t0 >= 0.0f) || (t1 >= 0.0f);
-    dist = (t0 >= 0.0f) ? t0 : t1;
-  }
-  return hit;
+  return sphere_test(s, c, dist);
+#else
+  return sphere_test_1div(s, c, dist);
+#endif
 }
 
 // Executed-work accounting (ART_CTX_COUNT_EXECUTED): one atomic per call from lane 0, off when
@@ -125,14 +118,14 @@ __device__ __forceinline__ int quad_max_i32(int v) {
 
 // The BVH node and leaf arrays as buffer resources (wave-uniform bases, 32-bit lane offsets).
 struct BvhRes {
-  __amdgpu_buffer_rsrc_t nodes, leaves;
+  __amdgpu_buffer_rsrc_t nodes, leaves, wide;
 };
 __device__ __forceinline__ BvhRes bvh_res(const DevScene& sc) {
   BvhRes b;
-  const int leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1;
-  b.nodes = __builtin_amdgcn_make_buffer_rsrc(const_cast<CullRec*>(sc.bvh), 0, (leaf0 + nleaf) * (int)sizeof(CullRec),
-                                              0x00020000);
+  const int leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1, total = leaf0 + nleaf;
+  b.nodes = __builtin_amdgcn_make_buffer_rsrc(const_cast<CullRec*>(sc.bvh), 0, total * (int)sizeof(CullRec), 0x00020000);
   b.leaves = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(sc.bvh_leaf), 0, nleaf * kBvhLeaf * 64, 0x00020000);
+  b.wide = __builtin_amdgcn_make_buffer_rsrc(const_cast<CullRec*>(sc.bvh + total), 0, total * 32, 0x00020000);
   return b;
 }
 __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
@@ -142,6 +135,25 @@ __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
   r.lox = a.x; r.loy = a.y; r.loz = a.z; r.scale = a.w;
   r.hix = c.x; r.hiy = c.y; r.hiz = c.z; r.factor = c.w;
   return r;
+}
+// The origin-magnitude cap of the pre-widened boxes (bvh_wide_kernel; -1: none).
+__device__ __forceinline__ float wide_cap(const DevScene& sc) {
+  return reinterpret_cast<const float*>(sc.bvh + (4 * sc.bvh_leaf0 + 1))[3];
+}
+// Entry of node i: its pre-widened box (WIDE: every ray of the wave has |o|_1 (+ maxd) <= the cap)
+// or its box widened for this ray's om (node_entry); `valid` = the node is not empty.
+__device__ __forceinline__ bool node_entry_at(const Seg& s, const BvhRes& br, int i, float om, bool wide, float& tn,
+                                              bool& valid) {
+  if (wide) {
+    const float4 lo = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.wide, i * 32, 0, 0));
+    const float4 hi = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.wide, i * 32 + 16, 0, 0));
+    float tf;
+    valid = lo.x <= hi.x;
+    return slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, tn, tf);
+  }
+  const CullRec r = load_node(br, i);
+  valid = r.lox <= r.hix;
+  return node_entry(s, r, om, tn);
 }
 
 // One inner step of a quad traversal (lane qd holds child c0 + qd; `enter` / entry `en` its
@@ -258,6 +270,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
+  const bool wide = !__any(alive && !(om <= wide_cap(sc)));  // wave-uniform: the pre-widened boxes hold every ray
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
   float lim = FLT_MAX;   // pruning bound: best, and (shared work) the other quads' results for the ray
   bool shared = false;   // wave-uniform: work was shared in this wave
@@ -279,11 +292,11 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     const int c0 = 4 * g + 1;
     if (EX && qd == 0) ++nnode;
     ART_DIAG_STEP(nsteps);
-    const CullRec r = load_node(br, c0 + qd);
     float tn;
-    const bool h = node_entry(s, r, om, tn);
+    bool valid;
+    const bool h = node_entry_at(s, br, c0 + qd, om, wide, tn, valid);
     const float en = fmaxf(tn, 0.0f);
-    const bool enter = (r.lox <= r.hix) & (force | (h & (en <= lim)));  // bitwise: no branch
+    const bool enter = valid & (force | (h & (en <= lim)));  // bitwise: no branch
     quad_descend(enter, en, force, qd, c0, my, g, sp);
     if (sp == bp) sp = bp = 0;
   };
@@ -758,6 +771,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
   const BvhRes br = bvh_res(sc);
+  const bool wide = !__any(valid && !(om <= wide_cap(sc)));  // wave-uniform: the pre-widened boxes hold every segment
   uint32_t* const s_wave = s_stk + w * 16 * kBvhStack;
   uint32_t* const my = s_wave + wq * kBvhStack;                // entries [bp, sp) pending
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
@@ -805,10 +819,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       const int c0 = 4 * g + 1;
       if (qd == 0) ++nnode;
       ART_DIAG_STEP(nsteps);
-      const CullRec r = load_node(br, c0 + qd);
       float tn;
-      const bool h = node_entry(s, r, om, tn);
-      const bool enter = (r.lox <= r.hix) & (force | (h & (tn <= maxd)));  // bitwise: no branch
+      bool valid_node;
+      const bool h = node_entry_at(s, br, c0 + qd, om, wide, tn, valid_node);
+      const bool enter = valid_node & (force | (h & (tn <= maxd)));  // bitwise: no branch
       const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);
@@ -941,15 +955,42 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
       const bool lists = sc.cell_ok[t] != 0u && maxd <= sc.cell_far[t] && (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f) &&
                          isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
       if (lists) {
-        const uint32_t* st = sc.cell_start + (size_t)t * kCells + cube_cell(v);
-        const uint32_t b = st[0], e = st[1];
+        // the cell's Sphere, AABB and OBB lists in turn (a type-uniform test per loop), each by
+        // ascending near bound: a walk stops at the first entry past the segment
+        const uint32_t* st = sc.cell_start + ((size_t)t * kCells + cube_cell(v)) * 3;
         const float lim = maxd * 1.00001f + 1e-6f;
-        if (EX) ne += e - b;
-        for (uint32_t k = b; k < e; ++k) {
-          const uint2 en = sc.cell_ent[k];
-          if (__uint_as_float(en.y) > lim) continue;  // the collider lies beyond the segment
-          if (muffle_test<OBB>(sc, s, en.x, maxd, nt)) { blocked = true; break; }
-        }
+        const uint32_t klim = near_key(__float_as_uint(lim));
+        const uint4 se = make_uint4(st[0], st[1], st[2], st[3]);
+        auto walk = [&](uint32_t b, uint32_t e, auto test) {
+          for (uint32_t k = b; k < e && !blocked; ++k) {
+            const uint2 en = sc.cell_ent[k];
+            if (near_key(en.y) > klim) break;             // this and every later entry lie beyond the segment
+            if (EX) ++ne;
+            if (__uint_as_float(en.y) > lim) continue;    // the collider lies beyond the segment
+            blocked = test(en.x & 0x0fffffffu);
+          }
+        };
+        walk(se.x, se.y, [&](uint32_t idx) {
+          const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
+          SphereRec r;
+          r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
+          ++nt[0];
+          float d;
+          return sphere_hit_dist(s, r, d) && d < maxd;
+        });
+        walk(se.y, se.z, [&](uint32_t idx) {
+          const AabbRec r = sc.aabb[idx];
+          ++nt[1];
+          float d;
+          return aabb_test<false>(s, r, d) && d < maxd;
+        });
+        if (OBB)
+          walk(se.z, se.w, [&](uint32_t idx) {
+            const ObbRec r = sc.obb[idx];
+            ++nt[2];
+            float d;
+            return obb_test<false>(s, r, stored_q(r), d) && d < maxd;
+          });
       } else {
         if (EX) ++nfb;
         blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
