@@ -217,9 +217,6 @@ size_t bvh_node_count(int n) {
   return bvh_layout(n, leaf0, total) ? (size_t)total : 0;
 }
 
-// Nodes of an L-level tree: (4^L - 1) / 3.
-static size_t bvh_node_count_levels(int L) { return (((size_t)1 << (2 * L)) - 1) / 3; }
-
 size_t bvh_slot_count(int n) {
   int leaf0 = 0, total = 0;
   return bvh_layout(n, leaf0, total) ? (size_t)(total - leaf0) * kBvhLeaf : 0;
@@ -337,48 +334,12 @@ __global__ __launch_bounds__(1024) void bvh_upper_kernel(CullRec* __restrict__ n
   }
 }
 
-// Pre-widened node boxes (the traversals' fast path): node i's box widened
-// by its margin for the origin-magnitude cap om_cap = 4 |scene corner|_1 + 16, written after the
-// nodes as 2 float4 (lo - m, om_cap in node 0's w | hi + m). A traversal whose rays all have
-// |o|_1 (+ maxd) <= om_cap tests these boxes instead of widening per ray: the margin is monotone
-// in the origin magnitude and fp32 rounding is monotone, so every box contains the per-ray widened
-// box and every entry is at most the per-ray entry (a superset of visited nodes, the same
-// results). An empty node keeps its lo > hi; a node whose widened bounds are not finite gets
-// infinite ones (always entered when non-empty).
-__global__ void bvh_wide_kernel(const CullRec* __restrict__ nodes, int total, float4* __restrict__ wide) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const CullRec root = nodes[0];
-  float cap = 4.0f * (fmaxf(fabsf(root.lox), fabsf(root.hix)) + fmaxf(fabsf(root.loy), fabsf(root.hiy)) +
-                      fmaxf(fabsf(root.loz), fabsf(root.hiz))) + 16.0f;
-  if (!isfinite(cap)) cap = -1.0f;  // non-finite scene bounds: every traversal widens per ray
-  const CullRec r = nodes[i];
-  float4 lo = make_float4(r.lox, r.loy, r.loz, 0.0f), hi = make_float4(r.hix, r.hiy, r.hiz, 0.0f);
-  if (r.lox <= r.hix && cap >= 0.0f) {
-    const float m = r.factor * (r.scale + cap);
-    lo = make_float4(r.lox - m, r.loy - m, r.loz - m, 0.0f);
-    hi = make_float4(r.hix + m, r.hiy + m, r.hiz + m, 0.0f);
-    if (!(isfinite(m) && isfinite(lo.x) && isfinite(lo.y) && isfinite(lo.z) && isfinite(hi.x) && isfinite(hi.y) &&
-          isfinite(hi.z))) {
-      lo = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
-      hi = make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
-    }
-  }
-  if (i == 0) lo.w = cap;
-  wide[2 * i] = lo;
-  wide[2 * i + 1] = hi;
-}
-
-// Inner levels L-2 .. 0: levels of more than 4096 nodes one launch each, the rest in one workgroup;
-// then the pre-widened boxes of every node.
+// Inner levels L-2 .. 0: levels of more than 4096 nodes one launch each, the rest in one workgroup.
 static void launch_bvh_upper(CullRec* nodes, int L, hipStream_t st) {
   int l = L - 2;
   for (; l >= 0 && (1 << (2 * l)) > 4096; --l)
     hipLaunchKernelGGL(bvh_level_kernel, dim3(((1 << (2 * l)) + 255) / 256), dim3(256), 0, st, nodes, l);
   if (l >= 0) hipLaunchKernelGGL(bvh_upper_kernel, dim3(1), dim3(1024), 0, st, nodes, l);
-  const int total = (int)bvh_node_count_levels(L);
-  hipLaunchKernelGGL(bvh_wide_kernel, dim3((total + 255) / 256), dim3(256), 0, st, nodes, total,
-                     reinterpret_cast<float4*>(nodes + total));
 }
 
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {

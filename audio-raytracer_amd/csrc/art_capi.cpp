@@ -459,7 +459,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_obb_s = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
     f.soa_cull_s = s; s = align_up(s + n * sizeof(CullRec), 256);
     f.soa_chunks = s; s = align_up(s + nch * sizeof(CullRec), 256);
-    f.soa_bvh = s; s = align_up(s + 2 * bvh_node_count((int)n) * sizeof(CullRec), 256);  // nodes + pre-widened boxes
+    f.soa_bvh = s; s = align_up(s + bvh_node_count((int)n) * sizeof(CullRec), 256);
     f.soa_bvh_ref = s; s = align_up(s + n * 4, 256);
     f.soa_bvh_leaf = s; s = align_up(s + bvh_slot_count((int)n) * 64, 256);
   }

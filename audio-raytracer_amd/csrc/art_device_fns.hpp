@@ -95,36 +95,6 @@ ART_HD bool sphere_test(const Seg& s, const SphereRec& c, float& dist) {
   return false;
 }
 
-// RayIntersectsSphere with one IEEE division instead of two (the traversals' leaf test): the same
-// hit verdict and distance bits as sphere_test. For 0 < a2 < inf the sign of t = n / a2 is the
-// sign of n, except that a negative n whose quotient rounds to -0 (|n / a2| <= 2^-150) gives
-// t >= 0; that needs |n| < a2 * 2^-148, where the exact quotient is computed. Other a2 (zero,
-// infinite, NaN: degenerate directions) take both divisions. The distance is then the one quotient
-// t0 or t1 that sphere_test selects, from the same operands.
-// (t0 = n0 / a2, t1 = n1 / a2: hit = t0 >= 0 || t1 >= 0, dist = t0 >= 0 ? t0 : t1)
-ART_HD bool sphere_pick_1div(float n0, float n1, float a2, float& dist) {
-  if (a2 > 0.0f && a2 < INFINITY) {
-    const float thr = a2 * 0x1p-148f;
-    const bool p0 = n0 >= 0.0f || (fabsf(n0) < thr && n0 / a2 >= 0.0f);
-    const bool p1 = n1 >= 0.0f || (fabsf(n1) < thr && n1 / a2 >= 0.0f);
-    dist = (p0 ? n0 : n1) / a2;
-    return p0 || p1;
-  }
-  const float t0 = n0 / a2, t1 = n1 / a2;
-  dist = t0 >= 0.0f ? t0 : t1;
-  return t0 >= 0.0f || t1 >= 0.0f;
-}
-ART_HD bool sphere_test_1div(const Seg& s, const SphereRec& c, float& dist) {
-  vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
-  float b = 2.0f * dot(oc, s.d);
-  float cc = dot(oc, oc) - c.r2;
-  float disc = b * b - (2.0f * s.a2) * cc;  // 4 * a * c (:329)
-  dist = 0.0f;
-  if (!(disc >= 0.0f)) return false;
-  const float sq = sqrtf(disc);
-  return sphere_pick_1div(-b - sq, -b + sq, s.a2, dist);
-}
-
 struct LaneCounts {
   uint32_t s, a, o;
 };

@@ -80,8 +80,7 @@ struct DevScene {
   // of node g at 4g + 1 .. 4g + 4) over the Morton order of the bounds' centres, kBvhLeaf colliders
   // per leaf; the leaves are nodes bvh_leaf0 .. bvh_leaf0 + 4^(levels - 1) - 1 (those past the
   // last collider are empty). A node's CullRec is the union of its colliders' bounds with their
-  // largest margin scale and factor; an empty node has lo > hi. The node array is followed by the
-  // nodes' pre-widened boxes (bvh_wide_kernel, art_bvh.hip): 2 float4 per node.
+  // largest margin scale and factor; an empty node has lo > hi.
   const CullRec* bvh;
   const uint32_t* bvh_ref;        // [ns + na + no] in Morton order: type rank << 30 | in-type index
   const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] 64-B slots in Morton order: the
@@ -119,7 +118,7 @@ struct SortBufs {
   uint32_t* keys; uint32_t* keys_s; int* vals; int* perm;
   void* temp; size_t temp_bytes;
   SphereRec* sph_s; AabbRec* aabb_s; ObbRec* obb_s; CullRec* cull_s; CullRec* chunks;
-  CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count, then as many pre-widened boxes) and leaf references
+  CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count) and leaf references
   float4* bvh_leaf;                 // leaf slots (bvh_slot_count)
 };
 // per-sample spatializer DSP (art_dsp.hip)

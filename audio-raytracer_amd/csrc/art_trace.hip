@@ -27,16 +27,25 @@ namespace art {
 constexpr int kNoHit = 0x7fffffff;
 constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
 
-// Sphere test of the traversals and visibility kernels: RayIntersectsSphere (:323-355) with one
-// IEEE division (sphere_test_1div: the same verdict and distance bits; the square root and the
-// division run only for lanes whose discriminant is non-negative).
+// Sphere test split so the common miss costs no branch: the square root and the two IEEE
+// divisions run only for lanes whose discriminant is non-negative (RayIntersectsSphere :323-355).
+// (A one-division form, selecting the quotient by the numerators' signs, measured 1-3 % slower in
+// both traversals: DESIGN.md §4.)
 __device__ __forceinline__ bool sphere_hit_dist(const Seg& s, const SphereRec& c, float& dist) {
-#if ART_SPHERE_2DIV
+  vec3 oc = s.o - mk3(c.cx, c.cy, c.cz);
+  float b = 2.0f * dot(oc, s.d);
+  float cc = dot(oc, oc) - c.r2;
+  float disc = b * b - (2.0f * s.a2) * cc;  // 4 * a * c (:329)
+  bool hit = false;
   dist = 0.0f;
-  return sphere_test(s, c, dist);
-#else
-  return sphere_test_1div(s, c, dist);
-#endif
+  if (disc >= 0.0f) {
+    float sq = sqrtf(disc);
+    float t0 = (-b - sq) / s.a2;
+    float t1 = (-b + sq) / s.a2;
+    hit = (t0 >= 0.0f) || (t1 >= 0.0f);
+    dist = (t0 >= 0.0f) ? t0 : t1;
+  }
+  return hit;
 }
 
 // Executed-work accounting (ART_CTX_COUNT_EXECUTED): one atomic per call from lane 0, off when
@@ -118,14 +127,13 @@ __device__ __forceinline__ int quad_max_i32(int v) {
 
 // The BVH node and leaf arrays as buffer resources (wave-uniform bases, 32-bit lane offsets).
 struct BvhRes {
-  __amdgpu_buffer_rsrc_t nodes, leaves, wide;
+  __amdgpu_buffer_rsrc_t nodes, leaves;
 };
 __device__ __forceinline__ BvhRes bvh_res(const DevScene& sc) {
   BvhRes b;
   const int leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1, total = leaf0 + nleaf;
   b.nodes = __builtin_amdgcn_make_buffer_rsrc(const_cast<CullRec*>(sc.bvh), 0, total * (int)sizeof(CullRec), 0x00020000);
   b.leaves = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(sc.bvh_leaf), 0, nleaf * kBvhLeaf * 64, 0x00020000);
-  b.wide = __builtin_amdgcn_make_buffer_rsrc(const_cast<CullRec*>(sc.bvh + total), 0, total * 32, 0x00020000);
   return b;
 }
 __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
@@ -135,25 +143,6 @@ __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
   r.lox = a.x; r.loy = a.y; r.loz = a.z; r.scale = a.w;
   r.hix = c.x; r.hiy = c.y; r.hiz = c.z; r.factor = c.w;
   return r;
-}
-// The origin-magnitude cap of the pre-widened boxes (bvh_wide_kernel; -1: none).
-__device__ __forceinline__ float wide_cap(const DevScene& sc) {
-  return reinterpret_cast<const float*>(sc.bvh + (4 * sc.bvh_leaf0 + 1))[3];
-}
-// Entry of node i: its pre-widened box (WIDE: every ray of the wave has |o|_1 (+ maxd) <= the cap)
-// or its box widened for this ray's om (node_entry); `valid` = the node is not empty.
-__device__ __forceinline__ bool node_entry_at(const Seg& s, const BvhRes& br, int i, float om, bool wide, float& tn,
-                                              bool& valid) {
-  if (wide) {
-    const float4 lo = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.wide, i * 32, 0, 0));
-    const float4 hi = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.wide, i * 32 + 16, 0, 0));
-    float tf;
-    valid = lo.x <= hi.x;
-    return slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, tn, tf);
-  }
-  const CullRec r = load_node(br, i);
-  valid = r.lox <= r.hix;
-  return node_entry(s, r, om, tn);
 }
 
 // One inner step of a quad traversal (lane qd holds child c0 + qd; `enter` / entry `en` its
@@ -270,7 +259,6 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
-  const bool wide = !__any(alive && !(om <= wide_cap(sc)));  // wave-uniform: the pre-widened boxes hold every ray
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
   float lim = FLT_MAX;   // pruning bound: best, and (shared work) the other quads' results for the ray
   bool shared = false;   // wave-uniform: work was shared in this wave
@@ -292,11 +280,11 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     const int c0 = 4 * g + 1;
     if (EX && qd == 0) ++nnode;
     ART_DIAG_STEP(nsteps);
+    const CullRec r = load_node(br, c0 + qd);
     float tn;
-    bool valid;
-    const bool h = node_entry_at(s, br, c0 + qd, om, wide, tn, valid);
+    const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
-    const bool enter = valid & (force | (h & (en <= lim)));  // bitwise: no branch
+    const bool enter = (r.lox <= r.hix) & (force | (h & (en <= lim)));  // bitwise: no branch
     quad_descend(enter, en, force, qd, c0, my, g, sp);
     if (sp == bp) sp = bp = 0;
   };
@@ -771,7 +759,6 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
   const BvhRes br = bvh_res(sc);
-  const bool wide = !__any(valid && !(om <= wide_cap(sc)));  // wave-uniform: the pre-widened boxes hold every segment
   uint32_t* const s_wave = s_stk + w * 16 * kBvhStack;
   uint32_t* const my = s_wave + wq * kBvhStack;                // entries [bp, sp) pending
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
@@ -819,10 +806,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       const int c0 = 4 * g + 1;
       if (qd == 0) ++nnode;
       ART_DIAG_STEP(nsteps);
+      const CullRec r = load_node(br, c0 + qd);
       float tn;
-      bool valid_node;
-      const bool h = node_entry_at(s, br, c0 + qd, om, wide, tn, valid_node);
-      const bool enter = valid_node & (force | (h & (tn <= maxd)));  // bitwise: no branch
+      const bool h = node_entry(s, r, om, tn);
+      const bool enter = (r.lox <= r.hix) & (force | (h & (tn <= maxd)));  // bitwise: no branch
       const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);
