@@ -432,8 +432,15 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
       }
     }
     __syncthreads();
-    if (lane == 0) {
+    if (lane == 0) {  // 8 LDS reads in flight ahead of the 32 dependent adds they feed
       int i = 0;
+      for (; i + 32 <= m; i += 32) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = s_f4[(i >> 2) + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { total += v[j].x; total += v[j].y; total += v[j].z; total += v[j].w; }
+      }
       for (; i + 4 <= m; i += 4) {
         const float4 v = s_f4[i >> 2];
         total += v.x; total += v.y; total += v.z; total += v.w;

@@ -948,36 +948,48 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
         const float lim = maxd * 1.00001f + 1e-6f;
         const uint32_t klim = near_key(__float_as_uint(lim));
         const uint4 se = make_uint4(st[0], st[1], st[2], st[3]);
-        auto walk = [&](uint32_t b, uint32_t e, auto test) {
-          for (uint32_t k = b; k < e && !blocked; ++k) {
-            const uint2 en = sc.cell_ent[k];
-            if (near_key(en.y) > klim) break;             // this and every later entry lie beyond the segment
-            if (EX) ++ne;
-            if (__uint_as_float(en.y) > lim) continue;    // the collider lies beyond the segment
-            blocked = test(en.x & 0x0fffffffu);
+        // two entries per step: both records are fetched before either is tested (two dependent
+        // fetch chains in flight per lane instead of one)
+        auto walk = [&](uint32_t b, uint32_t e, auto load, auto test) {
+          for (uint32_t k = b; k < e && !blocked; k += 2) {
+            const uint2 e0 = sc.cell_ent[k];
+            const bool has1 = k + 1 < e;
+            const uint2 e1 = sc.cell_ent[has1 ? k + 1 : k];
+            if (near_key(e0.y) > klim) break;             // this and every later entry lie beyond the segment
+            const bool use1 = has1 && near_key(e1.y) <= klim;
+            const auto r0 = load(e0.x & 0x0fffffffu);
+            const auto r1 = load((use1 ? e1.x : e0.x) & 0x0fffffffu);
+            if (EX) ne += use1 ? 2u : 1u;
+            if (!(__uint_as_float(e0.y) > lim) && test(r0)) { blocked = true; break; }
+            if (!use1) break;
+            if (!(__uint_as_float(e1.y) > lim) && test(r1)) { blocked = true; break; }
           }
         };
-        walk(se.x, se.y, [&](uint32_t idx) {
-          const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
-          SphereRec r;
-          r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
-          ++nt[0];
-          float d;
-          return sphere_hit_dist(s, r, d) && d < maxd;
-        });
-        walk(se.y, se.z, [&](uint32_t idx) {
-          const AabbRec r = sc.aabb[idx];
-          ++nt[1];
-          float d;
-          return aabb_test<false>(s, r, d) && d < maxd;
-        });
+        walk(se.x, se.y,
+             [&](uint32_t idx) {
+               const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
+               SphereRec r;
+               r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
+               return r;
+             },
+             [&](const SphereRec& r) {
+               ++nt[0];
+               float d;
+               return sphere_hit_dist(s, r, d) && d < maxd;
+             });
+        walk(se.y, se.z, [&](uint32_t idx) { return sc.aabb[idx]; },
+             [&](const AabbRec& r) {
+               ++nt[1];
+               float d;
+               return aabb_test<false>(s, r, d) && d < maxd;
+             });
         if (OBB)
-          walk(se.z, se.w, [&](uint32_t idx) {
-            const ObbRec r = sc.obb[idx];
-            ++nt[2];
-            float d;
-            return obb_test<false>(s, r, stored_q(r), d) && d < maxd;
-          });
+          walk(se.z, se.w, [&](uint32_t idx) { return sc.obb[idx]; },
+               [&](const ObbRec& r) {
+                 ++nt[2];
+                 float d;
+                 return obb_test<false>(s, r, stored_q(r), d) && d < maxd;
+               });
       } else {
         if (EX) ++nfb;
         blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
