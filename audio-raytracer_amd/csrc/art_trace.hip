@@ -1087,10 +1087,12 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, B_, true, true); else ART_VIS(S_, BLOCKS_, B_, true, false); } \
     else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true); else ART_VIS(S_, BLOCKS_, B_, false, false); }       \
   } while (0)
-  // The echo traversal (latency-bound) needs only the path kernel's pairs, so it runs on the side
-  // stream: in multi-hit frames each bounce's echoes right after that bounce's path kernel, beside
-  // the next bounces' nearest traversals (their tails leave CUs idle); in one-hit frames beside the
-  // muffle kernel. Without a side stream it runs on st.
+  // The echo traversal needs only the path kernel's pairs: in multi-hit frames each bounce's echoes
+  // run on the side stream right after that bounce's path kernel, beside the next bounces' nearest
+  // traversals (their tails leave CUs idle), and the muffle kernel follows the last bounce on st;
+  // in one-hit frames the echo traversal follows the path kernel on st (it is the longer of the
+  // two, and a fork costs ~10 us before the side stream starts) while the muffle kernel runs on
+  // the side stream. Without a side stream both run on st.
   const bool split = echo.st != nullptr;
   const bool per_bounce = split && multi && ecnt;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
@@ -1112,21 +1114,29 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
       ART_VIS_ANY(echo.st, groups, k);
     }
   }
-  if (!per_bounce) {
-    if (split) {
-      (void)hipEventRecord(echo.fork, st);
-      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-      ART_VIS_ANY(echo.st, eb, -1);
-    } else {
-      ART_VIS_ANY(st, eb, -1);
-    }
-  }
   const unsigned mblocks = (unsigned)((hcap + 255) / 256);  // hit records: at most one per ray and bounce
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
-#define ART_MUFFLE(EX_, OBB_) \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_>), dim3(mblocks, mt), dim3(256), 0, st, sc, fp, pb.vp, pair_count, muffle_acc)
-  if (fp.exec) { if (obb) ART_MUFFLE(true, true); else ART_MUFFLE(true, false); }
-  else { if (obb) ART_MUFFLE(false, true); else ART_MUFFLE(false, false); }
+#define ART_MUFFLE(S_, EX_, OBB_) \
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, muffle_acc)
+#define ART_MUFFLE_ANY(S_)                                                                           \
+  do {                                                                                               \
+    if (fp.exec) { if (obb) ART_MUFFLE(S_, true, true); else ART_MUFFLE(S_, true, false); }         \
+    else { if (obb) ART_MUFFLE(S_, false, true); else ART_MUFFLE(S_, false, false); }               \
+  } while (0)
+  if (per_bounce) {
+    ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
+  } else if (split) {
+    // one-hit frames: the echo traversal (the longer one) follows the path kernel on st with no
+    // fork latency; the muffle kernel goes to the side stream
+    (void)hipEventRecord(echo.fork, st);
+    (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+    ART_MUFFLE_ANY(echo.st);
+    ART_VIS_ANY(st, eb, -1);
+  } else {
+    ART_VIS_ANY(st, eb, -1);
+    ART_MUFFLE_ANY(st);
+  }
+#undef ART_MUFFLE_ANY
 #undef ART_MUFFLE
 #undef ART_VIS_ANY
 #undef ART_VIS
