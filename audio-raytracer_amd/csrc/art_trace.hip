@@ -502,7 +502,7 @@ template <bool HITS, bool MULTI>
 __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu(4))) void path_kernel(
     DevScene sc, FrameParams fp, FanLayout L, const float* __restrict__ origins, uint8_t* __restrict__ block,
     const int* __restrict__ ray_order, VisPairs vp, uint32_t* __restrict__ pair_count,
-    const int2* __restrict__ pre_hits, float4* __restrict__ state, int step) {
+    const int2* __restrict__ pre_hits, float4* __restrict__ state, int step, int emit_echo) {
   constexpr int K = kPathWaves;
   __shared__ uint32_t s_agg[2][K][2];
   __shared__ uint32_t s_aggb[2][2];
@@ -620,8 +620,8 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       const unsigned long long me = __ballot(live_slot), mr = __ballot(hit);
       exec_add(fp.exec, kExecEchoPairs, (unsigned long long)__popcll(me));
       uint32_t eb, rb;
-      reserve((uint32_t)__popcll(me), (uint32_t)__popcll(mr), pair_count, eb, rb);
-      if (live_slot) {
+      reserve(emit_echo ? (uint32_t)__popcll(me) : 0u, (uint32_t)__popcll(mr), pair_count, eb, rb);
+      if (emit_echo && live_slot) {
         const uint32_t at = eb + (uint32_t)__popcll(me & lt);
         const vec3 qdir = normalize(O - off);
         vp.seg[2 * (size_t)at] = make_float4(off.x, off.y, off.z, dist0);
@@ -635,7 +635,8 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       }
     }
     // a blocked echo leaves the reset value (:76); the echo traversal overwrites the visible ones
-    if (live_slot && single_slot) echo[ray * H + k] = 0;
+    // (or, tracing from the hits (!emit_echo), writes both itself)
+    if (emit_echo && live_slot && single_slot) echo[ray * H + k] = 0;
 
     // termination / reflection — :179-193, ReflectRay :456-532
     if (!MULTI) {
@@ -730,31 +731,83 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
 // blocked (wave-uniform mask), which ends every traversal of that segment. Any-hit is an OR over
 // the subtrees, so the split does not change a verdict.
 // ------------------------------------------------------------------------------------------
-template <bool OBB>
+// One-hit frames with one batch slot (H == 1, TC == 1) trace the echo rays straight from the
+// nearest hits (HM: `blk` = a 64-ray group), so the traversal does not wait for the path kernel:
+// the segment, its output index and value are the path kernel's own expressions (:111, :124-145,
+// the zero-distance re-evaluation included), and the traversal stores the echo half or, when a
+// collider blocks it, the reset value 0 (the path kernel, running beside it, then leaves those
+// slots alone). With H == 1 no later batch resets a ray's slot, so every hit slot is live.
+struct EchoFromHits {
+  FrameParams fp;
+  FanLayout L;
+  const float* origins;
+  const int* ray_order;
+  const int2* pre;
+};
+__device__ __forceinline__ bool echo_seg_from_hit(const DevScene& sc, const EchoFromHits& eh, uint32_t g, int r, Seg& s,
+                                                  float& maxd, uint32_t& out_at, uint16_t& out_val) {
+  const FrameParams& fp = eh.fp;
+  const int nrb = (fp.R + 63) >> 6;
+  const int fan = (int)(g / (uint32_t)nrb);
+  const int slot = (int)(g - (uint32_t)fan * nrb) * 64 + r;
+  if (fan >= fp.S || slot >= fp.R) return false;
+  const int2 ph = eh.pre[(size_t)g * 64 + r];
+  if (ph.y == kNoHit) return false;  // a miss: no echo ray (the path kernel resets the slot)
+  const int ray = eh.ray_order[slot];
+  const vec3 O = load3(eh.origins, fan);
+  const vec3 d = load_dir(sc.dirs, ray);
+  const Seg s0 = make_seg(O, d);
+  const int rank = ph.y >> 28, idx = ph.y & 0x0fffffff;
+  const int type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
+  float dist = __int_as_float(ph.x);
+  if (dist == 0.0f) {  // as path_kernel
+    if (type == kSphere) sphere_hit_dist(s0, sc.sph[idx], dist);
+    if (type == kAabb) aabb_test<true>(s0, sc.aabb[idx], dist);
+    if (type == kObb) { const ObbRec rr = sc.obb[idx]; obb_test<true>(s0, rr, stored_q(rr), dist); }
+  }
+  const vec3 o = O + d * dist;                   // :111
+  const vec3 off = o - d * kEps;                 // :124
+  const float dist0 = distance(O, o);            // :130
+  s = make_seg(off, normalize(O - off));
+  maxd = dist0;
+  out_at = (uint32_t)(((size_t)fan * eh.L.stride + eh.L.echo_off) / 2) + (uint32_t)ray;  // ray * H + 0
+  out_val = (uint16_t)f32tof16(dist0 * echo_of(sc, type, idx));   // :142-144
+  return true;
+}
+
+template <bool OBB, bool HM>
 __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
                                               unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
-                                              const uint32_t* ecnt, int bounce, uint8_t* block) {
+                                              const uint32_t* ecnt, int bounce, uint8_t* block, const EchoFromHits& eh) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
   const int wq = lane >> 2, slot = w * 16 + wq;                // segment of the block's 64-pair batch
-  // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
-  uint32_t start = 0u, n;
-  if (bounce < 0) {
-    n = ldc(count, 0);
-  } else {
-    for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
-    n = start + ldc(ecnt, bounce);
-  }
-  const uint32_t base = start + blk * 64u;
-  if (sc.bvh_levels == 0) return;                              // no colliders: nothing blocks
-  if (base + (uint32_t)(w * 16) >= n) return;                  // this wave's 16 segments are past the emitted pairs
-  const bool valid = base + (uint32_t)slot < n;
-  const uint32_t p = valid ? base + (uint32_t)slot : base;
+  if (sc.bvh_levels == 0 && !HM) return;                       // no colliders: nothing blocks
+  bool valid;
+  uint32_t p = 0u, out_at = 0u;
+  uint16_t out_val = 0;
   Seg s;
   float maxd = 0.0f;
   int owner = kNoOwner;
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
   s.a2 = 0.0f;
-  if (valid) load_pair_seg(vp, p, s, maxd, owner);
+  if (HM) {
+    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val);
+    if (!__any(valid)) return;
+  } else {
+    // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
+    uint32_t start = 0u, n;
+    if (bounce < 0) {
+      n = ldc(count, 0);
+    } else {
+      for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
+      n = start + ldc(ecnt, bounce);
+    }
+    const uint32_t base = start + blk * 64u;
+    if (base + (uint32_t)(w * 16) >= n) return;                // this wave's 16 segments are past the emitted pairs
+    valid = base + (uint32_t)slot < n;
+    p = valid ? base + (uint32_t)slot : base;
+    if (valid) load_pair_seg(vp, p, s, maxd, owner);
+  }
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
@@ -839,7 +892,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   if (qd == 0 && valid) diag_add(3, nsteps);
   if (lane == 0) diag_add(1, clock64() - t0);
 #endif
-  if (valid && !((wblocked >> wq) & 1u) && qd == 0) {  // visible: the echo is stored (:142-144)
+  const bool visible = !((wblocked >> wq) & 1u);
+  if (HM) {
+    if (valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = visible ? out_val : (uint16_t)0;  // :76, :142-144
+  } else if (valid && visible && qd == 0) {  // visible: the echo is stored (:142-144)
     const uint2 o = vp.out[p];
     reinterpret_cast<uint16_t*>(block)[o.x] = (uint16_t)(o.y & 0xffffu);
   }
@@ -853,12 +909,12 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 
 // The echo traversal: one 64-pair batch per workgroup. EX: count the executed tests (fp.exec);
 // without it the counters compile out. 8 waves per SIMD.
-template <bool EX, bool OBB>
+template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, unsigned long long* ex,
-                const uint32_t* __restrict__ ecnt, int bounce, uint8_t* __restrict__ block) {
+                const uint32_t* __restrict__ ecnt, int bounce, uint8_t* __restrict__ block, EchoFromHits eh) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
-  vis_quad_body<OBB>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, ecnt, bounce, block);
+  vis_quad_body<OBB, HM>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, ecnt, bounce, block, eh);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1079,41 +1135,28 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const size_t hcap = (size_t)fp.S * fp.R * fp.H;
   uint32_t* ecnt = pb.state ? reinterpret_cast<uint32_t*>(pb.state + 2 * (size_t)groups * 64) + (size_t)groups * 64 + kLiveCounters
                             : nullptr;  // per-bounce echo counts (echo_counts)
-#define ART_VIS(S_, BLOCKS_, B_, EX_, OBB_)                                                                     \
-  hipLaunchKernelGGL((vis_kernel<EX_, OBB_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, \
-                     EX_ ? fp.exec : nullptr, ecnt, B_, block)
-#define ART_VIS_ANY(S_, BLOCKS_, B_)                                                                              \
-  do {                                                                                                           \
-    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, B_, true, true); else ART_VIS(S_, BLOCKS_, B_, true, false); } \
-    else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true); else ART_VIS(S_, BLOCKS_, B_, false, false); }       \
-  } while (0)
-  // The echo traversal needs only the path kernel's pairs: in multi-hit frames each bounce's echoes
-  // run on the side stream right after that bounce's path kernel, beside the next bounces' nearest
-  // traversals (their tails leave CUs idle), and the muffle kernel follows the last bounce on st;
-  // in one-hit frames the echo traversal follows the path kernel on st (it is the longer of the
-  // two, and a fork costs ~10 us before the side stream starts) while the muffle kernel runs on
-  // the side stream. Without a side stream both run on st.
+  // One-hit frames with one batch slot trace the echo rays straight from the nearest hits (HM)
+  // when the frame's echo traversal fits the chip in one round of waves (4 per 64-ray group, 8 per
+  // SIMD): a larger one would hold every wave slot and starve the path kernel beside it (config 4:
+  // path 30 -> 977 us).
   const bool split = echo.st != nullptr;
-  const bool per_bounce = split && multi && ecnt;
-  for (int k = 0; k < (multi ? fp.H : 1); ++k) {
-#define ART_NEAREST(EX_, OBB_)                                                                                      \
-  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
-                     pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr)
-    if (fp.exec) { if (obb) ART_NEAREST(true, true); else ART_NEAREST(true, false); }
-    else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
-#undef ART_NEAREST
-#define ART_PATH(H_, M_)                                                                                              \
-  hipLaunchKernelGGL((path_kernel<H_, M_>), dim3(path_blocks), dim3(64 * kPathWaves), 0, st, sc, fp, L, origins, block, \
-                     ray_order, pb.vp, pair_count, pb.pre, pb.state, k)
-    if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
-    else { if (multi) ART_PATH(false, true); else ART_PATH(false, false); }
-#undef ART_PATH
-    if (per_bounce) {  // this bounce's echoes (at most one per ray slot: `groups` batches)
-      (void)hipEventRecord(echo.fork, st);
-      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-      ART_VIS_ANY(echo.st, groups, k);
-    }
-  }
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  const bool hm = split && !multi && fp.TC == 1 && groups <= (unsigned)cus * 8u;
+  EchoFromHits eh;
+  eh.fp = fp; eh.L = L; eh.origins = origins; eh.ray_order = ray_order; eh.pre = pb.pre;
+#define ART_VIS(S_, BLOCKS_, B_, EX_, OBB_, HM_)                                                                   \
+  hipLaunchKernelGGL((vis_kernel<EX_, OBB_, HM_>), dim3((unsigned)(BLOCKS_)), dim3(256), 0, S_, sc, pb.vp, pair_count, \
+                     EX_ ? fp.exec : nullptr, ecnt, B_, block, eh)
+#define ART_VIS_ANY(S_, BLOCKS_, B_, HM_)                                                                              \
+  do {                                                                                                                \
+    if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, B_, true, true, HM_); else ART_VIS(S_, BLOCKS_, B_, true, false, HM_); } \
+    else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true, HM_); else ART_VIS(S_, BLOCKS_, B_, false, false, HM_); }       \
+  } while (0)
   const unsigned mblocks = (unsigned)((hcap + 255) / 256);  // hit records: at most one per ray and bounce
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
 #define ART_MUFFLE(S_, EX_, OBB_) \
@@ -1123,17 +1166,51 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (fp.exec) { if (obb) ART_MUFFLE(S_, true, true); else ART_MUFFLE(S_, true, false); }         \
     else { if (obb) ART_MUFFLE(S_, false, true); else ART_MUFFLE(S_, false, false); }               \
   } while (0)
+  // Stream plan. Multi-hit frames: per bounce nearest → path on st, that bounce's echo traversal
+  // on the side stream right after its path kernel (beside the next bounces' nearest traversals,
+  // whose tails leave CUs idle), the muffle kernel after the last bounce on st. One-hit frames
+  // with one batch slot (HM): nearest → echo traversal from the hits on st, path → muffle on the
+  // side stream (the path kernel leaves the critical path). Other one-hit frames: nearest → path →
+  // echo traversal on st, the muffle kernel on the side stream (the longer kernel stays on st: a
+  // fork costs ~10 us before the side stream starts). Without a side stream everything runs on st.
+  const bool per_bounce = split && multi && ecnt;
+  for (int k = 0; k < (multi ? fp.H : 1); ++k) {
+#define ART_NEAREST(EX_, OBB_)                                                                                      \
+  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
+                     pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr)
+    if (fp.exec) { if (obb) ART_NEAREST(true, true); else ART_NEAREST(true, false); }
+    else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
+#undef ART_NEAREST
+    hipStream_t pst = st;
+    if (hm) {
+      (void)hipEventRecord(echo.fork, st);
+      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+      pst = echo.st;
+    }
+#define ART_PATH(H_, M_)                                                                                              \
+  hipLaunchKernelGGL((path_kernel<H_, M_>), dim3(path_blocks), dim3(64 * kPathWaves), 0, pst, sc, fp, L, origins, block, \
+                     ray_order, pb.vp, pair_count, pb.pre, pb.state, k, (int)!hm)
+    if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
+    else { if (multi) ART_PATH(false, true); else ART_PATH(false, false); }
+#undef ART_PATH
+    if (per_bounce) {  // this bounce's echoes (at most one per ray slot: `groups` batches)
+      (void)hipEventRecord(echo.fork, st);
+      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+      ART_VIS_ANY(echo.st, groups, k, false);
+    }
+  }
   if (per_bounce) {
     ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
+  } else if (hm) {
+    ART_MUFFLE_ANY(echo.st);           // after the path kernel there
+    ART_VIS_ANY(st, groups, -1, true);  // one 64-ray group per workgroup
   } else if (split) {
-    // one-hit frames: the echo traversal (the longer one) follows the path kernel on st with no
-    // fork latency; the muffle kernel goes to the side stream
     (void)hipEventRecord(echo.fork, st);
     (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
     ART_MUFFLE_ANY(echo.st);
-    ART_VIS_ANY(st, eb, -1);
+    ART_VIS_ANY(st, eb, -1, false);
   } else {
-    ART_VIS_ANY(st, eb, -1);
+    ART_VIS_ANY(st, eb, -1, false);
     ART_MUFFLE_ANY(st);
   }
 #undef ART_MUFFLE_ANY
