@@ -221,6 +221,16 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #define ART_NEAREST_STEAL 1
 #endif
 constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
+
+// Waves per SIMD of the traversal kernels: 8 (64 VGPRs). Register spills inside the divergent
+// traversal loops hung a fused kernel once, so the counting instantiations and
+// the echo traversal's OBB one run at the occupancy that holds them without spills; the nearest
+// traversal's OBB instantiation keeps 8 waves and 5 spilled VGPRs (at 7 waves config 3's nearest
+// kernel took 300 instead of 243 us), covered by the full-size OBB parity tests.
+template <bool EX, bool OBB>
+constexpr int kNearestWaves = EX ? 6 : 8;
+template <bool EX, bool OBB>
+constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
 // k-th (0-based) set bit of m, k < popcount(m).
 __device__ __forceinline__ int select_bit(unsigned long long m, int k) {
   int pos = 0;
@@ -399,7 +409,7 @@ __device__ __forceinline__ uint32_t* echo_counts(float4* state, int ngroups) {
 
 // EX: count the executed tests (fp.exec); OBB: the scene has OBBs.
 template <bool EX, bool OBB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void nearest_first_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWaves<EX, OBB>))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
     uint32_t* __restrict__ counters) {
@@ -910,7 +920,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 // The echo traversal: one 64-pair batch per workgroup. EX: count the executed tests (fp.exec);
 // without it the counters compile out. 8 waves per SIMD.
 template <bool EX, bool OBB, bool HM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEchoWaves<EX, OBB>)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, unsigned long long* ex,
                 const uint32_t* __restrict__ ecnt, int bounce, uint8_t* __restrict__ block, EchoFromHits eh) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
