@@ -6,6 +6,8 @@ DSP parameters, RayHitResults / RayHitResultCounts. Floating-point outputs are r
 bit-identical (tolerance 0 ULP), which is stricter than north_star's 1e-5 absolute bound.
 Test counts (the tests/s metric's numerator) must equal the oracle's per-kind counts.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -421,3 +423,37 @@ def test_graph_replay_equals_direct_launches(ctx):
             got = art.unpack_block(d_blk.cpu().numpy(), lay, 12, 128, cfg.H, cfg.T, 1, hits=True, dsp=True)
             assert all(got.equal(ref).values()), (life, flags, got.equal(ref))
     ctx.set_flags(0)
+
+
+_LANES_SCRIPT = r"""
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import numpy as np
+import art
+import oracle
+ctx = art.Context(1)
+for ci, S, R, scale in ((2, 24, 256, 0.25), (5, 16, 128, 0.2), (3, 20, 128, 0.25)):
+    cfg = art.CONFIGS[ci]
+    scene, org, params = art.synth(cfg, S=S, R=R, C_scale=scale)
+    out = art.FanOutputs(S, R, cfg.H, cfg.T, 1, hits=True, dsp=params.dsp is not None)
+    ref = out.copy()
+    ctx.run(art.Frame(scene, params, org, out))
+    oracle.run_frame(art.Frame(scene, params, org, ref), threads=8)
+    eq = out.equal(ref)
+    assert all(eq.values()), (ci, eq)
+print("lanes ok")
+"""
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_fan_lanes_equal_oracle(lanes):
+    """ART_FAN_LANES > 1 (read once per process, so in a child process): a frame's fans split over
+    concurrent streams, each with its own echo side stream, pair buffer and counters; one-hit
+    (configs 2, 3) and multi-hit (config 5) frames byte-equal to the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ART_FAN_LANES=str(lanes))
+    r = subprocess.run([sys.executable, "-c", _LANES_SCRIPT, os.path.join(root, "audio-raytracer_amd"),
+                        os.path.join(root, "tests")], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "lanes ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
