@@ -212,6 +212,9 @@ struct art_ctx {
   } kinds[3];
   int synced[3] = {0, 0, 0};
   bool store_synced = false;
+  // the synced records the resident scene's muffle cell lists were built from (cell_still_valid)
+  std::vector<uint8_t> cell_base[3];
+  bool cell_base_ok = false;
   uint64_t sync_gen = 0;         // bumped by every art_colliders_sync that changed a record
   // audio_target_id of every synced record and their histogram (index = id + 32768), kept
   // incrementally from the dirty records (permeation loss test counts of counting frames)
@@ -508,6 +511,36 @@ int wait_launch(art_ctx* c, Device& dv) {
 }
 
 // Upload the packed inputs to one device and build its SoA records (async on dv.stream).
+// The resident store's records as the muffle cell lists were just built from them (none dirty).
+void snapshot_cell_base(art_ctx* c) {
+  bool clean = true;
+  for (int k = 0; k < 3; ++k) clean &= c->kinds[k].dirty_list.empty();
+  for (int k = 0; k < 3; ++k) c->cell_base[k] = c->kinds[k].recs;
+  c->cell_base_ok = clean;
+}
+
+// The lists built from record `base` still hold record `now` (cell_slack): same extents and owner,
+// centre moved by at most half the slack of the base's bounding radius.
+bool cell_still_valid(int kind, const uint8_t* now, const uint8_t* base) {
+  const size_t ext = kind == 0 ? 2 : 6;  // radius (half) or size (half3), after the centre
+  const size_t tid_off = kind == 0 ? offsetof(art_sphere, audio_target_id)
+                                   : (kind == 1 ? offsetof(art_aabb, audio_target_id) : offsetof(art_obb, audio_target_id));
+  if (memcmp(now + 6, base + 6, ext) != 0 || memcmp(now + tid_off, base + tid_off, 2) != 0) return false;
+  uint16_t cn[3], cb[3], e[3] = {0, 0, 0};
+  memcpy(cn, now, 6);
+  memcpy(cb, base, 6);
+  memcpy(e, base + 6, ext);
+  float d2 = 0.0f, r2 = 0.0f;
+  for (int a = 0; a < 3; ++a) {
+    const float dd = art::f16tof32(cn[a]) - art::f16tof32(cb[a]);
+    d2 += dd * dd;
+    const float ea = art::f16tof32(e[a]);
+    r2 += ea * ea;
+  }
+  const float half = 0.5f * art::cell_slack(std::sqrt(r2)) * 0.999f;
+  return std::isfinite(d2) && std::isfinite(r2) && d2 <= half * half;
+}
+
 int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   HIP_TRY(c, hipSetDevice(dv.id));
   if (int rc = wait_launch(c, dv)) return rc;
@@ -598,6 +631,8 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.geo = soa + f.soa_cgeo;
     if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
     dv.sorted_sc = sc;
+    if (f.resident) snapshot_cell_base(c);  // the store's synced records (clean unless edited since)
+    else c->cell_base_ok = false;
   }
   HIP_TRY(c, hipGetLastError());
   if (!f.resident) {
@@ -1529,6 +1564,18 @@ ART_API int art_colliders_sync(art_ctx* c) {
   }
   const int nd = (int)(lists[0].size() + lists[1].size() + lists[2].size());
   if (nd || counts_changed) ++c->sync_gen;  // resident frames refit / rebuild their sorted copies
+  // the muffle cell lists need a rebuild unless every changed collider stayed within their slack
+  bool cells_ok = c->cell_base_ok && !counts_changed && !fresh;
+  for (int k = 0; cells_ok && k < 3; ++k) {
+    const size_t rs = kRecSize[k];
+    if (c->cell_base[k].size() < (size_t)n[k] * rs) { cells_ok = false; break; }
+    for (int i : lists[k])
+      if (!cell_still_valid(k, c->kinds[k].recs.data() + (size_t)i * rs, c->cell_base[k].data() + (size_t)i * rs)) {
+        cells_ok = false;
+        break;
+      }
+  }
+  bool cells_rebuilt = false;
   for (Device& dv : c->devs) {  // the previous sync's copy may still read the pinned staging
     if (dv.st_pending) {
       HIP_TRY(c, hipSetDevice(dv.id));
@@ -1615,7 +1662,10 @@ ART_API int art_colliders_sync(art_ctx* c) {
         // moved colliders: refit the sorted copies and the BVH in place (device only, no H2D)
         if (nd) {
           if (launch_refit_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider refit failed");
-          if (launch_build_cells(dv.sc, dv.cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
+          if (!cells_ok) {
+            if (launch_build_cells(dv.sc, dv.cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
+            cells_rebuilt = true;
+          }
           if (dv.sorted_gen != ~0ull) dv.sorted_gen = c->sync_gen;
           HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));  // device-path launches wait for the sort too
         }
@@ -1647,6 +1697,8 @@ ART_API int art_colliders_sync(art_ctx* c) {
       hist[(size_t)(v + 32768)]++;
     }
   }
+  if (cells_rebuilt) snapshot_cell_base(c);
+  else if (!cells_ok) c->cell_base_ok = false;  // the lists (rebuilt at the next bind) no longer hold these records
   if (c->cpu)  // the CPU backend reads the synced snapshot (JobBatch) of each list
     for (int k = 0; k < 3; ++k) c->cpu_recs[k].assign(c->kinds[k].recs.begin(), c->kinds[k].recs.begin() + (size_t)n[k] * kRecSize[k]);
   c->store_synced = true;

@@ -31,6 +31,7 @@ namespace art {
 
 constexpr float kCellEta = 2e-6f;  // relative deviation of a float muffle ray from its exact segment
 
+
 // far_t: the largest distance from target t to the scene's bounds (every muffle segment of t
 // starts on a collider, so maxd <= far_t; muffle_kernel tests a longer segment against every
 // collider).
@@ -137,7 +138,8 @@ __global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb
     widen = 1.7321f;  // a box widened by m per axis: its half-diagonal grows by sqrt(3) m
   }
   const float m = cr.factor * (far + r + h1 + 1.0f);
-  const float rho = r + widen * m + 2.0f * (kCellEta * far + 1e-6f) + 1e-6f * (fabsf(cc0.x) + fabsf(cc0.y) + fabsf(cc0.z));
+  const float rho = r + widen * m + 2.0f * (kCellEta * far + 1e-6f) + 1e-6f * (fabsf(cc0.x) + fabsf(cc0.y) + fabsf(cc0.z)) +
+                    cell_slack(r);
   const vec3 w = mk3(cc0.x - tg.x, cc0.y - tg.y, cc0.z - tg.z);
   const float D = sqrtf(w.x * w.x + w.y * w.y + w.z * w.z);
   const bool all = !(D > rho * 1.0001f) || !isfinite(D) || !isfinite(rho);  // the sphere holds the target

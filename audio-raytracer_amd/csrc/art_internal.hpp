@@ -101,6 +101,17 @@ struct DevScene {
   const uint32_t* cell_ok;        // [T]
   uint32_t cell_cap;
 };
+// Motion slack of a listed collider (bounding radius r): the cell lists are built for its bounding
+// sphere grown by this much, so they stay valid while the collider keeps its extents and owner and
+// its centre stays within half of it of where the lists were built; art_colliders_sync then refits
+// the BVH and skips the list rebuild. Units are scene units (Unity metres).
+#ifndef ART_CELL_SLACK_REL
+#define ART_CELL_SLACK_REL 0.25f
+#endif
+#ifndef ART_CELL_SLACK_ABS
+#define ART_CELL_SLACK_ABS 0.25f
+#endif
+__host__ __device__ inline float cell_slack(float r) { return ART_CELL_SLACK_REL * r + ART_CELL_SLACK_ABS; }
 constexpr int kCellG = 32;                   // cells per cube-face axis
 constexpr int kCells = 6 * kCellG * kCellG;  // cells per target
 // Cell cone (host table, art_capi.cpp): unit axis and cos / sin of the half-angle plus slack.

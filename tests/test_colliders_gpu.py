@@ -331,3 +331,74 @@ def test_errors_and_state(fresh_ctx):
     assert store.get(abi.ART_KIND_AABB, 0).tobytes() == np.asarray(rec).tobytes()
     store.clear()
     assert [store.count(k) for k in KINDS] == [0, 0, 0]
+
+
+def _jitter(recs, rng, scale):
+    out = recs.copy()
+    c = out["center"].view(np.float16).astype(np.float32)
+    c += rng.uniform(-scale, scale, c.shape).astype(np.float32)
+    out["center"] = c.astype(np.float16).view(np.uint16).reshape(out["center"].shape)
+    return out
+
+
+@pytest.mark.parametrize("ci", [2, 5])
+def test_small_moves_keep_cell_lists(fresh_ctx, ci):
+    """Syncs whose moved colliders stay within the cell lists' motion slack (cell_slack) refit the
+    BVH but keep the muffle cell lists; larger moves and size changes rebuild them. Every round's
+    device frame must equal a fresh bind of the same colliders byte for byte, and the last round
+    the oracle too."""
+    import torch
+    cfg = art.CONFIGS[ci]
+    scene, org, params = art.synth(cfg, S=8, R=128, C_scale=0.25)
+    store, model = ColliderStore(fresh_ctx), ListsModel()
+    load(store, model, scene)
+    store.sync()
+    model.synced()
+    dev = torch.device("cuda", 0)
+    ref_ctx = art.Context(1)
+    rng = np.random.default_rng(11)
+    try:
+        fr = art.Frame(scene, params, org, art.FanOutputs(8, scene.R, cfg.H, scene.T, params.thread_count,
+                                                          dsp=params.dsp is not None))
+        lay = art.fan_layout(fr)
+        fresh_ctx.set_flags(abi.ART_CTX_RESIDENT_COLLIDERS)
+        fresh_ctx.bind(resident_frame(fr))
+        d_org = torch.from_numpy(np.ascontiguousarray(org)).to(dev)
+        st = torch.cuda.current_stream().cuda_stream
+        # small jitters from the original positions (lists kept), then a large move and a resize
+        for rnd, scale in enumerate((0.05, 0.05, 0.1, 0.05, 2.0, 0.05, "resize", 0.05)):
+            for k, name in KIND_FIELDS.items():
+                src = getattr(scene, name)
+                if src.size == 0:
+                    continue
+                ids = rng.choice(src.size, max(1, src.size // 10), replace=False)
+                if scale == "resize":
+                    recs = src[ids].copy()
+                    if name == "spheres":
+                        recs["radius"] = (recs["radius"].view(np.float16) * np.float16(1.5)).view(np.uint16)
+                    else:
+                        recs["size"] = (recs["size"].view(np.float16) * np.float16(1.5)).view(np.uint16).reshape(
+                            recs["size"].shape)
+                else:
+                    recs = _jitter(src[ids], rng, scale)
+                for j, i in enumerate(ids):
+                    store.set(k, int(i), recs[j])
+                    model.set(k, int(i), recs[j])
+            store.sync()
+            model.synced()
+            blk = torch.zeros(8 * lay["stride"], dtype=torch.uint8, device=dev)
+            fresh_ctx.launch_device(d_org.data_ptr(), 8, blk.data_ptr(), 0, st)
+            torch.cuda.synchronize()
+            ref_ctx.bind(art.Frame(scene_with(scene, model), params, org, fr.out))
+            rblk = torch.zeros_like(blk)
+            ref_ctx.launch_device(d_org.data_ptr(), 8, rblk.data_ptr(), 0, st)
+            torch.cuda.synchronize()
+            assert torch.equal(blk, rblk), (rnd, scale)
+        got = art.unpack_block(blk.cpu().numpy(), lay, 8, scene.R, cfg.H, scene.T, params.thread_count,
+                               dsp=params.dsp is not None)
+        ref = art.FanOutputs(8, scene.R, cfg.H, scene.T, params.thread_count, dsp=params.dsp is not None)
+        oracle.run_frame(art.Frame(scene_with(scene, model), params, org, ref), threads=8)
+        assert all(got.equal(ref).values())
+    finally:
+        fresh_ctx.set_flags(0)
+        ref_ctx.close()
