@@ -106,10 +106,10 @@ struct DevScene {
 // its centre stays within half of it of where the lists were built; art_colliders_sync then refits
 // the BVH and skips the list rebuild. Units are scene units (Unity metres).
 #ifndef ART_CELL_SLACK_REL
-#define ART_CELL_SLACK_REL 0.25f
+#define ART_CELL_SLACK_REL 0.1f
 #endif
 #ifndef ART_CELL_SLACK_ABS
-#define ART_CELL_SLACK_ABS 0.25f
+#define ART_CELL_SLACK_ABS 0.2f
 #endif
 __host__ __device__ inline float cell_slack(float r) { return ART_CELL_SLACK_REL * r + ART_CELL_SLACK_ABS; }
 constexpr int kCellG = 32;                   // cells per cube-face axis
