@@ -121,7 +121,7 @@ class art_collider_sync_stats(C.Structure):
 class art_exec_counts(C.Structure):
     _fields_ = [("sphere", C.c_uint64), ("aabb", C.c_uint64), ("obb", C.c_uint64), ("cull_box", C.c_uint64),
                 ("cell_entries", C.c_uint64), ("launches", C.c_uint64), ("muffle_fallback", C.c_uint64),
-                ("echo_pairs", C.c_uint64)]
+                ("echo_pairs", C.c_uint64), ("bounce_rays", C.c_uint64 * 16)]
 
 
 # include/art_dsp.h

@@ -292,7 +292,9 @@ class Context:
         rc = self.lib.art_executed_counts(self.ptr, C.byref(t))
         if rc:
             self._raise(rc)
-        return {k: int(getattr(t, k)) for k, _ in abi.art_exec_counts._fields_}
+        out = {k: int(getattr(t, k)) for k, ty in abi.art_exec_counts._fields_ if k != "bounce_rays"}
+        out["bounce_rays"] = [int(v) for v in t.bounce_rays]
+        return out
 
     def close(self):
         if getattr(self, "ptr", None):

@@ -45,7 +45,7 @@ static_assert(sizeof(art_dsp_params) == 24, "art_dsp_params");
 
 namespace {
 
-constexpr uint32_t kAbiVersion = (2u << 16) | 1u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1: art_exec_counts.cell_entries / muffle_fallback, ART_CTX_GRAPH
+constexpr uint32_t kAbiVersion = (2u << 16) | 2u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1: art_exec_counts.cell_entries / muffle_fallback, ART_CTX_GRAPH; 2.2: art_exec_counts.bounce_rays
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
@@ -753,8 +753,8 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.TC, f.L.stride);
   if (fast) {
     if ((c->flags & ART_CTX_COUNT_EXECUTED) && !dv.exec.p) {
-      if (!dv.exec.reserve(64)) return fail(c, ART_E_NOMEM, "device allocation failed");
-      HIP_TRY(c, hipMemsetAsync(dv.exec.p, 0, 64, st));
+      if (!dv.exec.reserve(8 * kExecSlots)) return fail(c, ART_E_NOMEM, "device allocation failed");
+      HIP_TRY(c, hipMemsetAsync(dv.exec.p, 0, 8 * kExecSlots, st));
     }
     if (!dv.echo.st) {
       HIP_TRY(c, hipStreamCreateWithFlags(&dv.echo.st, hipStreamNonBlocking));
@@ -1398,11 +1398,12 @@ ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
     if (!dv.exec.p) continue;
     HIP_TRY(c, hipSetDevice(dv.id));
     HIP_TRY(c, hipDeviceSynchronize());
-    unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long v[kExecSlots] = {};
     HIP_TRY(c, hipMemcpy(v, dv.exec.p, sizeof v, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemset(dv.exec.p, 0, 64));
-    out->sphere += v[0]; out->aabb += v[1]; out->obb += v[2]; out->cull_box += v[3]; out->cell_entries += v[4];
-    out->muffle_fallback += v[5]; out->echo_pairs += v[6];
+    HIP_TRY(c, hipMemset(dv.exec.p, 0, sizeof v));
+    out->sphere += v[kExecSphere]; out->aabb += v[kExecAabb]; out->obb += v[kExecObb]; out->cull_box += v[kExecCullBox];
+    out->cell_entries += v[kExecCellEntries]; out->muffle_fallback += v[kExecMuffleFallback]; out->echo_pairs += v[kExecEchoPairs];
+    for (int k = 0; k < kExecBounces; ++k) out->bounce_rays[k] += v[kExecBounce0 + k];
     out->launches += dv.exec_launches;
     dv.exec_launches = 0;
   }

@@ -200,7 +200,7 @@ struct FrameParams {
 
 // Slots of FrameParams::exec (art_exec_counts order).
 enum ExecSlot { kExecSphere = 0, kExecAabb = 1, kExecObb = 2, kExecCullBox = 3, kExecCellEntries = 4, kExecMuffleFallback = 5,
-                kExecEchoPairs = 6 };
+                kExecEchoPairs = 6, kExecBounce0 = 8, kExecBounces = 16, kExecSlots = 24 };
 
 // Device counters for the counting variant, in art_test_counts order.
 struct DevCounts { unsigned long long v[9]; };

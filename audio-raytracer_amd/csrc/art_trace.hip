@@ -457,6 +457,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
     write = true;
     out = (uint32_t)g * 64u + (uint32_t)rr;
   }
+  if (EX && step < kExecBounces)  // live rays traced this bounce (one per quad)
+    exec_add(ex, kExecBounce0 + step, (unsigned long long)__popcll(__ballot(alive) & kQuad0));
 #ifdef ART_DIAG
   const unsigned long long t0 = clock64();
 #endif

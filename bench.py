@@ -706,7 +706,9 @@ def main():
                      "single_issue": {"achieved": ex_ops / (rt_ms * 1e-3) / 1e12, "peak": SINGLE_ISSUE_TLOPS,
                                       "unit": "T lane-op/s", "frac": ex_ops / (rt_ms * 1e-3) / 1e12 / SINGLE_ISSUE_TLOPS},
                      "executed": {"ops_per_launch": ex_ops, "exact_lane_tests_per_launch": ex_tests,
-                                  "counts": {k: v // ex_launches for k, v in executed.items() if k != "launches"}},
+                                  "counts": {k: v // ex_launches for k, v in executed.items()
+                                             if k not in ("launches", "bounce_rays")},
+                                  "bounce_rays": [v // ex_launches for v in executed["bounce_rays"][:cfg.H]]},
                      "equivalent": {"achieved": bf_tflops, "frac": bf_tflops / FP32_VALU_PEAK_TFLOPS,
                                     "reference_tests_per_launch": tests_rank,
                                     "note": "brute-force-equivalent: the reference algorithm's tests x ops per test / "

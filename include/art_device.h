@@ -93,6 +93,7 @@ typedef struct {
     uint64_t launches;               /* frames counted */
     uint64_t muffle_fallback;        /* muffle rays tested against every collider (no usable cell list) */
     uint64_t echo_pairs;             /* echo rays left to the BVH echo traversal (not decided by the nearest pass) */
+    uint64_t bounce_rays[16];        /* live rays the nearest traversal traced per bounce (bounce k, k < 16) */
 } art_exec_counts;
 /* Executed-work counters since the last call (needs ART_CTX_COUNT_EXECUTED); synchronizes. */
 ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);
