@@ -196,7 +196,7 @@ int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
-// BVH for per-lane nearest-hit traversal (raytrace_fast_kernel<..., BVH = true>): all colliders in
+// BVH of the quad traversals (art_trace.hip) and the permeation loss rays (art_kernels.hip): all colliders in
 // one Morton order of their bounds' centres (types mixed), kBvhLeaf per leaf, an implicit complete
 // 4-ary tree above. Node bounds are unions of CullRecs with the largest margin scale and factor,
 // so a node's widened box contains every widened member box (broad phase).
