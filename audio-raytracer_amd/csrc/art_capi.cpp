@@ -96,7 +96,7 @@ struct Frame {
          off_reset = 0, off_order = 0, raw_bytes = 0;
   size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_cull = 0, soa_bytes = 0;
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
-  size_t soa_sph_s = 0, soa_aabb_s = 0, soa_obb_s = 0, soa_cull_s = 0, soa_chunks = 0, soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0;
+  size_t soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0, soa_kd = 0;
   // muffle candidate lists (art_cells.hip)
   size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, cells_temp = 0,
          soa_cgeo = 0;
@@ -449,7 +449,6 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
   f.soa_cull = s; s = align_up(s + (sn + an + on) * sizeof(CullRec), 256);
   {  // broad-phase structure (art_bvh.hip)
     const size_t n = (size_t)(f.ns + f.na + f.no);
-    const size_t nch = (size_t)((f.ns + 63) / 64 + (f.na + 63) / 64 + (f.no + 63) / 64);
     f.sort_temp = sort_scene_temp_bytes((int)n);
     f.soa_box = s; s = align_up(s + 6 * sizeof(float), 256);
     f.soa_keys = s; s = align_up(s + n * 4, 256);
@@ -457,14 +456,10 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_vals = s; s = align_up(s + n * 4, 256);
     f.soa_perm = s; s = align_up(s + n * 4, 256);
     f.soa_temp = s; s = align_up(s + f.sort_temp, 256);
-    f.soa_sph_s = s; s = align_up(s + (size_t)f.ns * sizeof(SphereRec), 256);
-    f.soa_aabb_s = s; s = align_up(s + (size_t)f.na * sizeof(AabbRec), 256);
-    f.soa_obb_s = s; s = align_up(s + (size_t)f.no * sizeof(ObbRec), 256);
-    f.soa_cull_s = s; s = align_up(s + n * sizeof(CullRec), 256);
-    f.soa_chunks = s; s = align_up(s + nch * sizeof(CullRec), 256);
     f.soa_bvh = s; s = align_up(s + bvh_node_count((int)n) * sizeof(CullRec), 256);
     f.soa_bvh_ref = s; s = align_up(s + n * 4, 256);
     f.soa_bvh_leaf = s; s = align_up(s + bvh_slot_count((int)n) * 64, 256);
+    f.soa_kd = s; s = align_up(s + kd_scratch_bytes((int)n), 256);
   }
   {  // muffle candidate lists
     const size_t cells = (size_t)f.T * kCells * 3;  // lists per (target, cell, collider type)
@@ -584,13 +579,10 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sb.keys = reinterpret_cast<uint32_t*>(soa + f.soa_keys); sb.keys_s = reinterpret_cast<uint32_t*>(soa + f.soa_keys_s);
   sb.vals = reinterpret_cast<int*>(soa + f.soa_vals); sb.perm = reinterpret_cast<int*>(soa + f.soa_perm);
   sb.temp = soa + f.soa_temp; sb.temp_bytes = f.sort_temp;
-  sb.sph_s = reinterpret_cast<SphereRec*>(soa + f.soa_sph_s); sb.aabb_s = reinterpret_cast<AabbRec*>(soa + f.soa_aabb_s);
-  sb.obb_s = reinterpret_cast<ObbRec*>(soa + f.soa_obb_s); sb.cull_s = reinterpret_cast<CullRec*>(soa + f.soa_cull_s);
-  sb.chunks = reinterpret_cast<CullRec*>(soa + f.soa_chunks);
   sb.bvh = bvh_node_count(f.ns + f.na + f.no) ? reinterpret_cast<CullRec*>(soa + f.soa_bvh) : nullptr;
   sb.bvh_ref = reinterpret_cast<uint32_t*>(soa + f.soa_bvh_ref);
   sb.bvh_leaf = reinterpret_cast<float4*>(soa + f.soa_bvh_leaf);
-  sc.sph_s = nullptr; sc.aabb_s = nullptr; sc.obb_s = nullptr; sc.cull_s = nullptr; sc.chunks = nullptr; sc.nchunks = 0;
+  sb.kd = kd_scratch_bytes(f.ns + f.na + f.no) ? soa + f.soa_kd : nullptr;
   sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
   dv.sb = sb;
   {
@@ -598,8 +590,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
                        dv.sorted_n[1] == f.na && dv.sorted_n[2] == f.no;
     if (reuse) {  // same resident colliders (or only moved ones): keep the orders, refit if needed
       const DevScene& o = dv.sorted_sc;
-      sc.sph_s = o.sph_s; sc.aabb_s = o.aabb_s; sc.obb_s = o.obb_s; sc.cull_s = o.cull_s; sc.chunks = o.chunks;
-      sc.nchunks = o.nchunks; sc.bvh = o.bvh; sc.bvh_ref = o.bvh_ref; sc.bvh_leaf = o.bvh_leaf;
+      sc.bvh = o.bvh; sc.bvh_ref = o.bvh_ref; sc.bvh_leaf = o.bvh_leaf;
       sc.bvh_levels = o.bvh_levels; sc.bvh_leaf0 = o.bvh_leaf0;
       if (dv.sorted_gen != c->sync_gen && launch_refit_scene(sc, sb, dv.stream) != 0)
         return fail(c, ART_E_DEVICE, "collider refit failed");

@@ -70,20 +70,14 @@ struct DevScene {
   const float* targets; int T;    // float3[T]
   const uint16_t* dirs; int R;    // half3[R] as 3 x u16
   const CullRec* cull;            // [ns + na + no]
-  // spatially sorted copies (art_bvh.hip): Morton order within each type; the records' pad field
-  // holds the original in-type index
-  const SphereRec* sph_s; const AabbRec* aabb_s; const ObbRec* obb_s;
-  const CullRec* cull_s;          // [ns + na + no], sorted order
-  const CullRec* chunks;          // [nchunks]: union bounds of 64 sorted colliders of one type
-  int nchunks;
   // BVH over all colliders (art_bvh.hip): a complete 4-ary tree in heap order (root 0, children
-  // of node g at 4g + 1 .. 4g + 4) over the Morton order of the bounds' centres, kBvhLeaf colliders
+  // of node g at 4g + 1 .. 4g + 4) over a spatial order of the bounds' centres, kBvhLeaf colliders
   // per leaf; the leaves are nodes bvh_leaf0 .. bvh_leaf0 + 4^(levels - 1) - 1 (those past the
   // last collider are empty). A node's CullRec is the union of its colliders' bounds with their
   // largest margin scale and factor; an empty node has lo > hi.
   const CullRec* bvh;
-  const uint32_t* bvh_ref;        // [ns + na + no] in Morton order: type rank << 30 | in-type index
-  const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] 64-B slots in Morton order: the
+  const uint32_t* bvh_ref;        // [ns + na + no] in leaf order: type rank << 30 | in-type index
+  const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] 64-B slots in leaf order: the
                                   // hot record's test fields and the global order code (rank << 28 |
                                   // index; -1: empty slot) in the first 32 B (bvh_leaf_kernel)
   int bvh_levels;                 // 0: no BVH
@@ -128,9 +122,9 @@ struct SortBufs {
   float* box;                     // 6 floats
   uint32_t* keys; uint32_t* keys_s; int* vals; int* perm;
   void* temp; size_t temp_bytes;
-  SphereRec* sph_s; AabbRec* aabb_s; ObbRec* obb_s; CullRec* cull_s; CullRec* chunks;
   CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count) and leaf references
   float4* bvh_leaf;                 // leaf slots (bvh_slot_count)
+  void* kd;                         // kd leaf-order scratch (kd_scratch_bytes; NULL: Morton order)
 };
 // per-sample spatializer DSP (art_dsp.hip)
 int dsp_source_params(const art_spatializer_settings& st, const art_audio_source& src, int sample_rate,
@@ -145,6 +139,7 @@ int launch_sort_scene(DevScene& sc, const SortBufs& sb, hipStream_t st);
 // (after launch_sort_scene's buffers are free again; same stream).
 size_t bvh_node_count(int n);
 size_t bvh_slot_count(int n);
+size_t kd_scratch_bytes(int n);
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
 // Colliders moved, counts unchanged: recompute the sorted copies' records, chunk bounds and the
 // BVH's bounds and leaf slots in place, keeping every order.
