@@ -223,31 +223,26 @@ static void launch_bvh_upper(CullRec* nodes, int L, hipStream_t st) {
 // Method: three index arrays, each sorted by one axis of the centres (hipCUB radix sort), stay
 // sorted inside every segment through stable partitions: per binary level, each segment's axis is
 // read off its own sorted array (last - first centre), the side of each collider is its rank on
-// that axis, and every array is stably partitioned by side (one block-wide scan per array). One
-// workgroup, ~6 barriers per level.
+// that axis, and every array is stably partitioned by side. One workgroup holds the three arrays
+// in LDS (u16 ids, 96 KB at the 2^14-collider limit); each thread keeps its chunk's ids in
+// registers (two u16 per VGPR) across the block scan, so the partition scatters in place. 5 barriers
+// per level.
 // ------------------------------------------------------------------------------------------
-constexpr int kKdMaxColliders = 1 << 16;
+constexpr int kKdMaxColliders = 1 << 14;
+constexpr int kKdChunk = kKdMaxColliders / 1024;  // positions per thread
 
 struct KdBufs {
   float4* cen;  // [n] centre (non-finite components -> FLT_MAX)
-  int* p;       // [3][n] index arrays, ping
-  int* q;       // [3][n] pong
-  int* pre;     // [3][n] exclusive prefix of the left flags
-  int* side;    // [n] 1 = left half of its segment on the segment's axis
-  int* axis;    // [n] per segment: split axis, or -1 (the segment fits its left half)
+  int* p;       // [3][n] index arrays sorted by x, y, z
 };
 static KdBufs kd_bufs(void* base, int n) {
   char* b = static_cast<char*>(base);
   KdBufs k;
   k.cen = reinterpret_cast<float4*>(b);
   k.p = reinterpret_cast<int*>(b + 16 * (size_t)n);
-  k.q = k.p + 3 * (size_t)n;
-  k.pre = k.q + 3 * (size_t)n;
-  k.side = k.pre + 3 * (size_t)n;
-  k.axis = k.side + n;
   return k;
 }
-size_t kd_scratch_bytes(int n) { return n > 0 && n <= kKdMaxColliders ? (size_t)n * (16 + 4 * 11) : 0; }
+size_t kd_scratch_bytes(int n) { return n > 0 && n <= kKdMaxColliders ? (size_t)n * (16 + 4 * 3) : 0; }
 
 __global__ void kd_cen_kernel(const CullRec* __restrict__ cull, int n, float4* __restrict__ cen) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -295,60 +290,91 @@ __device__ __forceinline__ void kd_block_scan3(int v[3], int (*s_wave)[16]) {
 }
 
 __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap, int* __restrict__ perm) {
+  __shared__ uint16_t s_p[3][kKdMaxColliders];        // the three index arrays
+  __shared__ uint8_t s_side[kKdMaxColliders];         // 1: left half of its segment (by collider id)
+  __shared__ int8_t s_axis[kKdMaxColliders / 8];      // per segment: split axis, -1 = fits its left half
+  __shared__ uint16_t s_segpre[3][kKdMaxColliders / 8];  // left-flag prefix at each segment's start
   __shared__ int s_wave[3][16];
   const int tid = threadIdx.x;
   const int chunk = (n + 1023) / 1024;
   const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
-  int* p = k.p;
-  int* q = k.q;
-  for (int seg = cap; seg > kBvhLeaf; seg >>= 1) {
-    const int half = seg >> 1, nseg = (n + seg - 1) / seg;
+  for (int x = 0; x < 3; ++x)
+    for (int i = tid; i < n; i += 1024) s_p[x][i] = (uint16_t)k.p[(size_t)x * n + i];
+  __syncthreads();
+  for (int lg = 31 - __builtin_clz(cap); lg > 2; --lg) {  // segments of seg = 2^lg positions (cap: a power of 4)
+    const int seg = 1 << lg, half = seg >> 1, nseg = (n + seg - 1) >> lg;
     for (int s = tid; s < nseg; s += 1024) {  // each segment's axis: the widest spread of centres
-      const int a0 = s * seg, cnt = min(seg, n - a0);
+      const int a0 = s << lg, cnt = min(seg, n - a0);
       int ax = -1;
       if (cnt > half) {
         float best = -1.0f;
         for (int x = 0; x < 3; ++x) {
-          const int* px = p + (size_t)x * n;
-          const float e = kd_comp(k.cen[px[a0 + cnt - 1]], x) - kd_comp(k.cen[px[a0]], x);
+          const float e = kd_comp(k.cen[s_p[x][a0 + cnt - 1]], x) - kd_comp(k.cen[s_p[x][a0]], x);
           if (ax < 0 || e > best) { best = e; ax = x; }
         }
       }
-      k.axis[s] = ax;
+      s_axis[s] = (int8_t)ax;
     }
     __syncthreads();
     for (int i = tid; i < n; i += 1024) {  // side of each collider: its rank on its segment's axis
-      const int s = i / seg, ax = k.axis[s];
-      if (ax >= 0) k.side[p[(size_t)ax * n + i]] = (i - s * seg) < half ? 1 : 0;
+      const int ax = s_axis[i >> lg];
+      if (ax >= 0) s_side[s_p[ax][i]] = (i & (seg - 1)) < half ? 1 : 0;
     }
     __syncthreads();
+    uint32_t pk[3][kKdChunk / 2];  // the chunk's ids, two u16 per register
+    for (int x = 0; x < 3; ++x)
+      for (int j = 0; j < kKdChunk / 2; ++j) pk[x][j] = 0u;
+    uint32_t fl[3] = {0u, 0u, 0u};
     int c[3] = {0, 0, 0};
-    for (int i = i0; i < i1; ++i) {
-      const int ax = k.axis[i / seg];
-      for (int x = 0; x < 3; ++x) c[x] += ax < 0 ? 1 : k.side[p[(size_t)x * n + i]];
+#pragma unroll
+    for (int j = 0; j < kKdChunk; ++j) {
+      const int i = i0 + j;
+      if (i < i1) {
+        const int ax = s_axis[i >> lg];
+        for (int x = 0; x < 3; ++x) {
+          const uint32_t v = s_p[x][i];
+          pk[x][j >> 1] |= v << (16 * (j & 1));
+          const uint32_t f = ax < 0 ? 1u : s_side[v];
+          fl[x] |= f << j;
+          c[x] += (int)f;
+        }
+      }
     }
-    kd_block_scan3(c, s_wave);
-    for (int i = i0; i < i1; ++i) {
-      const int ax = k.axis[i / seg];
-      for (int x = 0; x < 3; ++x) {
-        k.pre[(size_t)x * n + i] = c[x];
-        c[x] += ax < 0 ? 1 : k.side[p[(size_t)x * n + i]];
+    kd_block_scan3(c, s_wave);  // (its barriers also order every read of s_p above before the scatter)
+    {
+      int run[3] = {c[0], c[1], c[2]};
+#pragma unroll
+      for (int j = 0; j < kKdChunk; ++j) {
+        const int i = i0 + j;
+        if (i < i1) {
+          const bool start = (i & (seg - 1)) == 0;
+          for (int x = 0; x < 3; ++x) {
+            if (start) s_segpre[x][i >> lg] = (uint16_t)run[x];
+            run[x] += (int)((fl[x] >> j) & 1u);
+          }
+        }
       }
     }
     __syncthreads();
-    for (int i = i0; i < i1; ++i) {  // stable partition of every array: left half first
-      const int s = i / seg, a0 = s * seg, ax = k.axis[s];
-      for (int x = 0; x < 3; ++x) {
-        const int id = p[(size_t)x * n + i];
-        const int lr = k.pre[(size_t)x * n + i] - k.pre[(size_t)x * n + a0];
-        const bool left = ax < 0 || k.side[id] != 0;
-        q[(size_t)x * n + (left ? a0 + lr : a0 + half + (i - a0 - lr))] = id;
+    {  // stable partition of every array: left half first
+      int run[3] = {c[0], c[1], c[2]};
+#pragma unroll
+      for (int j = 0; j < kKdChunk; ++j) {
+        const int i = i0 + j;
+        if (i < i1) {
+          const int s = i >> lg, a0 = s << lg;
+          for (int x = 0; x < 3; ++x) {
+            const bool left = ((fl[x] >> j) & 1u) != 0u;
+            const int lr = run[x] - (int)s_segpre[x][s];
+            s_p[x][left ? a0 + lr : a0 + half + (i - a0 - lr)] = (uint16_t)(pk[x][j >> 1] >> (16 * (j & 1)));
+            run[x] += left ? 1 : 0;
+          }
+        }
       }
     }
     __syncthreads();
-    int* t = p; p = q; q = t;
   }
-  for (int i = tid; i < n; i += 1024) perm[i] = p[i];
+  for (int i = tid; i < n; i += 1024) perm[i] = s_p[0][i];
 }
 
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {

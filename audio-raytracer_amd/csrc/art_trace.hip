@@ -755,34 +755,48 @@ struct EchoFromHits {
   const float* origins;
   const int* ray_order;
   const int2* pre;
+  int no_path;  // the frame runs no path kernel: the echo traversal writes the misses' reset 0 and counts the echo rays
 };
-__device__ __forceinline__ bool echo_seg_from_hit(const DevScene& sc, const EchoFromHits& eh, uint32_t g, int r, Seg& s,
-                                                  float& maxd, uint32_t& out_at, uint16_t& out_val) {
+// The hit of ray slot r of 64-ray group g from its nearest-hit record, as path_kernel computes it
+// (:111, :124, the zero-distance re-evaluation included): false for a slot past the fan's rays
+// (slot_ok false) or a miss.
+__device__ __forceinline__ bool hit_from_pre(const DevScene& sc, const EchoFromHits& eh, uint32_t g, int r, bool& slot_ok,
+                                             int& fan, int& ray, vec3& O, vec3& o, vec3& off, int& type, int& idx) {
   const FrameParams& fp = eh.fp;
   const int nrb = (fp.R + 63) >> 6;
-  const int fan = (int)(g / (uint32_t)nrb);
+  fan = (int)(g / (uint32_t)nrb);
   const int slot = (int)(g - (uint32_t)fan * nrb) * 64 + r;
-  if (fan >= fp.S || slot >= fp.R) return false;
+  slot_ok = fan < fp.S && slot < fp.R;
+  if (!slot_ok) return false;
+  ray = eh.ray_order[slot];
   const int2 ph = eh.pre[(size_t)g * 64 + r];
-  if (ph.y == kNoHit) return false;  // a miss: no echo ray (the path kernel resets the slot)
-  const int ray = eh.ray_order[slot];
-  const vec3 O = load3(eh.origins, fan);
+  if (ph.y == kNoHit) return false;  // a miss: no echo ray, no muffle rays
+  O = load3(eh.origins, fan);
   const vec3 d = load_dir(sc.dirs, ray);
   const Seg s0 = make_seg(O, d);
-  const int rank = ph.y >> 28, idx = ph.y & 0x0fffffff;
-  const int type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
+  const int rank = ph.y >> 28;
+  idx = ph.y & 0x0fffffff;
+  type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
   float dist = __int_as_float(ph.x);
   if (dist == 0.0f) {  // as path_kernel
     if (type == kSphere) sphere_hit_dist(s0, sc.sph[idx], dist);
     if (type == kAabb) aabb_test<true>(s0, sc.aabb[idx], dist);
     if (type == kObb) { const ObbRec rr = sc.obb[idx]; obb_test<true>(s0, rr, stored_q(rr), dist); }
   }
-  const vec3 o = O + d * dist;                   // :111
-  const vec3 off = o - d * kEps;                 // :124
+  o = O + d * dist;      // :111
+  off = o - d * kEps;    // :124, :158
+  return true;
+}
+__device__ __forceinline__ bool echo_seg_from_hit(const DevScene& sc, const EchoFromHits& eh, uint32_t g, int r, Seg& s,
+                                                  float& maxd, uint32_t& out_at, uint16_t& out_val, bool& slot_ok) {
+  int fan = 0, ray = 0, type = kNone, idx = 0;
+  vec3 O, o, off;
+  const bool hit = hit_from_pre(sc, eh, g, r, slot_ok, fan, ray, O, o, off, type, idx);
+  out_at = slot_ok ? (uint32_t)(((size_t)fan * eh.L.stride + eh.L.echo_off) / 2) + (uint32_t)ray : 0u;  // ray * H + 0
+  if (!hit) return false;
   const float dist0 = distance(O, o);            // :130
   s = make_seg(off, normalize(O - off));
   maxd = dist0;
-  out_at = (uint32_t)(((size_t)fan * eh.L.stride + eh.L.echo_off) / 2) + (uint32_t)ray;  // ray * H + 0
   out_val = (uint16_t)f32tof16(dist0 * echo_of(sc, type, idx));   // :142-144
   return true;
 }
@@ -803,7 +817,12 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
   s.a2 = 0.0f;
   if (HM) {
-    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val);
+    bool slot_ok;
+    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val, slot_ok);
+    if (eh.no_path) {  // the path kernel's duties for this frame: a miss keeps the reset 0 (:76, :200-207)
+      if (slot_ok && !valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = 0;
+      if (ex) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__ballot(valid) & 0x1111111111111111ull));
+    }
     if (!__any(valid)) return;
   } else {
     // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
@@ -987,17 +1006,31 @@ __device__ bool muffle_brute(const DevScene& sc, const Seg& s, float maxd, int t
   return false;
 }
 
-template <bool EX, bool OBB>
+// HM: one-hit frames with one batch slot whose path kernel does not run: lane i is ray slot i
+// (64-ray group i / 64) and its muffle rays start from the nearest hit as the path kernel computes
+// it (hit_from_pre); the accumulator base is fan * T (TC == 1: batch slot 0).
+template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
-                                                     const uint32_t* __restrict__ count, uint32_t* __restrict__ acc) {
+                                                     const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
+                                                     EchoFromHits eh) {
   const int lane = threadIdx.x & 63;
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t n = ldc(count, 1);
+  const uint32_t n = HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u : ldc(count, 1);
   if (__builtin_amdgcn_readfirstlane(i - (uint32_t)lane) >= n) return;
-  const bool valid = i < n;
-  const float4 r = vp.hrec[valid ? i : 0u];
-  const vec3 off = mk3(r.x, r.y, r.z);
-  const uint32_t dbase = __float_as_uint(r.w);
+  bool valid = i < n;
+  vec3 off = mk3(0.0f, 0.0f, 0.0f);
+  uint32_t dbase = 0u;
+  if (HM) {
+    bool slot_ok;
+    int fan = 0, ray = 0, type = kNone, idx = 0;
+    vec3 O, o;
+    valid = valid && hit_from_pre(sc, eh, i >> 6, (int)(i & 63u), slot_ok, fan, ray, O, o, off, type, idx);
+    dbase = (uint32_t)fan * (uint32_t)fp.T;
+  } else {
+    const float4 r = vp.hrec[valid ? i : 0u];
+    off = mk3(r.x, r.y, r.z);
+    dbase = __float_as_uint(r.w);
+  }
   unsigned nt[3] = {0u, 0u, 0u}, ne = 0u, nfb = 0u;  // tests, list entries scanned, fallback rays
   for (int t = blockIdx.y; t < fp.T; t += gridDim.y) {  // workgroup-uniform
     const vec3 tp = load3(sc.targets, t);
@@ -1169,14 +1202,24 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (fp.exec) { if (obb) ART_VIS(S_, BLOCKS_, B_, true, true, HM_); else ART_VIS(S_, BLOCKS_, B_, true, false, HM_); } \
     else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true, HM_); else ART_VIS(S_, BLOCKS_, B_, false, false, HM_); }       \
   } while (0)
-  const unsigned mblocks = (unsigned)((hcap + 255) / 256);  // hit records: at most one per ray and bounce
+  // One-hit frames with one batch slot, no hit outputs (HM2): no path kernel at all; the echo
+  // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too.
+  const bool hm2 = hm && !L.has_hits;
+  eh.no_path = hm2 ? 1 : 0;
+  const unsigned mblocks = hm2 ? (groups + 3) / 4 : (unsigned)((hcap + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
-#define ART_MUFFLE(S_, EX_, OBB_) \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, muffle_acc)
-#define ART_MUFFLE_ANY(S_)                                                                           \
-  do {                                                                                               \
-    if (fp.exec) { if (obb) ART_MUFFLE(S_, true, true); else ART_MUFFLE(S_, true, false); }         \
-    else { if (obb) ART_MUFFLE(S_, false, true); else ART_MUFFLE(S_, false, false); }               \
+#define ART_MUFFLE(S_, EX_, OBB_, HM_)                                                                                  \
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, \
+                     muffle_acc, eh)
+#define ART_MUFFLE_ANY(S_)                                                                                             \
+  do {                                                                                                                 \
+    if (hm2) {                                                                                                         \
+      if (fp.exec) { if (obb) ART_MUFFLE(S_, true, true, true); else ART_MUFFLE(S_, true, false, true); }             \
+      else { if (obb) ART_MUFFLE(S_, false, true, true); else ART_MUFFLE(S_, false, false, true); }                   \
+    } else {                                                                                                           \
+      if (fp.exec) { if (obb) ART_MUFFLE(S_, true, true, false); else ART_MUFFLE(S_, true, false, false); }           \
+      else { if (obb) ART_MUFFLE(S_, false, true, false); else ART_MUFFLE(S_, false, false, false); }                 \
+    }                                                                                                                  \
   } while (0)
   // Stream plan. Multi-hit frames: per bounce nearest → path on st, that bounce's echo traversal
   // on the side stream right after its path kernel (beside the next bounces' nearest traversals,
@@ -1202,7 +1245,8 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
 #define ART_PATH(H_, M_)                                                                                              \
   hipLaunchKernelGGL((path_kernel<H_, M_>), dim3(path_blocks), dim3(64 * kPathWaves), 0, pst, sc, fp, L, origins, block, \
                      ray_order, pb.vp, pair_count, pb.pre, pb.state, k, (int)!hm)
-    if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
+    if (hm2) {}
+    else if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
     else { if (multi) ART_PATH(false, true); else ART_PATH(false, false); }
 #undef ART_PATH
     if (per_bounce) {  // this bounce's echoes (at most one per ray slot: `groups` batches)
@@ -1214,7 +1258,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   if (per_bounce) {
     ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
   } else if (hm) {
-    ART_MUFFLE_ANY(echo.st);           // after the path kernel there
+    ART_MUFFLE_ANY(echo.st);           // after the path kernel there (HM2: the only kernel there)
     ART_VIS_ANY(st, groups, -1, true);  // one 64-ray group per workgroup
   } else if (split) {
     (void)hipEventRecord(echo.fork, st);
