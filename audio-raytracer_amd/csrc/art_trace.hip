@@ -1010,11 +1010,11 @@ __device__ bool muffle_brute(const DevScene& sc, const Seg& s, float maxd, int t
 // (64-ray group i / 64) and its muffle rays start from the nearest hit as the path kernel computes
 // it (hit_from_pre); the accumulator base is fan * T (TC == 1: batch slot 0).
 template <bool EX, bool OBB, bool HM>
-__global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
-                                                     const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
-                                                     EchoFromHits eh) {
+__device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParams& fp, const VisPairs& vp,
+                                            const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
+                                            const EchoFromHits& eh, uint32_t bx, int by, int gy) {
   const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t i = bx * 256u + threadIdx.x;
   const uint32_t n = HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u : ldc(count, 1);
   if (__builtin_amdgcn_readfirstlane(i - (uint32_t)lane) >= n) return;
   bool valid = i < n;
@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
     dbase = __float_as_uint(r.w);
   }
   unsigned nt[3] = {0u, 0u, 0u}, ne = 0u, nfb = 0u;  // tests, list entries scanned, fallback rays
-  for (int t = blockIdx.y; t < fp.T; t += gridDim.y) {  // workgroup-uniform
+  for (int t = by; t < fp.T; t += gy) {  // workgroup-uniform
     const vec3 tp = load3(sc.targets, t);
     const float maxd = distance(off, tp);                             // :165
     const bool act = valid && maxd < fp.max_muffle;                   // :168
@@ -1113,6 +1113,31 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
     exec_add(fp.exec, kExecCellEntries, wave_sum_u32(ne));
     exec_add(fp.exec, kExecMuffleFallback, wave_sum_u32(nfb));
   }
+}
+
+template <bool EX, bool OBB, bool HM>
+__global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
+                                                     const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
+                                                     EchoFromHits eh) {
+  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x, (int)blockIdx.y, (int)gridDim.y);
+}
+
+// One-hit frames with one batch slot, no path kernel (HM2) and no OBBs: the echo traversal and the
+// muffle rays, both from the nearest hits, as one launch on the launch stream: workgroups [0, groups) are
+// the echo batches (dispatched first, one round of waves), the rest the muffle blocks (mblocks x
+// mt, filling the echo traversal's tails). No side stream, so no fork / join on the frame's path.
+template <bool EX, bool OBB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEchoWaves<EX, OBB>)))
+void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t* __restrict__ count,
+                        unsigned long long* ex, uint8_t* __restrict__ block, EchoFromHits eh, uint32_t* __restrict__ acc,
+                        uint32_t groups, uint32_t mblocks, int mt) {
+  __shared__ uint32_t s_stk[64 * kBvhStack];
+  if (blockIdx.x < groups) {
+    vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, nullptr, -1, block, eh);
+    return;
+  }
+  const uint32_t b = blockIdx.x - groups;
+  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, b % mblocks, (int)(b / mblocks), mt);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1205,6 +1230,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // One-hit frames with one batch slot, no hit outputs (HM2): no path kernel at all; the echo
   // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too.
   const bool hm2 = hm && !L.has_hits;
+  // ... and in OBB-free scenes the two as one launch on st (echo_muffle_kernel; with the OBB tests
+  // the joint kernel would spill VGPRs inside the traversal loop, so OBB scenes keep the side stream)
+  const bool fused = hm2 && !obb;
   eh.no_path = hm2 ? 1 : 0;
   const unsigned mblocks = hm2 ? (groups + 3) / 4 : (unsigned)((hcap + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
@@ -1237,7 +1265,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
 #undef ART_NEAREST
     hipStream_t pst = st;
-    if (hm) {
+    if (hm && !hm2) {  // (HM2 forks the muffle rays below)
       (void)hipEventRecord(echo.fork, st);
       (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
       pst = echo.st;
@@ -1257,7 +1285,18 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   }
   if (per_bounce) {
     ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
+  } else if (fused) {
+#define ART_ECHO_MUFFLE(EX_)                                                                                          \
+  hipLaunchKernelGGL((echo_muffle_kernel<EX_, false>), dim3(groups + mblocks * mt), dim3(256), 0, st, sc, fp, pb.vp,  \
+                     pair_count, EX_ ? fp.exec : nullptr, block, eh, muffle_acc, groups, mblocks, (int)mt)
+    if (fp.exec) ART_ECHO_MUFFLE(true);
+    else ART_ECHO_MUFFLE(false);
+#undef ART_ECHO_MUFFLE
   } else if (hm) {
+    if (hm2) {  // no path kernel: fork the muffle rays here
+      (void)hipEventRecord(echo.fork, st);
+      (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
+    }
     ART_MUFFLE_ANY(echo.st);           // after the path kernel there (HM2: the only kernel there)
     ART_VIS_ANY(st, groups, -1, true);  // one 64-ray group per workgroup
   } else if (split) {
@@ -1273,7 +1312,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
 #undef ART_MUFFLE
 #undef ART_VIS_ANY
 #undef ART_VIS
-  if (split) {
+  if (split && !fused) {
     (void)hipEventRecord(echo.join, echo.st);
     (void)hipStreamWaitEvent(st, echo.join, 0);
   }
