@@ -1122,12 +1122,13 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
   muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x, (int)blockIdx.y, (int)gridDim.y);
 }
 
-// One-hit frames with one batch slot, no path kernel (HM2) and no OBBs: the echo traversal and the
-// muffle rays, both from the nearest hits, as one launch on the launch stream: workgroups [0, groups) are
+// One-hit frames with one batch slot and no path kernel (HM2): the echo traversal and the muffle
+// rays, both from the nearest hits, as one launch on the launch stream: workgroups [0, groups) are
 // the echo batches (dispatched first, one round of waves), the rest the muffle blocks (mblocks x
 // mt, filling the echo traversal's tails). No side stream, so no fork / join on the frame's path.
+// With OBB tests the joint kernel runs at 6 waves per SIMD (5 counting), where it needs no spills.
 template <bool EX, bool OBB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEchoWaves<EX, OBB>)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OBB ? (EX ? 5 : 6) : kEchoWaves<EX, OBB>)))
 void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t* __restrict__ count,
                         unsigned long long* ex, uint8_t* __restrict__ block, EchoFromHits eh, uint32_t* __restrict__ acc,
                         uint32_t groups, uint32_t mblocks, int mt) {
@@ -1230,9 +1231,8 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // One-hit frames with one batch slot, no hit outputs (HM2): no path kernel at all; the echo
   // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too.
   const bool hm2 = hm && !L.has_hits;
-  // ... and in OBB-free scenes the two as one launch on st (echo_muffle_kernel; with the OBB tests
-  // the joint kernel would spill VGPRs inside the traversal loop, so OBB scenes keep the side stream)
-  const bool fused = hm2 && !obb;
+  // ... and the two as one launch on st (echo_muffle_kernel)
+  const bool fused = hm2;
   eh.no_path = hm2 ? 1 : 0;
   const unsigned mblocks = hm2 ? (groups + 3) / 4 : (unsigned)((hcap + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
@@ -1286,11 +1286,11 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   if (per_bounce) {
     ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
   } else if (fused) {
-#define ART_ECHO_MUFFLE(EX_)                                                                                          \
-  hipLaunchKernelGGL((echo_muffle_kernel<EX_, false>), dim3(groups + mblocks * mt), dim3(256), 0, st, sc, fp, pb.vp,  \
+#define ART_ECHO_MUFFLE(EX_, OBB_)                                                                                    \
+  hipLaunchKernelGGL((echo_muffle_kernel<EX_, OBB_>), dim3(groups + mblocks * mt), dim3(256), 0, st, sc, fp, pb.vp,   \
                      pair_count, EX_ ? fp.exec : nullptr, block, eh, muffle_acc, groups, mblocks, (int)mt)
-    if (fp.exec) ART_ECHO_MUFFLE(true);
-    else ART_ECHO_MUFFLE(false);
+    if (fp.exec) { if (obb) ART_ECHO_MUFFLE(true, true); else ART_ECHO_MUFFLE(true, false); }
+    else { if (obb) ART_ECHO_MUFFLE(false, true); else ART_ECHO_MUFFLE(false, false); }
 #undef ART_ECHO_MUFFLE
   } else if (hm) {
     if (hm2) {  // no path kernel: fork the muffle rays here
