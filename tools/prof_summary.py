@@ -22,11 +22,11 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-HOT = ("nearest_first_kernel", "path_kernel", "vis_kernel", "muffle_kernel", "cells_collider_kernel",
+HOT = ("nearest_first_kernel", "path_kernel", "vis_kernel", "muffle_kernel", "echo_muffle_kernel", "cells_collider_kernel",
        "raytrace_kernel", "permeate_kernel", "reduce_kernel")
 # kernels of the timed raytrace stage (muffle_kernel runs once per frame; nearest, path and the echo
 # vis_kernel once per bounce)
-STAGE = ("nearest_first_kernel", "path_kernel", "vis_kernel", "muffle_kernel")
+STAGE = ("nearest_first_kernel", "path_kernel", "vis_kernel", "muffle_kernel", "echo_muffle_kernel")
 
 
 def short(name: str) -> str:
@@ -74,15 +74,14 @@ def main():
 
     # HBM traffic of the timed raytrace stage per frame (sum over its kernels of the mean per launch)
     # (the <true> instantiations are the one test-counting launch of a run, not timed frames)
-    stage = [k for k in per if k.startswith(STAGE) and not k.startswith(("nearest_first_kernel<true", "vis_kernel<true",
-                                                                          "muffle_kernel<true"))]
+    stage = [k for k in per if k.startswith(STAGE) and "<true" not in k]
     if stage:
         def mean(k, c):
             v = per[k].get(c, [])
             return sum(v) / len(v) if v else 0.0
         # launches per frame: multi-hit frames run nearest_first_kernel, path_kernel and the echo
-        # vis_kernel once per bounce, muffle_kernel once
-        ref = max((len(v.get("FETCH_SIZE", [])) for k, v in per.items() if k.startswith("muffle_kernel<false")), default=1) or 1
+        # vis_kernel once per bounce; reduce_kernel runs once per frame
+        ref = max((len(v.get("FETCH_SIZE", [])) for k, v in per.items() if k.startswith("reduce_kernel")), default=1) or 1
 
         def per_frame(k, c):  # mean per dispatch x dispatches per frame (rounded ratio to muffle_kernel's)
             v = per[k].get(c, [])
