@@ -214,9 +214,10 @@ static void launch_bvh_upper(CullRec* nodes, int L, hipStream_t st) {
 // blocks are aligned power-of-4 ranges of leaf positions, left-packed with the colliders. A
 // complete tree over the Morton order lets a node straddle a jump of the Z curve, and its box then
 // spans two distant cells; this order instead splits every node's block in two halves twice
-// (binary level by binary level), each time along the axis on which its colliders' centres extend
-// furthest, with the first half (capacity seg / 2) taking the colliders of smallest centre on that
-// axis: every node is a compact, equal-count kd cell. Measured on config 2's scene (host
+// (binary level by binary level), with the first half (capacity seg / 2) taking the colliders of
+// smallest centre on the split axis: every node is a compact, equal-count kd cell. The axis: on the
+// upper levels (at most kKdSahSegs segments) the one of least surface-area cost of the two halves,
+// below them the one on which the segment's centres extend furthest. Measured on config 2's scene (host
 // simulation of the near-first traversal): 11.5 inner steps and 3.8 leaves per ray vs 28 and 9.3
 // over the Morton order. Any order gives an exact BVH (node bounds are unions).
 //
@@ -232,14 +233,16 @@ constexpr int kKdMaxColliders = 1 << 14;
 constexpr int kKdChunk = kKdMaxColliders / 1024;  // positions per thread
 
 struct KdBufs {
-  float4* cen;  // [n] centre (non-finite components -> FLT_MAX)
-  int* p;       // [3][n] index arrays sorted by x, y, z
+  float4* cen;          // [n] centre (non-finite components -> FLT_MAX)
+  int* p;               // [3][n] index arrays sorted by x, y, z
+  const CullRec* cull;  // [n] the colliders' bounds (surface-area split costs)
 };
 static KdBufs kd_bufs(void* base, int n) {
   char* b = static_cast<char*>(base);
   KdBufs k;
   k.cen = reinterpret_cast<float4*>(b);
   k.p = reinterpret_cast<int*>(b + 16 * (size_t)n);
+  k.cull = nullptr;
   return k;
 }
 size_t kd_scratch_bytes(int n) { return n > 0 && n <= kKdMaxColliders ? (size_t)n * (16 + 4 * 3) : 0; }
@@ -289,12 +292,27 @@ __device__ __forceinline__ void kd_block_scan3(int v[3], int (*s_wave)[16]) {
   __syncthreads();
 }
 
+// Surface-area split costs on the upper binary levels (at most kKdSahSegs segments): for each
+// segment and axis, the bounds of the two halves the split on that axis would make, accumulated in
+// LDS as order-preserving integers (atomic min / max).
+constexpr int kKdSahSegs = 64;
+__device__ __forceinline__ int kd_ord(float f) {  // monotone float -> int (for atomicMin / atomicMax)
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float kd_unord(int v) { return __int_as_float(v >= 0 ? v : v ^ 0x7fffffff); }
+__device__ __forceinline__ float kd_area(float ex, float ey, float ez) {
+  ex = fmaxf(ex, 0.0f); ey = fmaxf(ey, 0.0f); ez = fmaxf(ez, 0.0f);
+  return ex * ey + ey * ez + ez * ex;
+}
+
 __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap, int* __restrict__ perm) {
   __shared__ uint16_t s_p[3][kKdMaxColliders];        // the three index arrays
   __shared__ uint8_t s_side[kKdMaxColliders];         // 1: left half of its segment (by collider id)
   __shared__ int8_t s_axis[kKdMaxColliders / 8];      // per segment: split axis, -1 = fits its left half
   __shared__ uint16_t s_segpre[3][kKdMaxColliders / 8];  // left-flag prefix at each segment's start
   __shared__ int s_wave[3][16];
+  __shared__ int s_box[2][3][kKdSahSegs][6];  // [half][axis][segment]: lo.xyz, hi.xyz (kd_ord)
   const int tid = threadIdx.x;
   const int chunk = (n + 1023) / 1024;
   const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
@@ -303,10 +321,47 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
   __syncthreads();
   for (int lg = 31 - __builtin_clz(cap); lg > 2; --lg) {  // segments of seg = 2^lg positions (cap: a power of 4)
     const int seg = 1 << lg, half = seg >> 1, nseg = (n + seg - 1) >> lg;
-    for (int s = tid; s < nseg; s += 1024) {  // each segment's axis: the widest spread of centres
+    const bool sah = nseg <= kKdSahSegs;
+    if (sah) {  // bounds of both halves of every segment for a split on each axis
+      for (int e = tid; e < 2 * 3 * kKdSahSegs * 6; e += 1024)
+        (&s_box[0][0][0][0])[e] = (e % 6) < 3 ? kd_ord(INFINITY) : kd_ord(-INFINITY);
+      __syncthreads();
+      for (int x = 0; x < 3; ++x) {
+        float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int key = -1;  // (segment << 1 | half) of the run accumulated in b
+        auto flush = [&]() {
+          if (key < 0) return;
+          int* o = s_box[key & 1][x][key >> 1];
+          for (int q = 0; q < 3; ++q) { atomicMin(o + q, kd_ord(b[q])); atomicMax(o + 3 + q, kd_ord(b[3 + q])); }
+          for (int q = 0; q < 3; ++q) { b[q] = INFINITY; b[3 + q] = -INFINITY; }
+        };
+        for (int i = i0; i < i1; ++i) {
+          const int kk = ((i >> lg) << 1) | ((i & (seg - 1)) >= half ? 1 : 0);
+          if (kk != key) { flush(); key = kk; }
+          const CullRec c = k.cull[s_p[x][i]];
+          b[0] = fminf(b[0], c.lox); b[1] = fminf(b[1], c.loy); b[2] = fminf(b[2], c.loz);
+          b[3] = fmaxf(b[3], c.hix); b[4] = fmaxf(b[4], c.hiy); b[5] = fmaxf(b[5], c.hiz);
+        }
+        flush();
+      }
+      __syncthreads();
+    }
+    for (int s = tid; s < nseg; s += 1024) {  // each segment's axis: the cheapest split (SAH) or the widest spread of centres
       const int a0 = s << lg, cnt = min(seg, n - a0);
       int ax = -1;
-      if (cnt > half) {
+      if (cnt > half && sah) {
+        float best = INFINITY;
+        for (int x = 0; x < 3; ++x) {
+          const int* l = s_box[0][x][s];
+          const int* r = s_box[1][x][s];
+          const float cost =
+              kd_area(kd_unord(l[3]) - kd_unord(l[0]), kd_unord(l[4]) - kd_unord(l[1]), kd_unord(l[5]) - kd_unord(l[2])) * (float)half +
+              kd_area(kd_unord(r[3]) - kd_unord(r[0]), kd_unord(r[4]) - kd_unord(r[1]), kd_unord(r[5]) - kd_unord(r[2])) *
+                  (float)(cnt - half);
+          if (cost < best) { best = cost; ax = x; }  // (a non-finite cost never wins)
+        }
+      }
+      if (cnt > half && ax < 0) {
         float best = -1.0f;
         for (int x = 0; x < 3; ++x) {
           const float e = kd_comp(k.cen[s_p[x][a0 + cnt - 1]], x) - kd_comp(k.cen[s_p[x][a0]], x);
@@ -385,7 +440,8 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   if (L == 0 || !sb.bvh || !sb.bvh_ref || !sb.bvh_leaf) return 0;
   const int nleaf = total - leaf0;
   if (sb.kd && n <= kKdMaxColliders) {  // kd leaf order
-    const KdBufs k = kd_bufs(sb.kd, n);
+    KdBufs k = kd_bufs(sb.kd, n);
+    k.cull = sc.cull;
     hipLaunchKernelGGL(kd_cen_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k.cen);
     for (int a = 0; a < 3; ++a) {
       hipLaunchKernelGGL(kd_key_kernel, dim3((n + 255) / 256), dim3(256), 0, st, k.cen, n, a, sb.keys, sb.vals);

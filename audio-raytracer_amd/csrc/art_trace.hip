@@ -227,8 +227,11 @@ constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every
 // the echo traversal's OBB one run at the occupancy that holds them without spills; the nearest
 // traversal's OBB instantiation keeps 8 waves and 5 spilled VGPRs (at 7 waves config 3's nearest
 // kernel took 300 instead of 243 us), covered by the full-size OBB parity tests.
+#ifndef ART_NEAREST_OBB_WAVES
+#define ART_NEAREST_OBB_WAVES 8
+#endif
 template <bool EX, bool OBB>
-constexpr int kNearestWaves = EX ? 6 : 8;
+constexpr int kNearestWaves = EX ? 6 : (OBB ? ART_NEAREST_OBB_WAVES : 8);
 template <bool EX, bool OBB>
 constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
 // k-th (0-based) set bit of m, k < popcount(m).
