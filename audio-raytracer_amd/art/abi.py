@@ -50,7 +50,6 @@ ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
-ART_CTX_GRAPH = 0x100
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 # art_fan.ray_hit_ids: ColliderType (Enums/ColliderType.cs) << 30 | index in that type's array
@@ -110,18 +109,26 @@ class art_fan_layout(C.Structure):
 
 class art_kernel_times(C.Structure):
     _fields_ = [("raytrace_ms", C.c_double), ("permeate_ms", C.c_double), ("reduce_ms", C.c_double),
-                ("launches", C.c_int32)]
+                ("launches", C.c_int32), ("nearest_launches", C.c_int32), ("nearest_ms", C.c_double)]
 
 
 class art_collider_sync_stats(C.Structure):
     _fields_ = [("dirty_records", C.c_int32), ("full_prep", C.c_int32), ("reallocated", C.c_int32),
-                ("reserved", C.c_int32), ("bytes_uploaded", C.c_uint64)]
+                ("cells_rebuilt", C.c_int32), ("bytes_uploaded", C.c_uint64)]
+
+
+class art_exec_kernel(C.Structure):
+    _fields_ = [("sphere", C.c_uint64), ("aabb", C.c_uint64), ("obb", C.c_uint64), ("cull_box", C.c_uint64),
+                ("cell_entries", C.c_uint64)]
+
+
+EXEC_KERNELS = ("nearest", "echo", "muffle")  # art_exec_counts.by_kernel order
 
 
 class art_exec_counts(C.Structure):
     _fields_ = [("sphere", C.c_uint64), ("aabb", C.c_uint64), ("obb", C.c_uint64), ("cull_box", C.c_uint64),
                 ("cell_entries", C.c_uint64), ("launches", C.c_uint64), ("muffle_fallback", C.c_uint64),
-                ("echo_pairs", C.c_uint64), ("bounce_rays", C.c_uint64 * 16)]
+                ("echo_pairs", C.c_uint64), ("bounce_rays", C.c_uint64 * 16), ("by_kernel", art_exec_kernel * 3)]
 
 
 # include/art_dsp.h

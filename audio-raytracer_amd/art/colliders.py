@@ -79,7 +79,7 @@ class ColliderStore:
         self._check(self.ctx.lib.art_colliders_sync(self.ctx.ptr))
         st = abi.art_collider_sync_stats()
         self._check(self.ctx.lib.art_colliders_last_sync(self.ctx.ptr, C.byref(st)))
-        return {k: int(getattr(st, k)) for k, _ in abi.art_collider_sync_stats._fields_ if k != "reserved"}
+        return {k: int(getattr(st, k)) for k, _ in abi.art_collider_sync_stats._fields_}
 
 
 def resident_frame(frame: Frame) -> Frame:

@@ -284,7 +284,7 @@ class Context:
         if rc:
             self._raise(rc)
         return {"raytrace_ms": t.raytrace_ms, "permeate_ms": t.permeate_ms, "reduce_ms": t.reduce_ms,
-                "launches": t.launches}
+                "launches": t.launches, "nearest_ms": t.nearest_ms, "nearest_launches": t.nearest_launches}
 
     def executed_counts(self) -> dict:
         """Work the throughput kernel executed since the last call (needs ART_CTX_COUNT_EXECUTED)."""
@@ -292,8 +292,10 @@ class Context:
         rc = self.lib.art_executed_counts(self.ptr, C.byref(t))
         if rc:
             self._raise(rc)
-        out = {k: int(getattr(t, k)) for k, ty in abi.art_exec_counts._fields_ if k != "bounce_rays"}
+        out = {k: int(getattr(t, k)) for k, ty in abi.art_exec_counts._fields_ if k not in ("bounce_rays", "by_kernel")}
         out["bounce_rays"] = [int(v) for v in t.bounce_rays]
+        out["by_kernel"] = {name: {f: int(getattr(t.by_kernel[i], f)) for f, _ in abi.art_exec_kernel._fields_}
+                            for i, name in enumerate(abi.EXEC_KERNELS)}
         return out
 
     def close(self):

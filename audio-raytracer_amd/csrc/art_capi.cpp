@@ -45,7 +45,7 @@ static_assert(sizeof(art_dsp_params) == 24, "art_dsp_params");
 
 namespace {
 
-constexpr uint32_t kAbiVersion = (2u << 16) | 2u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1: art_exec_counts.cell_entries / muffle_fallback, ART_CTX_GRAPH; 2.2: art_exec_counts.bounce_rays
+constexpr uint32_t kAbiVersion = (2u << 16) | 3u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1: art_exec_counts.cell_entries / muffle_fallback; 2.2: art_exec_counts.bounce_rays; 2.3: art_exec_counts.by_kernel, ART_CTX_GRAPH removed
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
@@ -98,35 +98,13 @@ struct Frame {
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
   size_t soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0, soa_kd = 0;
   // muffle candidate lists (art_cells.hip)
-  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, cells_temp = 0,
+  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, soa_ctot = 0, cells_temp = 0,
          soa_cgeo = 0;
   uint32_t cells_cap = 0;
 };
 
-// Everything a captured frame graph bakes in: a replay is valid only for an identical key.
-struct GraphKey {
-  DevScene sc;
-  FrameParams fp;
-  FanLayout L;
-  const void *org, *blk, *acc, *pairs, *raw, *exec;
-  uint32_t flags;
-  int fans;
-  bool count;
-};
-
 struct Device {
   int id = 0;
-  // frame graphs (enqueue_kernels): capture stream and a small cache of instantiated graphs
-  struct Graph {
-    GraphKey key;
-    hipGraphExec_t exec = nullptr;
-    uint64_t used = 0;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // permeation fork / join, echo fork / join
-  };
-  std::vector<hipEvent_t> graph_events;  // every graph's events (kept for the process's life)
-  hipStream_t cap = nullptr;
-  std::vector<Graph> graphs;
-  uint64_t graph_clock = 0, graph_captures = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   DevBuf raw, soa, origins, block, acc, counts;
@@ -472,6 +450,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_cent_s = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
     f.soa_cfar = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_cok = s; s = align_up(s + (size_t)f.T * 4, 256);
+    f.soa_ctot = s; s = align_up(s + (size_t)f.T * 8, 256);
     f.soa_ctemp = s; s = align_up(s + f.cells_temp, 256);
     f.soa_cent = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
     f.soa_cgeo = s; s = align_up(s + cells_geo_bytes(f.T, f.ns + f.na + f.no), 256);
@@ -614,6 +593,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.cursor = reinterpret_cast<uint32_t*>(soa + f.soa_ccur);
     cb.far = reinterpret_cast<float*>(soa + f.soa_cfar);
     cb.ok = reinterpret_cast<uint32_t*>(soa + f.soa_cok);
+    cb.tcount = reinterpret_cast<unsigned long long*>(soa + f.soa_ctot);
     cb.temp = soa + f.soa_ctemp; cb.temp_bytes = f.cells_temp;
     cb.ent = reinterpret_cast<uint2*>(soa + f.soa_cent);
     cb.ent_s = reinterpret_cast<uint2*>(soa + f.soa_cent_s);
@@ -679,7 +659,7 @@ hipEvent_t pool_event(Device& dv, size_t i) {
   return dv.ev_pool[i];
 }
 
-// Fan lanes per frame (ART_FAN_LANES, 1..kMaxFanLanes; graph-replayed and counting frames use 1).
+// Fan lanes per frame (ART_FAN_LANES, 1..kMaxFanLanes; counting frames use 1).
 int fan_lanes() {
   static const int n = [] {
     const char* e = getenv("ART_FAN_LANES");
@@ -687,18 +667,6 @@ int fan_lanes() {
     return std::max(1, std::min(v, kMaxFanLanes));
   }();
   return n;
-}
-
-constexpr size_t kGraphCache = 16;         // instantiated frame graphs per device
-constexpr int kGraphsPerProcess = 512;     // and per process (they are released only at exit)
-std::atomic<int> g_graphs_alive{0};
-
-bool graphs_forced() {
-  static const bool on = [] {
-    const char* e = getenv("ART_GRAPH");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 // Enqueue the kernels of one frame for fan_count fans on stream st.
@@ -753,8 +721,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.join, hipEventDisableTiming));
     }
   }
-  const bool graph = !count && !timing && ((c->flags & ART_CTX_GRAPH) || graphs_forced());
-  const int nlanes = fast && !graph ? std::min(fan_lanes(), fan_count) : 1;
+  const int nlanes = fast ? std::min(fan_lanes(), fan_count) : 1;
   const int lane_fans = (fan_count + nlanes - 1) / nlanes;
   size_t lane_pair_bytes = 0;
   if (fast) {
@@ -789,8 +756,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     dv.exec_launches++;
   }
 
-  // The frame's launch sequence on stream st: stage kernels, side-stream forks and joins. It
-  // allocates nothing and reads no device state on the host, so it can be captured as a graph.
+  // The frame's launch sequence on stream st: stage kernels, side-stream forks and joins.
   auto launch = [&](hipStream_t st, hipEvent_t pfork, hipEvent_t pjoin, const SideStream& echo) -> int {
   // an error return after the fork drains the side stream first (the caller may free d_block)
   struct SideDrain {
@@ -827,6 +793,19 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         HIP_TRY(c, hipEventRecord(dv.lanes[j].fork, st));
         HIP_TRY(c, hipStreamWaitEvent(dv.lanes[j].st, dv.lanes[j].fork, 0));
       }
+      // nearest-kernel marks (timed frames): pool pairs after the stage's own, kept for those recorded
+      NearestMarks marks;
+      std::vector<hipEvent_t> mev;
+      if (timing) {
+        const size_t base = dv.ev_used.size() * 2;
+        marks.cap = std::min(f.H * ((lane_fans + chunk - 1) / chunk), 64);
+        for (int k = 0; k < 2 * marks.cap; ++k) {
+          hipEvent_t e = pool_event(dv, base + k);
+          if (!e) { marks.cap = k / 2; break; }
+          mev.push_back(e);
+        }
+        marks.ev = mev.data();
+      }
       for (int j = 0; j < nlanes; ++j) {
         const int l0 = std::min(fan_count, j * lane_fans), l1 = std::min(fan_count, l0 + lane_fans);
         Device::Lane& ln = dv.lanes[j];
@@ -837,13 +816,14 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
           fpc.S = std::min(chunk, l1 - b0);
           launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
                                acc + (size_t)b0 * f.TC * f.T, order, pairs, pair_count + 4 * j, ls,
-                               j == 0 ? echo : ln.echo);
+                               j == 0 ? echo : ln.echo, j == 0 && timing ? &marks : nullptr);
         }
         if (j > 0) {
           HIP_TRY(c, hipEventRecord(ln.join, ls));
           HIP_TRY(c, hipStreamWaitEvent(st, ln.join, 0));
         }
       }
+      for (int k = 0; k < marks.used; ++k) dv.ev_used.push_back({3, dv.ev_used.size() * 2});  // = base + 2 k
     }
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
@@ -871,55 +851,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   return ART_OK;
   };
 
-  // Graph replay: the launch sequence is captured once on a private stream, with the
-  // side streams' event edges as graph edges, and the instantiated graph is launched on the
-  // caller's stream for every later frame with the same launch key (scene, frame parameters,
-  // buffers, fan count, flags). One graph launch replaces ~10 launches and the host-side fork /
-  // join gaps. Opt-in (ART_CTX_GRAPH / ART_GRAPH=1); counting and timed frames launch directly.
-  if (!graph) return launch(st, dv.fork, dv.join, dv.echo);
-  GraphKey key;
-  memset(&key, 0, sizeof key);
-  key.sc = dv.sc; key.fp = fp; key.L = f.L;
-  key.org = d_origins; key.blk = d_block; key.acc = dv.acc.p; key.pairs = dv.pairs.p; key.raw = dv.raw.p;
-  key.exec = exec_ctr; key.flags = c->flags; key.fans = fan_count; key.count = count;
-  for (Device::Graph& gr : dv.graphs)
-    if (memcmp(&key, &gr.key, sizeof key) == 0) {
-      gr.used = ++dv.graph_clock;
-      HIP_TRY(c, hipGraphLaunch(gr.exec, st));
-      return ART_OK;
-    }
-  // Instantiated graphs are never destroyed while the process runs: on ROCm 7.2 a hipGraphLaunch
-  // of a newly instantiated graph crashed (host SIGSEGV inside libamdhip64) after an earlier graph
-  // sharing its kernels had been destroyed with hipGraphExecDestroy (tests/test_parity_gpu.py
-  // sequence). A full cache, or the process-wide cap, launches new keys directly.
-  if (dv.graphs.size() >= kGraphCache || g_graphs_alive.load() >= kGraphsPerProcess) return launch(st, dv.fork, dv.join, dv.echo);
-  if (!dv.cap) HIP_TRY(c, hipStreamCreateWithFlags(&dv.cap, hipStreamNonBlocking));
-  // each graph records its own fork / join events (never shared between graphs or with direct launches)
-  Device::Graph gr;
-  for (hipEvent_t* e : {&gr.ev[0], &gr.ev[1], &gr.ev[2], &gr.ev[3]})
-    HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
-  for (hipEvent_t e : gr.ev) dv.graph_events.push_back(e);
-  SideStream gecho = dv.echo;
-  gecho.fork = gr.ev[2];
-  gecho.join = gr.ev[3];
-  HIP_TRY(c, hipStreamBeginCapture(dv.cap, hipStreamCaptureModeRelaxed));
-  const int rc = launch(dv.cap, gr.ev[0], gr.ev[1], gecho);
-  hipGraph_t g = nullptr;
-  const hipError_t ee = hipStreamEndCapture(dv.cap, &g);
-  if (rc || ee != hipSuccess || !g) {
-    if (g) (void)hipGraphDestroy(g);
-    return rc ? rc : fail(c, ART_E_DEVICE, "hipStreamEndCapture failed: %s", hipGetErrorString(ee));
-  }
-  gr.key = key;
-  const hipError_t ei = hipGraphInstantiate(&gr.exec, g, nullptr, nullptr, 0);
-  (void)hipGraphDestroy(g);
-  if (ei != hipSuccess) return fail(c, ART_E_DEVICE, "hipGraphInstantiate failed: %s", hipGetErrorString(ei));
-  gr.used = ++dv.graph_clock;
-  dv.graphs.push_back(gr);
-  dv.graph_captures++;
-  g_graphs_alive.fetch_add(1);
-  HIP_TRY(c, hipGraphLaunch(gr.exec, st));
-  return ART_OK;
+  return launch(st, dv.fork, dv.join, dv.echo);
 }
 
 int read_counts(art_ctx* c, Device& dv, hipStream_t st, art_test_counts* out, bool accumulate) {
@@ -1065,9 +997,6 @@ ART_API void art_destroy(art_ctx* c) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     if (dv.launch_done) (void)hipEventSynchronize(dv.launch_done);  // a device frame on the caller's stream
-    // the context's graphs and their events stay allocated until the process exits (see
-    // enqueue_kernels: destroying an instantiated graph broke later graph launches on ROCm 7.2)
-    if (dv.cap) (void)hipStreamDestroy(dv.cap);
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.exec.release(); dv.pairs.release(); dv.dsp.release(); dv.cones.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
@@ -1392,8 +1321,14 @@ ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
     unsigned long long v[kExecSlots] = {};
     HIP_TRY(c, hipMemcpy(v, dv.exec.p, sizeof v, hipMemcpyDeviceToHost));
     HIP_TRY(c, hipMemset(dv.exec.p, 0, sizeof v));
-    out->sphere += v[kExecSphere]; out->aabb += v[kExecAabb]; out->obb += v[kExecObb]; out->cull_box += v[kExecCullBox];
-    out->cell_entries += v[kExecCellEntries]; out->muffle_fallback += v[kExecMuffleFallback]; out->echo_pairs += v[kExecEchoPairs];
+    for (int k = 0; k < 3; ++k) {  // per kernel family (kExecNearest, kExecEcho, kExecMuffle), then the totals
+      const unsigned long long* g = v + kExecNearest + k * kExecGroup;
+      out->by_kernel[k].sphere += g[kExecSphere]; out->by_kernel[k].aabb += g[kExecAabb]; out->by_kernel[k].obb += g[kExecObb];
+      out->by_kernel[k].cull_box += g[kExecCullBox]; out->by_kernel[k].cell_entries += g[kExecCellEntries];
+      out->sphere += g[kExecSphere]; out->aabb += g[kExecAabb]; out->obb += g[kExecObb]; out->cull_box += g[kExecCullBox];
+      out->cell_entries += g[kExecCellEntries]; out->muffle_fallback += g[kExecMuffleFallback];
+    }
+    out->echo_pairs += v[kExecEchoPairs];
     for (int k = 0; k < kExecBounces; ++k) out->bounce_rays[k] += v[kExecBounce0 + k];
     out->launches += dv.exec_launches;
     dv.exec_launches = 0;
@@ -1414,6 +1349,7 @@ ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {
       HIP_TRY(c, hipEventElapsedTime(&ms, a, b));
       if (u.first == 0) { out->raytrace_ms += ms; frames++; }
       else if (u.first == 1) out->permeate_ms += ms;
+      else if (u.first == 3) { out->nearest_ms += ms; out->nearest_launches++; }
       else out->reduce_ms += ms;
     }
     dv.ev_used.clear();
@@ -1697,6 +1633,7 @@ ART_API int art_colliders_sync(art_ctx* c) {
   c->last_sync.dirty_records = nd;
   c->last_sync.full_prep = (counts_changed || fresh) ? 1 : 0;
   c->last_sync.reallocated = fresh ? 1 : 0;
+  c->last_sync.cells_rebuilt = cells_rebuilt ? 1 : 0;
   c->last_sync.bytes_uploaded = nd ? bytes : 0;
   return ART_OK;
 }

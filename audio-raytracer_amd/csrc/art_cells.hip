@@ -22,6 +22,7 @@
 // muffle_kernel skips entries beyond maxd. A segment longer than far_t (the bound the lists were
 // built for), a degenerate segment, or a target whose lists overflowed tests every collider.
 #include <algorithm>
+#include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
 
@@ -30,6 +31,14 @@
 namespace art {
 
 constexpr float kCellEta = 2e-6f;  // relative deviation of a float muffle ray from its exact segment
+
+// test hooks (read per call): ART_CELLS_MAX_PAIRS lowers the list threshold, ART_CELLS_CAP the
+// entry capacity, so the no-list and dropped-target paths run at small sizes
+static long long env_ll(const char* name, long long dflt) {
+  const char* e = getenv(name);
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? v : dflt;
+}
 
 
 // far_t: the largest distance from target t to the scene's bounds (every muffle segment of t
@@ -90,10 +99,15 @@ struct alignas(16) CellGeo {
 };
 
 // One thread per (target, collider).
+// (grid-stride over the pairs: one launch stays far below HIP's 2^32 work-item limit)
+__device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, long long k, CellGeo* __restrict__ geo);
 __global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb, int T, CellGeo* __restrict__ geo) {
   const int n = sc.ns + sc.na + sc.no;
-  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= (long long)n * T) return;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < (long long)n * T;
+       k += (long long)gridDim.x * blockDim.x)
+    cells_geo_one(sc, cb, n, k, geo);
+}
+__device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, long long k, CellGeo* __restrict__ geo) {
   const int t = (int)(k / n), g = (int)(k - (long long)t * n);
   CellGeo G;
   for (int f = 0; f < 6; ++f) { G.rect[f][0] = 1; G.rect[f][1] = 0; G.rect[f][2] = 1; G.rect[f][3] = 0; }
@@ -167,35 +181,60 @@ __global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb
   geo[k] = G;
 }
 
-// One thread per (target, collider, face, cell row): tests the row's cells of the pair's face
-// rectangle. FILL = false counts per cell; FILL = true writes the entries.
+// One work-item per (target, collider, face, cell row), grid-stride: tests the row's cells of the
+// pair's face rectangle. FILL = false counts per cell (and per target, for the capacity check);
+// FILL = true writes the entries of the targets whose lists fit (cells_fit_kernel).
 template <bool FILL>
 __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restrict__ geo, long long pairs, CellBufs cb, int n) {
-  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long p = k / (6 * kCellG);
-  if (p >= pairs) return;
-  const int fr = (int)(k - p * (6 * kCellG)), f = fr / kCellG, j = fr - f * kCellG;
-  const CellGeo G = geo[p];
-  const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
-  if (j < j0 || j > j1 || i0 > i1) return;
-  const int t = (int)(p / n);
-  const uint32_t ty = G.code >> 28;  // one list per collider type
-  uint32_t* cnt = cb.count + (size_t)t * kCells * 3 + ty;
-  uint32_t* cur = cb.cursor + (size_t)t * kCells * 3 + ty;
-  for (int i = i0; i <= i1; ++i) {
-    const int c = (f * kCellG + j) * kCellG + i;
-    const CellCone cc = cb.cones[c];
-    // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
-    const bool hit = G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
-    if (!hit) continue;
-    if (!FILL) {
-      atomicAdd(cnt + 3 * c, 1u);
-    } else {
-      const uint32_t pos = atomicAdd(cur + 3 * c, 1u);
-      if (pos < cb.cap) cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
-      else cb.ok[t] = 0u;  // overflow: this target's muffle rays test every collider
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < pairs * (6 * kCellG);
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long p = k / (6 * kCellG);
+    const int fr = (int)(k - p * (6 * kCellG)), f = fr / kCellG, j = fr - f * kCellG;
+    const CellGeo G = geo[p];
+    const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
+    if (j < j0 || j > j1 || i0 > i1) continue;
+    const int t = (int)(p / n);
+    if (FILL && !cb.ok[t]) continue;  // dropped by the capacity check: no entries (its counts are 0)
+    const uint32_t ty = G.code >> 28;  // one list per collider type
+    uint32_t* cnt = cb.count + (size_t)t * kCells * 3 + ty;
+    uint32_t* cur = cb.cursor + (size_t)t * kCells * 3 + ty;
+    uint32_t nhit = 0;
+    for (int i = i0; i <= i1; ++i) {
+      const int c = (f * kCellG + j) * kCellG + i;
+      const CellCone cc = cb.cones[c];
+      // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
+      const bool hit = G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
+      if (!hit) continue;
+      if (!FILL) {
+        atomicAdd(cnt + 3 * c, 1u);
+        ++nhit;
+      } else {
+        const uint32_t pos = atomicAdd(cur + 3 * c, 1u);
+        if (pos < cb.cap) cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
+        else cb.ok[t] = 0u;  // (cannot happen after the capacity check; kept as a guard)
+      }
     }
+    if (!FILL && nhit) atomicAdd(cb.tcount + t, (unsigned long long)nhit);
   }
+}
+
+// Capacity check between the count and the fill: targets in order keep their lists while the
+// running total of entries fits the capacity; a target that does not fit (or whose far bound is
+// non-finite) is dropped — ok = 0, its muffle rays test every collider. The kept targets' total is
+// at most the capacity (< 2^32), so the u32 scan of the cell counts cannot wrap.
+__global__ void cells_fit_kernel(CellBufs cb, int T) {
+  if (threadIdx.x != 0) return;
+  unsigned long long run = 0;
+  for (int t = 0; t < T; ++t) {
+    const unsigned long long c = cb.tcount[t];
+    if (cb.ok[t] && run + c <= (unsigned long long)cb.cap) run += c;
+    else cb.ok[t] = 0u;
+  }
+}
+// The dropped targets' cell counts are cleared before the scan.
+__global__ void cells_drop_kernel(CellBufs cb, uint32_t cells) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cells && !cb.ok[i / (kCells * 3)]) cb.count[i] = 0u;
 }
 
 size_t cells_scan_temp_bytes(int T, uint32_t cap) {
@@ -220,30 +259,51 @@ __global__ void cells_key_kernel(CellBufs cb, uint32_t total_cells) {
 // Entry capacity: 128 cells per (target, collider) on average (a collider near its target spans
 // hundreds, a far one a few); a target whose lists do not fit falls back to testing every collider.
 size_t cells_entry_cap(int T, int C) {
+  if (!cells_enabled(T, C)) return 0;
   const size_t want = (size_t)128 * (size_t)T * (size_t)(C > 0 ? C : 1);
-  return std::min<size_t>(std::max<size_t>(want, (size_t)1 << 16), (size_t)1 << 26);
+  return std::min<size_t>(std::min<size_t>(std::max<size_t>(want, (size_t)1 << 16), (size_t)1 << 26),
+                          (size_t)env_ll("ART_CELLS_CAP", 1ll << 26));
 }
+
+// Lists are built when the per-(target, collider) geometry stays within kCellsMaxPairs records
+// (512 MiB of scratch); larger scenes run without lists (every muffle ray tests every collider).
+constexpr long long kCellsMaxPairs = 1ll << 23;
+bool cells_enabled(int T, int C) {
+  return (long long)T * (long long)C <= env_ll("ART_CELLS_MAX_PAIRS", kCellsMaxPairs);
+}
+
+// grid of a grid-stride launch over `items` work-items (at most 2^16 workgroups of 256)
+static unsigned stride_grid(long long items) { return (unsigned)std::max(1ll, std::min((items + 255) / 256, 1ll << 16)); }
 
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   const int T = sc.T, n = sc.ns + sc.na + sc.no;
   const int cells = T * kCells * 3;  // lists: (target, cell, collider type)
   hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.far, cb.ok);
+  sc.cell_start = cb.start;
+  sc.cell_ent = cb.ent_s;
+  sc.cell_far = cb.far;
+  sc.cell_ok = cb.ok;
+  sc.cell_cap = cb.cap;
+  if (cb.cap == 0) {  // no lists for this scene size (cells_enabled): every target tests every collider
+    if (T > 0 && hipMemsetAsync(cb.ok, 0, (size_t)T * sizeof(uint32_t), st) != hipSuccess) return -1;
+    return 0;
+  }
   if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(cb.tcount, 0, (size_t)T * sizeof(unsigned long long), st) != hipSuccess) return -1;
   const long long pairs = (long long)n * T;
   CellGeo* geo = reinterpret_cast<CellGeo*>(cb.geo);
   if (pairs > 0) {
-    hipLaunchKernelGGL(cells_geo_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, st, sc, cb, T, geo);
-    const unsigned rb = (unsigned)((pairs * 6 * kCellG + 255) / 256);
-    hipLaunchKernelGGL(cells_row_kernel<false>, dim3(rb), dim3(256), 0, st, geo, pairs, cb, n);
+    hipLaunchKernelGGL(cells_geo_kernel, dim3(stride_grid(pairs)), dim3(256), 0, st, sc, cb, T, geo);
+    hipLaunchKernelGGL(cells_row_kernel<false>, dim3(stride_grid(pairs * 6 * kCellG)), dim3(256), 0, st, geo, pairs, cb, n);
   }
+  hipLaunchKernelGGL(cells_fit_kernel, dim3(1), dim3(64), 0, st, cb, T);
+  hipLaunchKernelGGL(cells_drop_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, cb, (uint32_t)cells);
   size_t bytes = cb.temp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(cb.temp, bytes, cb.count, cb.start, cells + 1, st) != hipSuccess) return -1;
   if (hipMemcpyAsync(cb.cursor, cb.start, (size_t)cells * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
     return -1;
-  if (pairs > 0) {
-    const unsigned rb = (unsigned)((pairs * 6 * kCellG + 255) / 256);
-    hipLaunchKernelGGL(cells_row_kernel<true>, dim3(rb), dim3(256), 0, st, geo, pairs, cb, n);
-  }
+  if (pairs > 0)
+    hipLaunchKernelGGL(cells_row_kernel<true>, dim3(stride_grid(pairs * 6 * kCellG)), dim3(256), 0, st, geo, pairs, cb, n);
   // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its segment
   {
     const uint32_t span = std::max<uint32_t>(cb.cap, (uint32_t)cells + 1);
@@ -255,14 +315,11 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
                                                     cb.cursor, cb.cursor + 1, 0, 16, st) != hipSuccess)
       return -1;
   }
-  sc.cell_start = cb.start;
-  sc.cell_ent = cb.ent_s;
-  sc.cell_far = cb.far;
-  sc.cell_ok = cb.ok;
-  sc.cell_cap = cb.cap;
-  return 0;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-size_t cells_geo_bytes(int T, int C) { return (size_t)T * (size_t)(C > 0 ? C : 1) * sizeof(CellGeo); }
+size_t cells_geo_bytes(int T, int C) {
+  return cells_enabled(T, C) ? (size_t)T * (size_t)(C > 0 ? C : 1) * sizeof(CellGeo) : 0;
+}
 
 }  // namespace art

@@ -163,12 +163,14 @@ struct CellBufs {
   uint32_t* keys;                 // [2 * cap] sort keys (near_key) and their sorted copy
   float* far;                     // [T]: distance bound of t's segments
   uint32_t* ok;                   // [T]
-  uint32_t cap;
+  unsigned long long* tcount;     // [T] entries per target (count pass), for the capacity check
+  uint32_t cap;                   // entry capacity; 0: no lists (cells_enabled false), every muffle ray tests every collider
   void* temp; size_t temp_bytes;  // hipcub scan / segmented sort storage
   void* geo;                      // [T * C] per-(target, collider) geometry (cells_geo_bytes)
 };
 size_t cells_scan_temp_bytes(int T, uint32_t cap);
 size_t cells_geo_bytes(int T, int C);
+bool cells_enabled(int T, int C);
 size_t cells_entry_cap(int T, int C);
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st);
 
@@ -193,9 +195,12 @@ struct FrameParams {
   unsigned long long* exec;  // executed-work counters (ExecSlot order) or nullptr
 };
 
-// Slots of FrameParams::exec (art_exec_counts order).
+// Slots of FrameParams::exec (art_exec_counts order). The per-test slots 0..5 are written per
+// kernel family at a group offset (nearest traversals, echo traversals, muffle rays); the host
+// sums the groups for the totals and reports each group (art_exec_counts.by_kernel).
 enum ExecSlot { kExecSphere = 0, kExecAabb = 1, kExecObb = 2, kExecCullBox = 3, kExecCellEntries = 4, kExecMuffleFallback = 5,
-                kExecEchoPairs = 6, kExecBounce0 = 8, kExecBounces = 16, kExecSlots = 24 };
+                kExecEchoPairs = 6, kExecBounce0 = 8, kExecBounces = 16, kExecNearest = 24, kExecEcho = 32, kExecMuffle = 40,
+                kExecGroup = 8, kExecSlots = 48 };
 
 // Device counters for the counting variant, in art_test_counts order.
 struct DevCounts { unsigned long long v[9]; };
@@ -226,9 +231,15 @@ struct SideStream {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
+// Timing marks (ART_CTX_TIME_KERNELS): event pairs recorded on the launch stream around each
+// nearest_first_kernel launch, while pairs are left (art_kernel_times.nearest_ms).
+struct NearestMarks {
+  hipEvent_t* ev = nullptr;  // [2 * cap]
+  int cap = 0, used = 0;
+};
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf,
-                          uint32_t* pair_count, hipStream_t st, const SideStream& echo);
+                          uint32_t* pair_count, hipStream_t st, const SideStream& echo, NearestMarks* marks = nullptr);
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, const int2* slot_batch, hipStream_t st);
 void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,

@@ -384,10 +384,10 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     code = k == ~0ull ? kNoHit : (int)(uint32_t)k;
   }
   if (ex) {
-    exec_add(ex, kExecSphere, wave_sum_u32(nt[0]));
-    exec_add(ex, kExecAabb, wave_sum_u32(nt[1]));
-    exec_add(ex, kExecObb, wave_sum_u32(nt[2]));
-    exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nnode));
+    exec_add(ex + kExecNearest, kExecSphere, wave_sum_u32(nt[0]));
+    exec_add(ex + kExecNearest, kExecAabb, wave_sum_u32(nt[1]));
+    exec_add(ex + kExecNearest, kExecObb, wave_sum_u32(nt[2]));
+    exec_add(ex + kExecNearest, kExecCullBox, 4ull * wave_sum_u32(nnode));
   }
 }
 
@@ -934,10 +934,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     reinterpret_cast<uint16_t*>(block)[o.x] = (uint16_t)(o.y & 0xffffu);
   }
   if (ex) {
-    exec_add(ex, kExecSphere, wave_sum_u32(nt[0]));
-    exec_add(ex, kExecAabb, wave_sum_u32(nt[1]));
-    exec_add(ex, kExecObb, wave_sum_u32(nt[2]));
-    exec_add(ex, kExecCullBox, 4ull * wave_sum_u32(nnode));
+    exec_add(ex + kExecEcho, kExecSphere, wave_sum_u32(nt[0]));
+    exec_add(ex + kExecEcho, kExecAabb, wave_sum_u32(nt[1]));
+    exec_add(ex + kExecEcho, kExecObb, wave_sum_u32(nt[2]));
+    exec_add(ex + kExecEcho, kExecCullBox, 4ull * wave_sum_u32(nnode));
   }
 }
 
@@ -1110,11 +1110,11 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
     }
   }
   if (EX) {  // lane-tests executed (each lane's own tests; the loop is per lane)
-    exec_add(fp.exec, kExecSphere, wave_sum_u32(nt[0]));
-    exec_add(fp.exec, kExecAabb, wave_sum_u32(nt[1]));
-    exec_add(fp.exec, kExecObb, wave_sum_u32(nt[2]));
-    exec_add(fp.exec, kExecCellEntries, wave_sum_u32(ne));
-    exec_add(fp.exec, kExecMuffleFallback, wave_sum_u32(nfb));
+    exec_add(fp.exec + kExecMuffle, kExecSphere, wave_sum_u32(nt[0]));
+    exec_add(fp.exec + kExecMuffle, kExecAabb, wave_sum_u32(nt[1]));
+    exec_add(fp.exec + kExecMuffle, kExecObb, wave_sum_u32(nt[2]));
+    exec_add(fp.exec + kExecMuffle, kExecCellEntries, wave_sum_u32(ne));
+    exec_add(fp.exec + kExecMuffle, kExecMuffleFallback, wave_sum_u32(nfb));
   }
 }
 
@@ -1197,7 +1197,7 @@ int fast_fans_per_launch(int R, int H, int T, int TC, uint32_t stride) {
 
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf, uint32_t* pair_count,
-                          hipStream_t st, const SideStream& echo) {
+                          hipStream_t st, const SideStream& echo, NearestMarks* marks) {
   if (fp.S == 0) return;
   const PairBufs pb = pair_bufs(pair_buf, fp);
   const unsigned groups = (unsigned)((size_t)fp.S * ((fp.R + 63) / 64));
@@ -1264,8 +1264,11 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
 #define ART_NEAREST(EX_, OBB_)                                                                                      \
   hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
                      pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr)
+    const bool mark = marks && marks->used < marks->cap;
+    if (mark) (void)hipEventRecord(marks->ev[2 * marks->used], st);
     if (fp.exec) { if (obb) ART_NEAREST(true, true); else ART_NEAREST(true, false); }
     else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
+    if (mark) (void)hipEventRecord(marks->ev[2 * marks->used++ + 1], st);
 #undef ART_NEAREST
     hipStream_t pst = st;
     if (hm && !hm2) {  // (HM2 forks the muffle rays below)

@@ -40,7 +40,9 @@ CULL_OPS = {"cull_box": 14, "cell_entries": 2}
 OPS = {"rt_sphere": 26, "rt_aabb": 34, "rt_obb": 118, "perm_hit_sphere": 26, "perm_hit_aabb": 34, "perm_hit_obb": 134,
        "perm_loss_sphere": 18, "perm_loss_aabb": 33, "perm_loss_obb": 117}
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
-SINGLE_ISSUE_TLOPS = 39.3      # 256 CU x 64 lanes x 2.4 GHz, one non-FMA lane-op per cycle
+# one non-FMA wave64 VALU op issues over 2 cycles per SIMD-32 (MI355X_MICROARCH.md:54, :473):
+# 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-op/s (SURVEY.md 8(d)'s 64 lanes/CU/clk undercounts 2x)
+SINGLE_ISSUE_TLOPS = 78.6
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW" (spec)
 
 
@@ -364,18 +366,34 @@ def lib_sha256():
 
 
 def read_traffic(cfg_index):
-    """HBM bytes per raytrace launch from the PMC pass (tools/pmc_traffic.sh, FETCH_SIZE and
-    WRITE_SIZE in separate passes) — used only when it was measured on this exact libart.so."""
+    """HBM bytes per raytrace frame from the PMC passes (tools/gpu_round.sh -> tools/prof_summary.py,
+    FETCH_SIZE and WRITE_SIZE in separate passes), total and per kernel — used only when they were
+    measured on this exact libart.so."""
     prof = os.path.join(ROOT, "profiles", f"traffic_config{cfg_index}.json")
     if not os.path.exists(prof):
-        return None, "no PMC traffic file for this config"
+        return None, {}, "no PMC traffic file for this config"
     try:
         t = json.load(open(prof))
     except Exception as e:  # noqa: BLE001
-        return None, f"unreadable traffic file: {e}"
+        return None, {}, f"unreadable traffic file: {e}"
     if t.get("lib_sha256") != lib_sha256():
-        return None, f"traffic file measured on another build ({str(t.get('lib_sha256'))[:12]}); not used"
-    return t.get("raytrace_bytes_per_launch"), f"PMC pass on this build (lib sha256 {t['lib_sha256'][:12]})"
+        return None, {}, f"traffic file measured on another build ({str(t.get('lib_sha256'))[:12]}); not used"
+    return (t.get("raytrace_bytes_per_launch"), t.get("bytes_per_frame_by_kernel", {}),
+            f"PMC pass on this build (lib sha256 {t['lib_sha256'][:12]})")
+
+
+def stage_kernels(cfg, S, has_obb):
+    """The kernels of the timed raytrace stage as launch_raytrace_fast (csrc/art_trace.hip) picks
+    them for this frame shape (no hit outputs, as the bench launches it)."""
+    obb = "true" if has_obb else "false"
+    groups = S * ((cfg.R + 63) // 64)
+    if cfg.H > 1:
+        return (f"per bounce: nearest_first_kernel<false, {obb}> -> path_kernel<false, true>, that bounce's echo "
+                f"vis_kernel<false, {obb}, false> on the side stream; then muffle_kernel<false, {obb}, false>")
+    if groups <= 8 * 256:  # one round of echo waves on 256 CUs: echo + muffle from the nearest hits, one launch
+        return f"nearest_first_kernel<false, {obb}> -> echo_muffle_kernel<false, {obb}> (one stream, no path kernel)"
+    return (f"nearest_first_kernel<false, {obb}> -> path_kernel<false, false> -> echo vis_kernel<false, {obb}, false>; "
+            f"muffle_kernel<false, {obb}, false> on the side stream")
 
 
 def jitter_records(rng, recs, scale):
@@ -659,12 +677,23 @@ def main():
               executed["cull_box"] * CULL_OPS["cull_box"] + executed["cell_entries"] * CULL_OPS["cell_entries"]) / ex_launches
     ex_tests = (executed["sphere"] + executed["aabb"] + executed["obb"]) / ex_launches
     ex_tflops = ex_ops / (rt_ms * 1e-3) / 1e12
+
+    def kernel_ops(k):  # executed ops of one kernel family per frame (art_exec_counts.by_kernel)
+        b = executed["by_kernel"][k]
+        return (b["sphere"] * OPS["rt_sphere"] + b["aabb"] * OPS["rt_aabb"] + b["obb"] * OPS["rt_obb"] +
+                b["cull_box"] * CULL_OPS["cull_box"] + b["cell_entries"] * CULL_OPS["cell_entries"]) / ex_launches
+    by_kernel_ops = {k: kernel_ops(k) for k in abi.EXEC_KERNELS}
+    # the dominant kernel: nearest_first_kernel, timed live by HIP events around its launches on the
+    # launch stream (art_kernel_times.nearest_ms, every 8th timed step)
+    near_ms = ktimes["nearest_ms"] / n_rt
+    near_tflops = by_kernel_ops["nearest"] / (near_ms * 1e-3) / 1e12 if near_ms > 0 else 0.0
     # algorithmic HBM bytes of one raytrace launch: the decoded collider records, directions,
     # origins and the fans' result blocks (everything else is L2-resident scratch)
     rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 32 + scene.obbs.size * 64  # hot records
     alg_bytes = rec_bytes + cfg.R * 6 + S * 12 + S * lay["stride"]
     hbm_gbs = alg_bytes / (rt_ms * 1e-3) / 1e9
-    traffic, traffic_note = read_traffic(cfg.index)
+    traffic, traffic_by_kernel, traffic_note = read_traffic(cfg.index)
+    near_traffic = next((v for k, v in traffic_by_kernel.items() if k.startswith("nearest_first_kernel")), None)
 
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
@@ -696,26 +725,44 @@ def main():
         "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
         "allgather_note": "HIP events on the launch stream around the all-gather of every 8th timed step, max over "
                           "ranks; the step time includes it" if world > 1 else None,
-        "roofline": {"bound": "valu", "achieved": ex_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic, "traffic_note": traffic_note,
-                     "kernel": "raytrace stage: nearest_first_kernel + path_kernel per bounce, echo vis_kernel (side stream) + muffle_kernel",
-                     "kernel_ms": rt_ms,
-                     "note": "FP32 VALU roof (no MFMA-shaped work). achieved = ops the kernels executed per launch (exact "
-                             "tests x SURVEY.md 8(d) ops per test, lane-tests = wave-level tests x 64, plus broad-phase "
-                             "bound tests at CULL_OPS) / raytrace-stage time (HIP events on the launch stream)",
-                     "single_issue": {"achieved": ex_ops / (rt_ms * 1e-3) / 1e12, "peak": SINGLE_ISSUE_TLOPS,
-                                      "unit": "T lane-op/s", "frac": ex_ops / (rt_ms * 1e-3) / 1e12 / SINGLE_ISSUE_TLOPS},
+        "roofline": {"bound": "valu", "kernel": f"nearest_first_kernel<false, {'true' if scene.obbs.size > 0 else 'false'}>",
+                     "achieved": near_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": near_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": near_traffic,
+                     "kernel_ms": near_ms, "launches_per_frame": ktimes["nearest_launches"] / n_rt,
+                     "ops_per_frame": by_kernel_ops["nearest"],
+                     "note": "the dominant kernel (nearest-hit BVH traversal; FP32 VALU roof, no MFMA-shaped work). "
+                             "achieved = ops it executed per frame (exact lane-tests x SURVEY.md 8(d) ops per test + "
+                             "BVH box tests x 14, art_exec_counts.by_kernel[0]) / its duration per frame (HIP events "
+                             "around its launches on the launch stream, every 8th timed step); traffic = its HBM bytes "
+                             "per frame from same-build FETCH_SIZE / WRITE_SIZE passes (" + traffic_note + ")",
+                     "single_issue": {"achieved": near_tflops, "peak": SINGLE_ISSUE_TLOPS, "unit": "T lane-op/s",
+                                      "frac": near_tflops / SINGLE_ISSUE_TLOPS,
+                                      "note": "one non-FMA lane-op per lane per issue: 256 CU x 128 lanes/clk x 2.4 GHz"},
+                     "stage": {"kernels": stage_kernels(cfg, S, scene.obbs.size > 0), "kernel_ms": rt_ms, "achieved": ex_tflops,
+                               "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS,
+                               "single_issue_frac": ex_ops / (rt_ms * 1e-3) / 1e12 / SINGLE_ISSUE_TLOPS,
+                               "traffic": traffic, "traffic_by_kernel": traffic_by_kernel, "traffic_note": traffic_note,
+                               "note": "the whole raytrace stage (HIP events on the launch stream): executed ops of "
+                                       "every kernel / stage time"},
                      "executed": {"ops_per_launch": ex_ops, "exact_lane_tests_per_launch": ex_tests,
+                                  "ops_per_frame_by_kernel": by_kernel_ops,
                                   "counts": {k: v // ex_launches for k, v in executed.items()
-                                             if k not in ("launches", "bounce_rays")},
+                                             if k not in ("launches", "bounce_rays", "by_kernel")},
+                                  "counts_by_kernel": {k: {f: v // ex_launches for f, v in d.items()}
+                                                       for k, d in executed["by_kernel"].items()},
                                   "bounce_rays": [v // ex_launches for v in executed["bounce_rays"][:cfg.H]]},
                      "equivalent": {"achieved": bf_tflops, "frac": bf_tflops / FP32_VALU_PEAK_TFLOPS,
                                     "reference_tests_per_launch": tests_rank,
                                     "note": "brute-force-equivalent: the reference algorithm's tests x ops per test / "
                                             "stage time; the broad phase skips most of them, so this is not a roofline"},
                      "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
-                             "algorithmic_bytes": alg_bytes}},
-        "kernel_ms": {"raytrace": rt_ms, "permeate": ktimes["permeate_ms"] / n_rt, "reduce": ktimes["reduce_ms"] / n_rt},
+                             "algorithmic_bytes": alg_bytes,
+                             "counter_gbs": traffic / (rt_ms * 1e-3) / 1e9 if traffic else None,
+                             "counter_frac": traffic / (rt_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+                             "note": "achieved = algorithmic bytes / stage time; counter_gbs = the stage's PMC HBM bytes "
+                                     "(2 x FETCH_SIZE + WRITE_SIZE, same build) / stage time"}},
+        "kernel_ms": {"raytrace": rt_ms, "nearest": near_ms, "permeate": ktimes["permeate_ms"] / n_rt,
+                      "reduce": ktimes["reduce_ms"] / n_rt},
         "lib_sha256": lib_sha256(),
         "cpu_baseline": cpu,
     }

@@ -80,7 +80,7 @@ typedef struct {
     int32_t dirty_records;   /* records uploaded and decoded */
     int32_t full_prep;       /* 1 if a count changed, so every record's bounds were rebuilt on the device */
     int32_t reallocated;     /* 1 if the device capacity grew (every record uploaded) */
-    int32_t reserved;
+    int32_t cells_rebuilt;   /* 1 if the muffle direction-cell lists were rebuilt (a record left its motion slack) */
     uint64_t bytes_uploaded; /* H2D bytes of the sync (indices + records) */
 } art_collider_sync_stats;
 

@@ -37,6 +37,8 @@ typedef struct {
 typedef struct {
     double raytrace_ms, permeate_ms, reduce_ms; /* summed hipEvent durations */
     int32_t launches;                           /* frames timed */
+    int32_t nearest_launches;                   /* nearest_first_kernel launches timed (ABI 2.3) */
+    double nearest_ms;                          /* summed durations of those launches (ABI 2.3) */
 } art_kernel_times;
 
 /* Record hipEvents around every kernel of art_launch_device (art_set_flags). */
@@ -47,11 +49,8 @@ typedef struct {
 /* (0x8, 0x40 and 0x80 selected round-1 alternative raytrace implementations; they are gone and
  * the bits are reserved.) */
 
-/* Replay each frame's launch sequence as a captured hipGraph (captured on first use, replayed while
- * the scene, buffers, fan count and flags stay the same; ART_GRAPH=1 in the environment turns it on
- * for every context). Off by default: on ROCm 7.2 the replay measured slower than direct launches
- * and graph lifetimes interact badly with hipGraphExecDestroy. */
-#define ART_CTX_GRAPH 0x100u
+/* (0x100 selected hipGraph replay of a frame's launch sequence, ABI 2.1-2.2; it measured no faster
+ * than direct launches and is gone, the bit is reserved.) */
 
 ART_API int art_fan_layout_get(const art_frame_desc* desc, uint32_t out_flags, art_fan_layout* out);
 
@@ -94,6 +93,13 @@ typedef struct {
     uint64_t muffle_fallback;        /* muffle rays tested against every collider (no usable cell list) */
     uint64_t echo_pairs;             /* echo rays left to the BVH echo traversal (not decided by the nearest pass) */
     uint64_t bounce_rays[16];        /* live rays the nearest traversal traced per bounce (bounce k, k < 16) */
+    /* The first five counters split by kernel family (ABI 2.3): [0] the nearest-hit traversals
+     * (nearest_first_kernel), [1] the echo any-hit traversals (vis_kernel, the echo half of
+     * echo_muffle_kernel), [2] the muffle rays (muffle_kernel, the muffle half of echo_muffle_kernel).
+     * Each field above is the sum of its three entries. */
+    struct {
+        uint64_t sphere, aabb, obb, cull_box, cell_entries;
+    } by_kernel[3];
 } art_exec_counts;
 /* Executed-work counters since the last call (needs ART_CTX_COUNT_EXECUTED); synchronizes. */
 ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);

@@ -54,10 +54,12 @@ def test_struct_sizes_match_csharp_layouts():
     offs = {n: getattr(abi.art_fan, n).offset for n, _ in abi.art_fan._fields_}
     assert offs["ray_hit_counts"] == 64 and offs["ray_hit_ids"] == 72  # appended after the editor arrays
     assert C.sizeof(abi.art_fan_layout) == 9 * 4
+    assert C.sizeof(abi.art_exec_counts) == 8 * 8 + 16 * 8 + 3 * 5 * 8  # 2.3: by_kernel appended
 
 
 def test_version():
-    assert art.load_library().art_version() >> 16 == 2  # 2.0: art_fan.ray_hit_ids
+    v = art.load_library().art_version()
+    assert v >> 16 == 2 and v & 0xffff >= 3  # 2.0: art_fan.ray_hit_ids; 2.3: art_exec_counts.by_kernel
 
 
 def test_no_gpu_fails_loudly():

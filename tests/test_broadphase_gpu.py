@@ -213,3 +213,49 @@ def test_bvh_exact_ties_across_leaves(ctx):
     for k in range(6):
         first = int(np.flatnonzero((s_pos == axes[k] * 10.0).all(1)).min())
         assert (o_gpu.hit_ids[:, k * 3] == abi.hit_id(abi.ART_COLLIDER_SPHERE, first)).all(), k
+
+
+# ---------------------------------------------------------------- muffle cell-list limits
+def _targets_scene(cfg_index, S, R, scale, T, seed):
+    scene, org, params = art.synth(art.CONFIGS[cfg_index], S=S, R=R, C_scale=scale)
+    rng = np.random.default_rng(seed)
+    sc = art.Scene(dirs=scene.dirs, targets=rng.uniform(-20, 20, (T, 3)).astype(np.float32),
+                   spheres=scene.spheres.copy(), aabbs=scene.aabbs.copy(), obbs=scene.obbs.copy())
+    for arr in (sc.spheres, sc.aabbs, sc.obbs):
+        arr["audio_target_id"] = rng.integers(-1, T, arr.size).astype(np.int16)
+    return sc, org, params
+
+
+def _muffle_fallback_rays(sc, params, org):
+    with art.Context(1) as c:
+        c.set_flags(abi.ART_CTX_COUNT_EXECUTED)
+        c.executed_counts()
+        c.run(art.Frame(sc, params, org, art.FanOutputs(org.shape[0], sc.R, params.max_hits_per_ray, sc.T,
+                                                         params.thread_count, dsp=params.dsp is not None)))
+        return c.executed_counts()["muffle_fallback"]
+
+
+@pytest.mark.parametrize("hook,value", [("ART_CELLS_MAX_PAIRS", "100"), ("ART_CELLS_CAP", "3000")])
+def test_cell_lists_disabled_or_overflowing(monkeypatch, hook, value):
+    """Scenes past the list limits: above the (target, collider) pair threshold the lists
+    are not built and every muffle ray tests every collider; past the entry capacity the targets that
+    do not fit are dropped in order (the u32 scan of the kept counts cannot wrap) and only theirs fall
+    back. Both lowered here by the test hooks; every output equals the oracle (CanRaySeeAudioTarget
+    AudioRaytracerJobBatched.cs:405-449), and the fallback is seen in the executed counts."""
+    sc, org, params = _targets_scene(5, 4, 128, 0.25, 6, 11)
+    assert _muffle_fallback_rays(sc, params, org) == 0
+    monkeypatch.setenv(hook, value)
+    with art.Context(1) as c:  # a fresh context: the scene (and its lists) is rebuilt under the hook
+        gpu_vs_oracle(c, sc, params, org, hits=True)
+    assert _muffle_fallback_rays(sc, params, org) > 0
+
+
+def test_cell_lists_threshold_real_size():
+    """T * C just above the 2^23-pair threshold (256 targets x 32,784 colliders): the lists are skipped
+    (no 512-MiB scratch, no launch past HIP's 2^32 work-item limit) and the frame still equals the
+    oracle; just below it (255 targets) the lists are built and used."""
+    for T, scale in ((256, 32784 / 4096), (255, 32784 / 4096)):
+        sc, org, params = _targets_scene(2, 1, 32, scale, T, 5)
+        assert T * sc.C > (1 << 23) if T == 256 else T * sc.C <= (1 << 23), sc.C
+        with art.Context(1) as c:
+            gpu_vs_oracle(c, sc, params, org, hits=False, counts=False)

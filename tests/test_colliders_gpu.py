@@ -384,8 +384,15 @@ def test_small_moves_keep_cell_lists(fresh_ctx, ci):
                 for j, i in enumerate(ids):
                     store.set(k, int(i), recs[j])
                     model.set(k, int(i), recs[j])
-            store.sync()
+            stats = store.sync()
             model.synced()
+            # the lists are kept while the moves stay in the slack (the first rounds: every record
+            # within 0.05 per axis of the records the lists were built from), rebuilt after the large
+            # move and the resize (art_collider_sync_stats.cells_rebuilt)
+            if rnd in (0, 1):
+                assert stats["cells_rebuilt"] == 0, (rnd, stats)
+            if scale in (2.0, "resize"):
+                assert stats["cells_rebuilt"] == 1, (rnd, stats)
             blk = torch.zeros(8 * lay["stride"], dtype=torch.uint8, device=dev)
             fresh_ctx.launch_device(d_org.data_ptr(), 8, blk.data_ptr(), 0, st)
             torch.cuda.synchronize()

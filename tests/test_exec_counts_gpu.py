@@ -44,4 +44,11 @@ def test_bounce_rays_bounded_by_hit_counts(cfg_index, S, R, scale):
         assert int((hc > k).sum()) <= br[k] <= int((hc >= k).sum()), (k, br[:H])
     assert all(v == 0 for v in br[H:])
     assert ex["sphere"] + ex["aabb"] + ex["obb"] > 0 and ex["cull_box"] > 0
+    # the per-kernel split sums to the totals; box culls come from the two traversals only,
+    # list entries from the muffle rays only
+    bk = ex["by_kernel"]
+    for f in ("sphere", "aabb", "obb", "cull_box", "cell_entries"):
+        assert sum(bk[k][f] for k in abi.EXEC_KERNELS) == ex[f], f
+    assert bk["nearest"]["cull_box"] > 0 and bk["echo"]["cull_box"] > 0 and bk["muffle"]["cull_box"] == 0
+    assert bk["nearest"]["cell_entries"] == 0 and bk["echo"]["cell_entries"] == 0
     assert again["launches"] == 0 and all(v == 0 for v in again["bounce_rays"])

@@ -17,5 +17,5 @@ for spec in "$@"; do
   echo "== $v"
   python3 tools/kstats.py "$out/trace/run_kernel_stats.csv" > "$out/kstats.txt"; sed -n 1,6p "$out/kstats.txt"
   env "${envset[@]}" ART_LIB=$lib timeout -k 10 200 python bench.py --config $cfg --no-cpu-baseline --no-dynamic --frames 5 > "$out/bench.log" 2>&1
-  tail -1 "$out/bench.log" | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); c=r['roofline']['executed']['counts']; print('ms_per_step %.4f stage %.4f echo_pairs %s cells %s fb %s' % (r['ms_per_step'], r['kernel_ms']['raytrace'], c.get('echo_pairs'), c.get('cell_entries'), c.get('muffle_fallback')))"
+  tail -1 "$out/bench.log" | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); c=r['roofline']['executed']['counts']; print('ms_per_step %.4f stage %.4f nearest %.4f echo_pairs %s cells %s fb %s' % (r['ms_per_step'], r['kernel_ms']['raytrace'], r['kernel_ms']['nearest'], c.get('echo_pairs'), c.get('cell_entries'), c.get('muffle_fallback')))"
 done

@@ -88,6 +88,7 @@ def main():
             return sum(v) / len(v) * max(1, round(len(v) / ref)) if v else 0.0
         fetch_kb = sum(per_frame(k, "FETCH_SIZE") for k in stage)
         write_kb = sum(per_frame(k, "WRITE_SIZE") for k in stage)
+        per_kernel = {k: (2.0 * per_frame(k, "FETCH_SIZE") + per_frame(k, "WRITE_SIZE")) * 1024.0 for k in sorted(stage)}
         rec = {
             "kernels": sorted(stage),
             "fetch_size_kb_raw": fetch_kb,
@@ -95,6 +96,7 @@ def main():
             # MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE reports half the bytes of a
             # wide read (64 B tallied per 128-B request) -> double it; WRITE_SIZE is exact.
             "raytrace_bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0,
+            "bytes_per_frame_by_kernel": per_kernel,
             "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024; FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 note",
             "source": f"profiles/{tag}_pmc.csv (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --config {cfg})",
             "config": cfg,
