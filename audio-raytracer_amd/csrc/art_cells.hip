@@ -184,22 +184,25 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, lon
 // One work-item per (target, collider, face, cell row), grid-stride: tests the row's cells of the
 // pair's face rectangle. FILL = false counts per cell (and per target, for the capacity check);
 // FILL = true writes the entries of the targets whose lists fit (cells_fit_kernel).
+// The 6 * kCellG = 192 rows of a pair are 3 whole waves (the work-item count is a multiple of 64),
+// so a wave's target is uniform and its entries per target are summed before one atomic.
 template <bool FILL>
 __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restrict__ geo, long long pairs, CellBufs cb, int n) {
+  static_assert((6 * kCellG) % 64 == 0, "a pair's rows are whole waves");
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < pairs * (6 * kCellG);
        k += (long long)gridDim.x * blockDim.x) {
     const long long p = k / (6 * kCellG);
     const int fr = (int)(k - p * (6 * kCellG)), f = fr / kCellG, j = fr - f * kCellG;
+    const int t = (int)(p / n);
     const CellGeo G = geo[p];
     const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
-    if (j < j0 || j > j1 || i0 > i1) continue;
-    const int t = (int)(p / n);
-    if (FILL && !cb.ok[t]) continue;  // dropped by the capacity check: no entries (its counts are 0)
+    uint32_t nhit = 0;
+    // (rows outside the pair's face rectangle, and the dropped targets' rows in the fill pass, test nothing)
+    const bool rows = !(j < j0 || j > j1 || i0 > i1) && (!FILL || cb.ok[t]);
     const uint32_t ty = G.code >> 28;  // one list per collider type
     uint32_t* cnt = cb.count + (size_t)t * kCells * 3 + ty;
     uint32_t* cur = cb.cursor + (size_t)t * kCells * 3 + ty;
-    uint32_t nhit = 0;
-    for (int i = i0; i <= i1; ++i) {
+    for (int i = i0; rows && i <= i1; ++i) {
       const int c = (f * kCellG + j) * kCellG + i;
       const CellCone cc = cb.cones[c];
       // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
@@ -214,7 +217,10 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
         else cb.ok[t] = 0u;  // (cannot happen after the capacity check; kept as a guard)
       }
     }
-    if (!FILL && nhit) atomicAdd(cb.tcount + t, (unsigned long long)nhit);
+    if (!FILL) {  // wave-uniform target
+      const unsigned long long sum = wave_sum_u32(nhit);
+      if ((threadIdx.x & 63) == 0 && sum) atomicAdd(cb.tcount + t, sum);
+    }
   }
 }
 

@@ -18,6 +18,7 @@
 // nearest hit is the (distance, reference order) minimum, any-hit verdicts are ORs.
 #include <algorithm>
 #include <cstdio>
+#include <type_traits>
 #include <cstdlib>
 
 #include "art_device_fns.hpp"
@@ -154,23 +155,23 @@ __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
 // entered lane counts them. No ballots: every value is a quad DPP reduction (measured 3 % faster in
 // the nearest traversal; the echo any-hit keeps its ballot form, index order, which measured 6 %
 // faster there than this near-first form).
-__device__ __forceinline__ void quad_descend(bool enter, float en, bool force, int qd, int c0, uint32_t* my, int& g,
-                                             int& sp) {
+// Stack entries carry the child's entry bits (a lower bound of its entry: the key's low bits
+// cleared), so a pop drops the subtrees whose entry lies past the bound found meanwhile without
+// loading their children. Returns false when no child is entered (the caller pops).
+__device__ __forceinline__ bool quad_descend(bool enter, float en, bool force, int qd, int c0, uint2* my, int& g,
+                                             float& gen, int& sp) {
   const uint32_t key = enter ? (((force ? 0u : (uint32_t)__float_as_int(en)) & ~3u) | (uint32_t)qd) : 0xffffffffu;
   const uint32_t k1 = (uint32_t)quad_perm<kQuadRot1>((int)key), k2 = (uint32_t)quad_perm<kQuadXor2>((int)key),
                  k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
   const int rank = (int)(k1 < key) + (int)(k2 < key) + (int)(k3 < key);
   const uint32_t kmin = min(min(key, k1), min(k2, k3));
   const int nent = quad_max_i32(enter ? rank + 1 : 0);
-  if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
-  if (nent) {
-    g = c0 + (int)(kmin & 3u);
-    sp += nent - 1;
-  } else {  // branch-free pop: the stack slot is read unconditionally (clamped), -1 when empty
-    const int t = (int)my[sp > 0 ? sp - 1 : 0];
-    g = sp > 0 ? t : -1;
-    sp = sp > 0 ? sp - 1 : 0;
-  }
+  if (enter && rank > 0) my[sp + nent - 1 - rank] = make_uint2((uint32_t)(c0 + qd), key & ~3u);
+  if (!nent) return false;
+  g = c0 + (int)(kmin & 3u);
+  gen = __uint_as_float(kmin & ~3u);
+  sp += nent - 1;
+  return true;
 }
 
 // Exact test of leaf slot `sl` (64 B: the hot record's test fields and the order code, art_bvh.hip
@@ -200,14 +201,22 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
     ++nt[1];
     return aabb_test<false>(s, r, dist);
   }
+  // RayIntersectsOBB (:314-320) in the order that keeps the fewest values live: the rotated
+  // direction's reciprocals first (the direction dies), then the rotated origin, and the local
+  // bounds fetched only then (same operations as obb_test)
+  quat q;
+  q.x = qa.w; q.y = qb.x; q.z = qb.y; q.w = qb.z;
+  const vec3 ld3 = qmul(q, s.d);
+  const float ix = 1.0f / ld3.x, iy = 1.0f / ld3.y, iz = 1.0f / ld3.z;
+  const vec3 lo = qmul(q, s.o - mk3(qa.x, qa.y, qa.z));
+  __builtin_amdgcn_sched_barrier(0);
   const float4 qc = ld(2), qe = ld(3);
-  ObbRec r;
-  r.cx = qa.x; r.cy = qa.y; r.cz = qa.z;
-  r.qx = qa.w; r.qy = qb.x; r.qz = qb.y; r.qw = qb.z;
-  r.lmnx = qc.x; r.lmny = qc.y; r.lmnz = qc.z; r.lmxx = qc.w; r.lmxy = qe.x; r.lmxz = qe.y;
   tid = __float_as_int(qe.z);
   ++nt[2];
-  return obb_test<false>(s, r, stored_q(r), dist);
+  float tNear, tFar;
+  const bool hit = slab<false>(lo.x, lo.y, lo.z, ix, iy, iz, qc.x, qc.y, qc.z, qc.w, qe.x, qe.y, tNear, tFar);
+  dist = tNear > 0.0f ? tNear : tFar;
+  return hit;
 }
 
 // Work sharing inside a wave (nearest and echo traversals): a wave lasts as long as its longest
@@ -234,6 +243,11 @@ template <bool EX, bool OBB>
 constexpr int kNearestWaves = EX ? 6 : (OBB ? ART_NEAREST_OBB_WAVES : 8);
 template <bool EX, bool OBB>
 constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
+// echo_muffle_kernel<false, true> (the muffle walk's OBB records need 72 VGPRs): 6 waves per SIMD
+// without spills; 8 spills 3 VGPRs (outside the traversal loops' divergent regions)
+#ifndef ART_ECHO_MUFFLE_OBB_WAVES
+#define ART_ECHO_MUFFLE_OBB_WAVES 6
+#endif
 // k-th (0-based) set bit of m, k < popcount(m).
 __device__ __forceinline__ int select_bit(unsigned long long m, int k) {
   int pos = 0;
@@ -259,33 +273,41 @@ __device__ __forceinline__ unsigned long long nearest_key(float d, int code) {
 // bits, order); the two zeros compare equal, as in the reference's `<`, and the path kernel
 // re-evaluates a zero distance).
 template <bool EX, bool OBB>
-__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint32_t* my,
+__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint2* my,
                                                   int* s_bound, unsigned long long* s_key, float& best, int& code,
                                                   unsigned long long* ex) {
   const int qd = lane & 3, wq = lane >> 2;
-  uint32_t* const s_wave = my - wq * kBvhStack;
+  uint2* const s_wave = my - wq * kBvhStack;
   best = FLT_MAX;
   code = kNoHit;
   if (sc.bvh_levels == 0) return;  // no colliders: every ray misses
+  if (ART_NEAREST_STEAL && qd == 0) s_key[wq] = ~0ull;  // the ray's shared result key, opened before the loop
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
+  float gen = 0.0f;      // entry of node g (a lower bound), checked against the bound after leaf tests
   float lim = FLT_MAX;   // pruning bound: best, and (shared work) the other quads' results for the ray
   bool shared = false;   // wave-uniform: work was shared in this wave
   float mybest = FLT_MAX;  // this quad's own (distance, order) minimum over the leaves it tested
   int mycode = kNoHit;
   unsigned nsteps = 0;
   (void)nsteps;
-  // branch-free pop of entries [bp, sp): the slot is read unconditionally (clamped), -1 when empty
+  // pop of entries [bp, sp), dropping those entered past the bound (a winner or tie lies strictly
+  // after the entry, so such a subtree holds neither); -1 when none is left
   auto pop = [&]() {
-    const bool has = sp > bp;
-    const int t = (int)my[has ? sp - 1 : 0];
-    g = has ? t : -1;
-    sp = has ? sp - 1 : sp;
-    if (sp == bp) sp = bp = 0;
+    for (;;) {
+      if (sp <= bp) { g = -1; sp = bp = 0; return; }
+      const uint2 t = my[--sp];
+      if (__uint_as_float(t.y) <= lim) {
+        g = (int)t.x;
+        gen = __uint_as_float(t.y);
+        if (sp == bp) sp = bp = 0;
+        return;
+      }
+    }
   };
   // A child is entered when its widened box is entered at or before the bound (a winner or tie
   // lies strictly after every ancestor's entry); quad_descend orders the entered ones.
@@ -298,8 +320,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
     const bool enter = (r.lox <= r.hix) & (force | (h & (en <= lim)));  // bitwise: no branch
-    quad_descend(enter, en, force, qd, c0, my, g, sp);
-    if (sp == bp) sp = bp = 0;
+    if (!quad_descend(enter, en, force, qd, c0, my, g, gen, sp)) pop();
   };
   auto leaf_step = [&](int leaf) {
     ART_DIAG_STEP(nsteps);
@@ -336,22 +357,27 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     if (ART_NEAREST_STEAL) {
       const unsigned long long donors = __ballot(sp > bp) & kQuad0, idle = ~act & kQuad0;
       if (donors && idle) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
-        if (!shared) {       // publish every ray's bound once, open its result key
+        if (!shared) {       // publish every ray's bound once
           shared = true;
-          if (qd == 0) { s_bound[wq] = __float_as_int(lim); s_key[wq] = ~0ull; }
+          if (qd == 0) s_bound[wq] = __float_as_int(lim);
         }
-        const unsigned long long below = (1ull << (lane & ~3)) - 1ull;
+        // (the quad's lane masks are recomputed here, not hoisted out of the loop: four live VGPRs)
+        int l4 = lane & ~3;
+        asm volatile("" : "+v"(l4));
+        const unsigned long long below = (1ull << l4) - 1ull;
         const int ir = __popcll(idle & below), dr = __popcll(donors & below);
-        const bool thief = (act >> (lane & ~3) & 1ull) == 0ull && ir < __popcll(donors);
+        const bool thief = (act >> l4 & 1ull) == 0ull && ir < __popcll(donors);
         const bool robbed = sp > bp && dr < __popcll(idle);
-        const int src = (thief ? select_bit(donors, ir) : (lane & ~3)) + qd;
+        const int src = (thief ? select_bit(donors, ir) : l4) + qd;
         const int dbp = __shfl(bp, src), dhome = __shfl(home, src);
         const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
         const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
         const float dlim = __shfl(lim, src);
         if (thief && mycode != kNoHit && qd == 0) atomicMin(s_key + home, nearest_key(mybest, mycode));
         if (thief) {  // the ray's derived values are recomputed as the home computed them
-          g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
+          const uint2 t = s_wave[(src >> 2) * kBvhStack + dbp];
+          g = (int)t.x;
+          gen = __uint_as_float(t.y);
           sp = bp = 0;
           home = dhome;
           s = make_seg(mk3(ox, oy, oz), mk3(dx, dy, dz));
@@ -364,13 +390,18 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
       }
       if (shared) lim = fminf(lim, __int_as_float(s_bound[home]));
     }
+    if (g >= 0 && gen > lim) pop();  // the current node, entered before the last leaf tests lowered the bound
+    float pend_en = 0.0f;
     for (;;) {
-      if (g >= leaf0 && pend < 0) { pend = g; pop(); }
+      if (g >= leaf0 && pend < 0) { pend = g; pend_en = gen; pop(); }
       const bool inner = g >= 0 && g < leaf0;
       if (!__any(inner) || !__any(pend < 0 && g >= 0)) break;
       if (inner) inner_step();
     }
-    if (pend >= 0) { leaf_step(pend); pend = -1; }
+    if (pend >= 0) {  // (a parked leaf entered past the bound holds no winner)
+      if (pend_en <= lim) leaf_step(pend);
+      pend = -1;
+    }
   }
 #ifdef ART_DIAG
   if (qd == 0 && alive) diag_add(2, nsteps);
@@ -416,7 +447,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
     uint32_t* __restrict__ counters) {
-  __shared__ uint32_t s_stk[kBvhStack * 64];
+  __shared__ uint2 s_stk[kBvhStack * 64];
   __shared__ int s_bound[64];
   __shared__ unsigned long long s_key[64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -424,7 +455,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   const int ngroups = fp.S * nrb;
   const int g = blockIdx.x;
   const int rr = 16 * w + (lane >> 2);
-  uint32_t* my = s_stk + rr * kBvhStack;
+  uint2* my = s_stk + rr * kBvhStack;
   unsigned long long* ex = EX ? fp.exec : nullptr;
   float best;
   int code;
@@ -444,6 +475,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
     alive = ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
     write = ok;
     out = i;
+    asm volatile("" : "+v"(out));  // (a 32-bit copy, apart from the 64-bit state offset above)
   } else {
     if (state && blockIdx.x == 0 && threadIdx.x < 2 * kLiveCounters)  // multi-hit frame: clear the counters
       live_list(state, ngroups)[(size_t)ngroups * 64 + threadIdx.x] = 0u;
@@ -466,6 +498,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   const unsigned long long t0 = clock64();
 #endif
   quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code, ex);
+  // (the ray slot stays a 32-bit value across the traversal: an opaque copy keeps the compiler from
+  // widening it to a 64-bit offset before the loop, two more live VGPRs)
+  asm volatile("" : "+v"(out));
   if ((lane & 3) == 0 && write) hits[out] = make_int2(__float_as_int(best), code);
 #ifdef ART_DIAG
   if (lane == 0) diag_add(0, clock64() - t0);
@@ -870,11 +905,13 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     if (!act) break;
     const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
     if (ART_VIS_STEAL && donors && idle) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
-      const unsigned long long below = (1ull << (lane & ~3)) - 1ull;
+      int l4 = lane & ~3;
+      asm volatile("" : "+v"(l4));  // (recomputed here, not hoisted out of the loop)
+      const unsigned long long below = (1ull << l4) - 1ull;
       const int ir = __popcll(idle & below), dr = __popcll(donors & below);
       const bool thief = g < 0 && ir < __popcll(donors);
       const bool robbed = g >= 0 && sp > bp && dr < __popcll(idle);
-      const int src = (thief ? select_bit(donors, ir) : (lane & ~3)) + qd;
+      const int src = (thief ? select_bit(donors, ir) : l4) + qd;
       const int dbp = __shfl(bp, src), dhome = __shfl(home, src), downer = __shfl(owner, src);
       const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
       const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
@@ -1053,8 +1090,18 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
         const uint32_t klim = near_key(__float_as_uint(lim));
         const uint4 se = make_uint4(st[0], st[1], st[2], st[3]);
         // two entries per step: both records are fetched before either is tested (two dependent
-        // fetch chains in flight per lane instead of one)
-        auto walk = [&](uint32_t b, uint32_t e, auto load, auto test) {
+        // fetch chains in flight per lane instead of one); OBB records (64 B) one at a time, which
+        // keeps the kernel within 64 VGPRs
+        auto walk = [&](uint32_t b, uint32_t e, auto load, auto test, auto pair) {
+          if (!decltype(pair)::value) {
+            for (uint32_t k = b; k < e; ++k) {
+              const uint2 e0 = sc.cell_ent[k];
+              if (near_key(e0.y) > klim) break;  // this and every later entry lie beyond the segment
+              if (EX) ++ne;
+              if (!(__uint_as_float(e0.y) > lim) && test(load(e0.x & 0x0fffffffu))) { blocked = true; break; }
+            }
+            return;
+          }
           for (uint32_t k = b; k < e && !blocked; k += 2) {
             const uint2 e0 = sc.cell_ent[k];
             const bool has1 = k + 1 < e;
@@ -1080,20 +1127,23 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
                ++nt[0];
                float d;
                return sphere_hit_dist(s, r, d) && d < maxd;
-             });
+             },
+             std::true_type{});
         walk(se.y, se.z, [&](uint32_t idx) { return sc.aabb[idx]; },
              [&](const AabbRec& r) {
                ++nt[1];
                float d;
                return aabb_test<false>(s, r, d) && d < maxd;
-             });
+             },
+             std::true_type{});
         if (OBB)
           walk(se.z, se.w, [&](uint32_t idx) { return sc.obb[idx]; },
                [&](const ObbRec& r) {
                  ++nt[2];
                  float d;
                  return obb_test<false>(s, r, stored_q(r), d) && d < maxd;
-               });
+               },
+               std::false_type{});
       } else {
         if (EX) ++nfb;
         blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
@@ -1131,7 +1181,7 @@ __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp
 // mt, filling the echo traversal's tails). No side stream, so no fork / join on the frame's path.
 // With OBB tests the joint kernel runs at 6 waves per SIMD (5 counting), where it needs no spills.
 template <bool EX, bool OBB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OBB ? (EX ? 5 : 6) : kEchoWaves<EX, OBB>)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OBB ? (EX ? 5 : ART_ECHO_MUFFLE_OBB_WAVES) : kEchoWaves<EX, OBB>)))
 void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t* __restrict__ count,
                         unsigned long long* ex, uint8_t* __restrict__ block, EchoFromHits eh, uint32_t* __restrict__ acc,
                         uint32_t groups, uint32_t mblocks, int mt) {
