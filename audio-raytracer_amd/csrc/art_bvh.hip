@@ -49,12 +49,14 @@ __device__ __forceinline__ uint32_t spread10(uint32_t v) {
 }
 
 size_t sort_scene_temp_bytes(int n) {
-  size_t bytes = 0;
+  size_t bytes = 0, scan = 0;
   if (n <= 0) return 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                          (const int*)nullptr, (int*)nullptr, n, 0, 32) != hipSuccess)
     return 0;
-  return bytes;
+  // (the multi-workgroup kd order scans 3 n side flags per binary level)
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, 3 * n) != hipSuccess) return 0;
+  return std::max(bytes, scan);
 }
 
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
@@ -131,12 +133,14 @@ __global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __r
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nleaf) return;
   CullRec u = cull_empty();
-  // slot (64 B): a = first 16 B, b = next 16 B (b.w = code), c, d = an OBB's local bounds
+  // slot (64 B; 32 B in scenes without OBBs, so a leaf is one 128-B line): a = first 16 B,
+  // b = next 16 B (b.w = code), c, d = an OBB's local bounds
   //   sphere: a = (cx, cy, cz, r2), b.z = AudioTargetId
   //   AABB:   a = (mn.xyz, mx.x), b.xy = mx.yz, b.z = AudioTargetId
   //   OBB:    a = (c.xyz, q.x), b.xyz = q.yzw, c = (lmn.xyz, lmx.x), d.xy = lmx.yz, d.z = AudioTargetId
+  const int per = n - ns - na > 0 ? 4 : 2;  // float4s per slot (bvh_slot_bytes)
   for (int k = j * kBvhLeaf; k < (j + 1) * kBvhLeaf; ++k) {
-    float4* sl = slots + 4 * (size_t)k;
+    float4* sl = slots + per * (size_t)k;
     float4 a = make_float4(0, 0, 0, 0), b = a, c = a, d = a;
     int code = -1;
     if (k < n) {
@@ -171,7 +175,8 @@ __global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __r
       }
     }
     b.w = __int_as_float(code);
-    sl[0] = a; sl[1] = b; sl[2] = c; sl[3] = d;
+    sl[0] = a; sl[1] = b;
+    if (per == 4) { sl[2] = c; sl[3] = d; }
   }
   leaves[j] = u;
 }
@@ -236,16 +241,33 @@ struct KdBufs {
   float4* cen;          // [n] centre (non-finite components -> FLT_MAX)
   int* p;               // [3][n] index arrays sorted by x, y, z
   const CullRec* cull;  // [n] the colliders' bounds (surface-area split costs)
+  // scenes above kKdMaxColliders (kd_big_*): the partitioned copies, side flags and their scan
+  int* p2;              // [3][n]
+  int* flag;            // [3][n] 1: left half of its segment
+  int* scan;            // [3][n] exclusive scan of flag
+  uint8_t* side;        // [n] by collider id
 };
+static size_t kd_al(size_t v) { return (v + 255) & ~(size_t)255; }
 static KdBufs kd_bufs(void* base, int n) {
   char* b = static_cast<char*>(base);
-  KdBufs k;
-  k.cen = reinterpret_cast<float4*>(b);
-  k.p = reinterpret_cast<int*>(b + 16 * (size_t)n);
+  KdBufs k{};
+  size_t o = 0;
+  k.cen = reinterpret_cast<float4*>(b + o); o += kd_al(16 * (size_t)n);
+  k.p = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
+  if (n > kKdMaxColliders) {
+    k.p2 = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
+    k.flag = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
+    k.scan = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
+    k.side = reinterpret_cast<uint8_t*>(b + o);
+  }
   k.cull = nullptr;
   return k;
 }
-size_t kd_scratch_bytes(int n) { return n > 0 && n <= kKdMaxColliders ? (size_t)n * (16 + 4 * 3) : 0; }
+size_t kd_scratch_bytes(int n) {
+  if (n <= 0) return 0;
+  const size_t base = kd_al(16 * (size_t)n) + kd_al(12 * (size_t)n);
+  return n <= kKdMaxColliders ? base : base + 3 * kd_al(12 * (size_t)n) + kd_al((size_t)n);
+}
 
 __global__ void kd_cen_kernel(const CullRec* __restrict__ cull, int n, float4* __restrict__ cen) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -326,6 +348,11 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       for (int e = tid; e < 2 * 3 * kKdSahSegs * 6; e += 1024)
         (&s_box[0][0][0][0])[e] = (e % 6) < 3 ? kd_ord(INFINITY) : kd_ord(-INFINITY);
       __syncthreads();
+      // a wave whose positions all lie in one half-segment (the upper levels) reduces its bounds
+      // across lanes first: one set of LDS atomics per wave instead of per thread
+      const int w0 = min(n, (tid & ~63) * chunk), w1 = min(n, w0 + 64 * chunk);
+      const bool wave_one = w1 > w0 && (((w0 >> lg) << 1) | ((w0 & (seg - 1)) >= half ? 1 : 0)) ==
+                                           ((((w1 - 1) >> lg) << 1) | (((w1 - 1) & (seg - 1)) >= half ? 1 : 0));
       for (int x = 0; x < 3; ++x) {
         float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
         int key = -1;  // (segment << 1 | half) of the run accumulated in b
@@ -337,12 +364,23 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
         };
         for (int i = i0; i < i1; ++i) {
           const int kk = ((i >> lg) << 1) | ((i & (seg - 1)) >= half ? 1 : 0);
-          if (kk != key) { flush(); key = kk; }
+          if (kk != key && !wave_one) { flush(); }
+          key = kk;
           const CullRec c = k.cull[s_p[x][i]];
           b[0] = fminf(b[0], c.lox); b[1] = fminf(b[1], c.loy); b[2] = fminf(b[2], c.loz);
           b[3] = fmaxf(b[3], c.hix); b[4] = fmaxf(b[4], c.hiy); b[5] = fmaxf(b[5], c.hiz);
         }
-        flush();
+        if (wave_one) {  // (wave-uniform) min / max over the wave, then lane 0 publishes
+          for (int q = 0; q < 6; ++q)
+            for (int off = 32; off > 0; off >>= 1) {
+              const float o = __shfl_xor(b[q], off, 64);
+              b[q] = q < 3 ? fminf(b[q], o) : fmaxf(b[q], o);
+            }
+          key = __shfl(key, 0, 64);  // (lane 0's chunk is not empty: w1 > w0)
+          if ((tid & 63) == 0) flush();
+        } else {
+          flush();
+        }
       }
       __syncthreads();
     }
@@ -432,6 +470,60 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
   for (int i = tid; i < n; i += 1024) perm[i] = s_p[0][i];
 }
 
+// ------------------------------------------------------------------------------------------
+// kd leaf order of larger scenes (above kKdMaxColliders, up to 2^24 colliders): the same binary
+// splits over global arrays, one launch sequence per binary level: side flags by collider id,
+// per-array flags, one exclusive scan of the 3 n flags, a stable scatter into the other copy. Every
+// segment splits on the axis its centres extend furthest on (no surface-area costs).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int kd_big_axis(const KdBufs& k, int n, int s, int lg) {
+  const int seg = 1 << lg, half = seg >> 1, a0 = s << lg, cnt = min(seg, n - a0);
+  if (cnt <= half) return -1;  // fits its left half: stays
+  int ax = -1;
+  float best = -1.0f;
+  for (int x = 0; x < 3; ++x) {
+    const int* px = k.p + (size_t)x * n;
+    const float e = kd_comp(k.cen[px[a0 + cnt - 1]], x) - kd_comp(k.cen[px[a0]], x);
+    if (ax < 0 || e > best) { best = e; ax = x; }
+  }
+  return ax;
+}
+__global__ void kd_big_side_kernel(KdBufs k, int n, int lg) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int ax = kd_big_axis(k, n, i >> lg, lg);
+  if (ax >= 0) k.side[k.p[(size_t)ax * n + i]] = (i & ((1 << lg) - 1)) < (1 << (lg - 1)) ? 1 : 0;
+}
+__global__ void kd_big_flag_kernel(KdBufs k, int n, int lg) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 3ll * n) return;
+  const int i = (int)(e % n);
+  const int ax = kd_big_axis(k, n, i >> lg, lg);
+  k.flag[e] = ax < 0 ? 1 : (int)k.side[k.p[e]];
+}
+__global__ void kd_big_scatter_kernel(KdBufs k, int n, int lg) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 3ll * n) return;
+  const int x = (int)(e / n), i = (int)(e - (long long)x * n);
+  const int a0 = (i >> lg) << lg, half = 1 << (lg - 1);
+  const size_t row = (size_t)x * n;
+  const int lr = k.scan[e] - k.scan[row + a0];  // left-flagged entries before i in its segment
+  const int dst = k.flag[e] ? a0 + lr : a0 + half + (i - a0 - lr);
+  k.p2[row + dst] = k.p[e];
+}
+static int launch_kd_big(KdBufs k, int n, int cap, const SortBufs& sb, hipStream_t st) {
+  const unsigned b1 = (unsigned)((n + 255) / 256), b3 = (unsigned)((3ll * n + 255) / 256);
+  for (int lg = 31 - __builtin_clz(cap); lg > 2; --lg) {
+    hipLaunchKernelGGL(kd_big_side_kernel, dim3(b1), dim3(256), 0, st, k, n, lg);
+    hipLaunchKernelGGL(kd_big_flag_kernel, dim3(b3), dim3(256), 0, st, k, n, lg);
+    size_t bytes = sb.temp_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(sb.temp, bytes, k.flag, k.scan, 3 * n, st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(kd_big_scatter_kernel, dim3(b3), dim3(256), 0, st, k, n, lg);
+    std::swap(k.p, k.p2);
+  }
+  return hipMemcpyAsync(sb.perm, k.p, (size_t)n * sizeof(int), hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : -1;
+}
+
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   const int n = sc.ns + sc.na + sc.no;
   int leaf0 = 0, total = 0;
@@ -439,7 +531,7 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0; sc.bvh_leaf0 = 0;
   if (L == 0 || !sb.bvh || !sb.bvh_ref || !sb.bvh_leaf) return 0;
   const int nleaf = total - leaf0;
-  if (sb.kd && n <= kKdMaxColliders) {  // kd leaf order
+  if (sb.kd) {  // kd leaf order
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
     hipLaunchKernelGGL(kd_cen_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k.cen);
@@ -450,7 +542,8 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
                                              st) != hipSuccess)
         return -1;
     }
-    hipLaunchKernelGGL(kd_split_kernel, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
+    if (n <= kKdMaxColliders) hipLaunchKernelGGL(kd_split_kernel, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
+    else if (launch_kd_big(k, n, nleaf * kBvhLeaf, sb, st) != 0) return -1;
   } else {  // Morton order of the centres (larger scenes)
     hipLaunchKernelGGL(scene_box_kernel, dim3(1), dim3(1024), 0, st, sc.cull, n, sb.box);
     hipLaunchKernelGGL(morton_all_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, sb.box, sb.keys, sb.vals);

@@ -599,6 +599,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.ent_s = reinterpret_cast<uint2*>(soa + f.soa_cent_s);
     cb.keys = reinterpret_cast<uint32_t*>(soa + f.soa_ckeys);
     cb.cap = f.cells_cap;
+    cb.compact = (f.ns < (1 << 16) && f.na < (1 << 16) && f.no < (1 << 16)) ? 1u : 0u;  // 4-B list entries
     cb.geo = soa + f.soa_cgeo;
     if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
     dv.sorted_sc = sc;
@@ -709,6 +710,9 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // Everything the stages allocate or create comes first: once the permeation job is forked to the
   // side stream, an early error return would leave it writing the caller's block unjoined.
   const bool fast = (f.stages & ART_STAGE_RAYTRACE) && !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
+  // the permeation job over the BVH (art_trace.hip); reference-order and counting frames sweep every
+  // collider (art_kernels.hip), an independent implementation the parity tests compare too
+  const bool perm_bvh = !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
   const int chunk = fast_fans_per_launch(f.R, f.H, f.T, f.TC, f.L.stride);
   if (fast) {
     if ((c->flags & ART_CTX_COUNT_EXECUTED) && !dv.exec.p) {
@@ -768,7 +772,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     HIP_TRY(c, hipEventRecord(pfork, st));
     HIP_TRY(c, hipStreamWaitEvent(dv.side, pfork, 0));
     size_t ti = timing ? tstart(1, dv.side) : 0;
-    launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, dv.side);
+    (perm_bvh ? launch_permeate : launch_permeate_sweep)(dv.sc, fp, f.L, d_origins, d_block, slot_batch, dv.side);
     if (timing) tstop(ti, dv.side);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(pjoin, dv.side));
@@ -834,7 +838,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   }
   if ((f.stages & ART_STAGE_PERMEATE) && !overlap) {
     size_t ti = timing ? tstart(1, st) : 0;
-    launch_permeate(dv.sc, fp, f.L, d_origins, d_block, slot_batch, st);
+    (perm_bvh ? launch_permeate : launch_permeate_sweep)(dv.sc, fp, f.L, d_origins, d_block, slot_batch, st);
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
     if (count) {

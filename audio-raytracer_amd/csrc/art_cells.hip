@@ -22,6 +22,7 @@
 // muffle_kernel skips entries beyond maxd. A segment longer than far_t (the bound the lists were
 // built for), a degenerate segment, or a target whose lists overflowed tests every collider.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
@@ -213,7 +214,12 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
         ++nhit;
       } else {
         const uint32_t pos = atomicAdd(cur + 3 * c, 1u);
-        if (pos < cb.cap) cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
+        if (pos < cb.cap) {  // the entry and its sort key (the segmented sort orders each cell by near bound)
+          const uint32_t key = near_key(__float_as_uint(G.near));
+          if (cb.compact) reinterpret_cast<uint32_t*>(cb.ent)[pos] = (G.code & 0xffffu) | (key << 16);
+          else cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
+          cb.keys[pos] = key;
+        }
         else cb.ok[t] = 0u;  // (cannot happen after the capacity check; kept as a guard)
       }
     }
@@ -247,18 +253,20 @@ size_t cells_scan_temp_bytes(int T, uint32_t cap) {
   size_t scan = 0, sort = 0;
   const int n = T * kCells * 3 + 1;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, n);
+  size_t sort32 = 0;
   (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, sort, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                     (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                                     (int)cap, n - 1, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
                                                     0, 16);
-  return std::max(scan, sort);
+  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, sort32, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, n - 1,
+                                                    (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0, 16);
+  return std::max(scan, std::max(sort, sort32));
 }
 
-// Sort keys of the filled entries, and the segment offsets clamped to the capacity (a target
-// whose lists overflowed is tested against every collider; its segments are sorted harmlessly).
+// The sort's segment offsets, clamped to the capacity (the fill pass wrote the entries' keys).
 __global__ void cells_key_kernel(CellBufs cb, uint32_t total_cells) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cb.cap) cb.keys[i] = near_key(cb.ent[i].y);
   if (i <= total_cells) cb.cursor[i] = min(cb.start[i], cb.cap);
 }
 
@@ -287,6 +295,8 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.far, cb.ok);
   sc.cell_start = cb.start;
   sc.cell_ent = cb.ent_s;
+  sc.cell_ent32 = reinterpret_cast<const uint32_t*>(cb.ent_s);
+  sc.cell_compact = cb.compact;
   sc.cell_far = cb.far;
   sc.cell_ok = cb.ok;
   sc.cell_cap = cb.cap;
@@ -312,14 +322,25 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
     hipLaunchKernelGGL(cells_row_kernel<true>, dim3(stride_grid(pairs * 6 * kCellG)), dim3(256), 0, st, geo, pairs, cb, n);
   // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its segment
   {
-    const uint32_t span = std::max<uint32_t>(cb.cap, (uint32_t)cells + 1);
+    const uint32_t span = (uint32_t)cells + 1;
     hipLaunchKernelGGL(cells_key_kernel, dim3((span + 255) / 256), dim3(256), 0, st, cb, (uint32_t)cells);
     size_t sbytes = cb.temp_bytes;
-    if (hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
-                                                    reinterpret_cast<const unsigned long long*>(cb.ent),
-                                                    reinterpret_cast<unsigned long long*>(cb.ent_s), (int)cb.cap, cells,
-                                                    cb.cursor, cb.cursor + 1, 0, 16, st) != hipSuccess)
-      return -1;
+    const hipError_t e =
+        cb.compact ? hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
+                                                                 reinterpret_cast<const uint32_t*>(cb.ent),
+                                                                 reinterpret_cast<uint32_t*>(cb.ent_s), (int)cb.cap, cells,
+                                                                 cb.cursor, cb.cursor + 1, 0, 16, st)
+                   : hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
+                                                                 reinterpret_cast<const unsigned long long*>(cb.ent),
+                                                                 reinterpret_cast<unsigned long long*>(cb.ent_s), (int)cb.cap,
+                                                                 cells, cb.cursor, cb.cursor + 1, 0, 16, st);
+    if (e != hipSuccess) return -1;
+  }
+  if (env_ll("ART_DEBUG_CELLS", 0)) {  // diagnostics: the built lists' size (synchronizes the stream)
+    uint32_t total = 0;
+    if (hipMemcpyAsync(&total, cb.start + cells, 4, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
+      fprintf(stderr, "[cells] T %d colliders %d: %u entries (capacity %u, %.1f per pair)\n", T, n, total, cb.cap,
+              (double)total / std::max(1ll, pairs));
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -78,6 +78,26 @@ ART_HD bool obb_test(const Seg& s, const ObbRec& b, quat q, float& dist) {
 }
 
 ART_HD quat stored_q(const ObbRec& b) { quat q; q.x = b.qx; q.y = b.qy; q.z = b.qz; q.w = b.qw; return q; }
+
+// obb_test<false> with the stored rotation on the record at p, fetched in the order that keeps the
+// fewest values live (the kernels' register budget): the rotation and the rotated direction's
+// reciprocals, then the centre and the rotated origin, then the local bounds. Same operations.
+__device__ __forceinline__ bool obb_test_staged(const Seg& s, const ObbRec* p, float& dist) {
+  const float4* v = reinterpret_cast<const float4*>(p);
+  const float4 qa = v[1];
+  quat q;
+  q.x = qa.x; q.y = qa.y; q.z = qa.z; q.w = qa.w;
+  const vec3 ld = qmul(q, s.d);
+  const float ix = 1.0f / ld.x, iy = 1.0f / ld.y, iz = 1.0f / ld.z;
+  const float4 c = v[0];
+  const vec3 lo = qmul(q, s.o - mk3(c.x, c.y, c.z));
+  __builtin_amdgcn_sched_barrier(0);
+  const float4 mn = v[2], mx = v[3];
+  float tNear, tFar;
+  const bool hit = slab<false>(lo.x, lo.y, lo.z, ix, iy, iz, mn.x, mn.y, mn.z, mx.x, mx.y, mx.z, tNear, tFar);
+  dist = tNear > 0.0f ? tNear : tFar;
+  return hit;
+}
 ART_HD quat inverse_q(const ObbCold& b) { quat q; q.x = b.iqx; q.y = b.iqy; q.z = b.iqz; q.w = b.iqw; return q; }
 
 // RayIntersectsSphere :323-355 (general quadratic)

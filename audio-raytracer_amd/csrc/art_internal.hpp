@@ -77,9 +77,9 @@ struct DevScene {
   // largest margin scale and factor; an empty node has lo > hi.
   const CullRec* bvh;
   const uint32_t* bvh_ref;        // [ns + na + no] in leaf order: type rank << 30 | in-type index
-  const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] 64-B slots in leaf order: the
-                                  // hot record's test fields and the global order code (rank << 28 |
-                                  // index; -1: empty slot) in the first 32 B (bvh_leaf_kernel)
+  const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] slots in leaf order, 64 B (32 B when the
+                                  // scene has no OBBs): the hot record's test fields and the global order
+                                  // code (rank << 28 | index; -1: empty slot) in the first 32 B (bvh_leaf_kernel)
   int bvh_levels;                 // 0: no BVH
   int bvh_leaf0;
   // Muffle candidate lists (art_cells.hip): for target t and direction cell c (a
@@ -91,6 +91,8 @@ struct DevScene {
   // overflowed (cell_ok[t] == 0) is tested against every collider instead.
   const uint32_t* cell_start;     // [T * kCells * 3 + 1]
   const uint2* cell_ent;          // [cell_cap]: (code, near bits), each cell's entries by ascending near_key
+  const uint32_t* cell_ent32;     // the same lists in 4-B entries (in-type index | near_key << 16), when
+  uint32_t cell_compact;          //   cell_compact (every type's count < 2^16)
   const float* cell_far;          // [T]: the segment length the lists were built for
   const uint32_t* cell_ok;        // [T]
   uint32_t cell_cap;
@@ -160,6 +162,7 @@ struct CellBufs {
   uint32_t* cursor;               // [T * kCells * 3 + 1] fill positions, then the sort's segment offsets
   uint2* ent;                     // [cap] in fill order
   uint2* ent_s;                   // [cap] each cell's entries by ascending near bound (DevScene::cell_ent)
+  uint32_t compact;               // 4-B entries in the same storage (DevScene::cell_compact)
   uint32_t* keys;                 // [2 * cap] sort keys (near_key) and their sorted copy
   float* far;                     // [T]: distance bound of t's segments
   uint32_t* ok;                   // [T]
@@ -241,6 +244,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf,
                           uint32_t* pair_count, hipStream_t st, const SideStream& echo, NearestMarks* marks = nullptr);
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
+                     uint8_t* block, const int2* slot_batch, hipStream_t st);
+// (the collider sweep of every loss ray, art_kernels.hip: the reference-order and counting frames)
+void launch_permeate_sweep(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, const int2* slot_batch, hipStream_t st);
 void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,
                        unsigned long long* nhit, hipStream_t st);

@@ -284,6 +284,9 @@ __global__ __launch_bounds__(kPermBlock) void permeate_kernel(DevScene sc, Frame
   __shared__ float s_terms[kPermBlock];
   __shared__ float s_rd[kPermBlock];
   __shared__ int s_ri[kPermBlock];
+#ifdef ART_PERM_EMPTY  // measurement-only build (tools/build_variant.sh): bounds what a faster pass could gain
+  return;
+#endif
   const int fan = blockIdx.y, slot = blockIdx.x, tid = threadIdx.x;
   const int2 br = slot_batch[slot];
   if (br.y <= br.x) return;  // no batch maps to this slot: value stays (stale / uninitialized, Q7)
@@ -572,8 +575,8 @@ void launch_raytrace(const DevScene& sc, const FrameParams& fp, const FanLayout&
   }
 }
 
-void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,
-                     const int2* slot_batch, hipStream_t st) {
+void launch_permeate_sweep(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,
+                           const int2* slot_batch, hipStream_t st) {
   if (fp.S == 0) return;
   hipLaunchKernelGGL(permeate_kernel, dim3(fp.TC, fp.S), dim3(kPermBlock), 0, st, sc, fp, L, origins, block, slot_batch);
 }

@@ -22,6 +22,7 @@
 #include <cstdlib>
 
 #include "art_device_fns.hpp"
+#include "art_frame_math.hpp"
 
 namespace art {
 
@@ -155,32 +156,37 @@ __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
 // entered lane counts them. No ballots: every value is a quad DPP reduction (measured 3 % faster in
 // the nearest traversal; the echo any-hit keeps its ballot form, index order, which measured 6 %
 // faster there than this near-first form).
-// Stack entries carry the child's entry bits (a lower bound of its entry: the key's low bits
-// cleared), so a pop drops the subtrees whose entry lies past the bound found meanwhile without
-// loading their children. Returns false when no child is entered (the caller pops).
-__device__ __forceinline__ bool quad_descend(bool enter, float en, bool force, int qd, int c0, uint2* my, int& g,
-                                             float& gen, int& sp) {
+__device__ __forceinline__ void quad_descend(bool enter, float en, bool force, int qd, int c0, uint32_t* my, int& g,
+                                             int& sp) {
   const uint32_t key = enter ? (((force ? 0u : (uint32_t)__float_as_int(en)) & ~3u) | (uint32_t)qd) : 0xffffffffu;
   const uint32_t k1 = (uint32_t)quad_perm<kQuadRot1>((int)key), k2 = (uint32_t)quad_perm<kQuadXor2>((int)key),
                  k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
   const int rank = (int)(k1 < key) + (int)(k2 < key) + (int)(k3 < key);
   const uint32_t kmin = min(min(key, k1), min(k2, k3));
   const int nent = quad_max_i32(enter ? rank + 1 : 0);
-  if (enter && rank > 0) my[sp + nent - 1 - rank] = make_uint2((uint32_t)(c0 + qd), key & ~3u);
-  if (!nent) return false;
-  g = c0 + (int)(kmin & 3u);
-  gen = __uint_as_float(kmin & ~3u);
-  sp += nent - 1;
-  return true;
+  if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
+  if (nent) {
+    g = c0 + (int)(kmin & 3u);
+    sp += nent - 1;
+  } else {  // branch-free pop: the stack slot is read unconditionally (clamped), -1 when empty
+    const int t = (int)my[sp > 0 ? sp - 1 : 0];
+    g = sp > 0 ? t : -1;
+    sp = sp > 0 ? sp - 1 : 0;
+  }
 }
 
 // Exact test of leaf slot `sl` (64 B: the hot record's test fields and the order code, art_bvh.hip
 // bvh_leaf_kernel) against segment s; tid = the collider's AudioTargetId. OBB = false: the scene has
-// no OBBs (no rank-2 slots), their test compiles out.
-template <bool OBB>
+// no OBBs (no rank-2 slots), their test compiles out. PERM: the permeation job's first-hit cast,
+// whose OBB test rotates by the inverse of the stored rotation (AudioPermeationJobBatched.cs
+// :172-179, App. B Q5), read from the cold record (obbc).
+template <bool OBB, bool PERM = false>
 __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, int slot, int& cc, float& dist, int& tid,
-                                               unsigned* nt) {
-  auto ld = [&](int k) { return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.leaves, slot * 64 + 16 * k, 0, 0)); };
+                                               unsigned* nt, const ObbCold* obbc = nullptr) {
+  // (slots are 64 B with OBBs in the scene, 32 B without: art_bvh.hip bvh_leaf_kernel)
+  auto ld = [&](int k) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.leaves, slot * (OBB ? 64 : 32) + 16 * k, 0, 0));
+  };
   const float4 qa = ld(0), qb = ld(1);
   cc = __float_as_int(qb.w);
   dist = 0.0f;
@@ -205,7 +211,11 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
   // direction's reciprocals first (the direction dies), then the rotated origin, and the local
   // bounds fetched only then (same operations as obb_test)
   quat q;
-  q.x = qa.w; q.y = qb.x; q.z = qb.y; q.w = qb.z;
+  if (PERM) {
+    q = inverse_q(obbc[cc & 0x0fffffff]);
+  } else {
+    q.x = qa.w; q.y = qb.x; q.z = qb.y; q.w = qb.z;
+  }
   const vec3 ld3 = qmul(q, s.d);
   const float ix = 1.0f / ld3.x, iy = 1.0f / ld3.y, iz = 1.0f / ld3.z;
   const vec3 lo = qmul(q, s.o - mk3(qa.x, qa.y, qa.z));
@@ -243,10 +253,9 @@ template <bool EX, bool OBB>
 constexpr int kNearestWaves = EX ? 6 : (OBB ? ART_NEAREST_OBB_WAVES : 8);
 template <bool EX, bool OBB>
 constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
-// echo_muffle_kernel<false, true> (the muffle walk's OBB records need 72 VGPRs): 6 waves per SIMD
-// without spills; 8 spills 3 VGPRs (outside the traversal loops' divergent regions)
+// echo_muffle_kernel<false, true>: 7 waves per SIMD (67 VGPRs) without spills; at 8 it spills 2
 #ifndef ART_ECHO_MUFFLE_OBB_WAVES
-#define ART_ECHO_MUFFLE_OBB_WAVES 6
+#define ART_ECHO_MUFFLE_OBB_WAVES 7
 #endif
 // k-th (0-based) set bit of m, k < popcount(m).
 __device__ __forceinline__ int select_bit(unsigned long long m, int k) {
@@ -272,12 +281,14 @@ __device__ __forceinline__ unsigned long long nearest_key(float d, int code) {
 // result is the (distance, order) minimum of their results (a 64-bit LDS minimum of (distance
 // bits, order); the two zeros compare equal, as in the reference's `<`, and the path kernel
 // re-evaluates a zero distance).
-template <bool EX, bool OBB>
-__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint2* my,
+// PERM: the permeation job's first-hit cast (ShootRayCast :101-141: INFINITY sentinel, inverse OBB
+// rotation); otherwise the raytracer's (:225-280: float.MaxValue sentinel).
+template <bool EX, bool OBB, bool PERM = false>
+__device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint32_t* my,
                                                   int* s_bound, unsigned long long* s_key, float& best, int& code,
                                                   unsigned long long* ex) {
   const int qd = lane & 3, wq = lane >> 2;
-  uint2* const s_wave = my - wq * kBvhStack;
+  uint32_t* const s_wave = my - wq * kBvhStack;
   best = FLT_MAX;
   code = kNoHit;
   if (sc.bvh_levels == 0) return;  // no colliders: every ray misses
@@ -288,26 +299,19 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
-  float gen = 0.0f;      // entry of node g (a lower bound), checked against the bound after leaf tests
   float lim = FLT_MAX;   // pruning bound: best, and (shared work) the other quads' results for the ray
   bool shared = false;   // wave-uniform: work was shared in this wave
   float mybest = FLT_MAX;  // this quad's own (distance, order) minimum over the leaves it tested
   int mycode = kNoHit;
   unsigned nsteps = 0;
   (void)nsteps;
-  // pop of entries [bp, sp), dropping those entered past the bound (a winner or tie lies strictly
-  // after the entry, so such a subtree holds neither); -1 when none is left
+  // branch-free pop of entries [bp, sp): the slot is read unconditionally (clamped), -1 when empty
   auto pop = [&]() {
-    for (;;) {
-      if (sp <= bp) { g = -1; sp = bp = 0; return; }
-      const uint2 t = my[--sp];
-      if (__uint_as_float(t.y) <= lim) {
-        g = (int)t.x;
-        gen = __uint_as_float(t.y);
-        if (sp == bp) sp = bp = 0;
-        return;
-      }
-    }
+    const bool has = sp > bp;
+    const int t = (int)my[has ? sp - 1 : 0];
+    g = has ? t : -1;
+    sp = has ? sp - 1 : sp;
+    if (sp == bp) sp = bp = 0;
   };
   // A child is entered when its widened box is entered at or before the bound (a winner or tie
   // lies strictly after every ancestor's entry); quad_descend orders the entered ones.
@@ -320,17 +324,19 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
     const bool enter = (r.lox <= r.hix) & (force | (h & (en <= lim)));  // bitwise: no branch
-    if (!quad_descend(enter, en, force, qd, c0, my, g, gen, sp)) pop();
+    quad_descend(enter, en, force, qd, c0, my, g, sp);
+    if (sp == bp) sp = bp = 0;
   };
   auto leaf_step = [&](int leaf) {
     ART_DIAG_STEP(nsteps);
     int cc, tid;
     float dd;
-    const bool h = leaf_slot_test<OBB>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, dd, tid, nt);
-    // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue)
+    const bool h = leaf_slot_test<OBB, PERM>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, dd, tid, nt, sc.obbc);
+    // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue; the permeation
+    // cast: against INFINITY, so a hit at FLT_MAX counts)
     float d = INFINITY;
     int dc = kNoHit;
-    if (h && dd < FLT_MAX) { d = dd; dc = cc; }
+    if (h && (PERM ? dd < INFINITY : dd < FLT_MAX)) { d = dd; dc = cc; }
     quad_min(d, dc);
     if (d < mybest || (d == mybest && dc < mycode)) {
       mybest = d;
@@ -375,9 +381,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
         const float dlim = __shfl(lim, src);
         if (thief && mycode != kNoHit && qd == 0) atomicMin(s_key + home, nearest_key(mybest, mycode));
         if (thief) {  // the ray's derived values are recomputed as the home computed them
-          const uint2 t = s_wave[(src >> 2) * kBvhStack + dbp];
-          g = (int)t.x;
-          gen = __uint_as_float(t.y);
+          g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
           sp = bp = 0;
           home = dhome;
           s = make_seg(mk3(ox, oy, oz), mk3(dx, dy, dz));
@@ -390,18 +394,13 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
       }
       if (shared) lim = fminf(lim, __int_as_float(s_bound[home]));
     }
-    if (g >= 0 && gen > lim) pop();  // the current node, entered before the last leaf tests lowered the bound
-    float pend_en = 0.0f;
     for (;;) {
-      if (g >= leaf0 && pend < 0) { pend = g; pend_en = gen; pop(); }
+      if (g >= leaf0 && pend < 0) { pend = g; pop(); }
       const bool inner = g >= 0 && g < leaf0;
       if (!__any(inner) || !__any(pend < 0 && g >= 0)) break;
       if (inner) inner_step();
     }
-    if (pend >= 0) {  // (a parked leaf entered past the bound holds no winner)
-      if (pend_en <= lim) leaf_step(pend);
-      pend = -1;
-    }
+    if (pend >= 0) { leaf_step(pend); pend = -1; }
   }
 #ifdef ART_DIAG
   if (qd == 0 && alive) diag_add(2, nsteps);
@@ -447,7 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
     uint32_t* __restrict__ counters) {
-  __shared__ uint2 s_stk[kBvhStack * 64];
+  __shared__ uint32_t s_stk[kBvhStack * 64];
   __shared__ int s_bound[64];
   __shared__ unsigned long long s_key[64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -455,7 +454,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   const int ngroups = fp.S * nrb;
   const int g = blockIdx.x;
   const int rr = 16 * w + (lane >> 2);
-  uint2* my = s_stk + rr * kBvhStack;
+  uint32_t* my = s_stk + rr * kBvhStack;
   unsigned long long* ex = EX ? fp.exec : nullptr;
   float best;
   int code;
@@ -1027,9 +1026,8 @@ __device__ __forceinline__ bool muffle_test(const DevScene& sc, const Seg& s, ui
     ++nt[1];
     h = aabb_test<false>(s, r, d);
   } else {
-    const ObbRec r = sc.obb[idx];
     ++nt[2];
-    h = obb_test<false>(s, r, stored_q(r), d);
+    h = obb_test_staged(s, sc.obb + idx, d);
   }
   return h && d < maxd;
 }
@@ -1092,28 +1090,41 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
         // two entries per step: both records are fetched before either is tested (two dependent
         // fetch chains in flight per lane instead of one); OBB records (64 B) one at a time, which
         // keeps the kernel within 64 VGPRs
+        // entry k: in-type index, near key and near bound (4-B entries carry the key, whose float
+        // is a lower bound of the near bound: the per-entry bound check then admits a little more)
+        auto entry = [&](uint32_t k, uint32_t& idx, uint32_t& key, float& nearf) {
+          if (sc.cell_compact) {  // (wave-uniform)
+            const uint32_t v = sc.cell_ent32[k];
+            idx = v & 0xffffu; key = v >> 16; nearf = __uint_as_float(key << 16);
+          } else {
+            const uint2 v = sc.cell_ent[k];
+            idx = v.x & 0x0fffffffu; key = near_key(v.y); nearf = __uint_as_float(v.y);
+          }
+        };
         auto walk = [&](uint32_t b, uint32_t e, auto load, auto test, auto pair) {
+          uint32_t i0, k0, i1, k1;
+          float n0, n1;
           if (!decltype(pair)::value) {
             for (uint32_t k = b; k < e; ++k) {
-              const uint2 e0 = sc.cell_ent[k];
-              if (near_key(e0.y) > klim) break;  // this and every later entry lie beyond the segment
+              entry(k, i0, k0, n0);
+              if (k0 > klim) break;  // this and every later entry lie beyond the segment
               if (EX) ++ne;
-              if (!(__uint_as_float(e0.y) > lim) && test(load(e0.x & 0x0fffffffu))) { blocked = true; break; }
+              if (!(n0 > lim) && test(load(i0))) { blocked = true; break; }
             }
             return;
           }
           for (uint32_t k = b; k < e && !blocked; k += 2) {
-            const uint2 e0 = sc.cell_ent[k];
             const bool has1 = k + 1 < e;
-            const uint2 e1 = sc.cell_ent[has1 ? k + 1 : k];
-            if (near_key(e0.y) > klim) break;             // this and every later entry lie beyond the segment
-            const bool use1 = has1 && near_key(e1.y) <= klim;
-            const auto r0 = load(e0.x & 0x0fffffffu);
-            const auto r1 = load((use1 ? e1.x : e0.x) & 0x0fffffffu);
+            entry(k, i0, k0, n0);
+            entry(has1 ? k + 1 : k, i1, k1, n1);
+            if (k0 > klim) break;             // this and every later entry lie beyond the segment
+            const bool use1 = has1 && k1 <= klim;
+            const auto r0 = load(i0);
+            const auto r1 = load(use1 ? i1 : i0);
             if (EX) ne += use1 ? 2u : 1u;
-            if (!(__uint_as_float(e0.y) > lim) && test(r0)) { blocked = true; break; }
+            if (!(n0 > lim) && test(r0)) { blocked = true; break; }
             if (!use1) break;
-            if (!(__uint_as_float(e1.y) > lim) && test(r1)) { blocked = true; break; }
+            if (!(n1 > lim) && test(r1)) { blocked = true; break; }
           }
         };
         walk(se.x, se.y,
@@ -1137,11 +1148,11 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
              },
              std::true_type{});
         if (OBB)
-          walk(se.z, se.w, [&](uint32_t idx) { return sc.obb[idx]; },
-               [&](const ObbRec& r) {
+          walk(se.z, se.w, [&](uint32_t idx) { return sc.obb + idx; },
+               [&](const ObbRec* r) {
                  ++nt[2];
                  float d;
-                 return obb_test<false>(s, r, stored_q(r), d) && d < maxd;
+                 return obb_test_staged(s, r, d) && d < maxd;
                },
                std::false_type{});
       } else {
@@ -1168,11 +1179,29 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
   }
 }
 
+// Muffle workgroup b of M ray blocks x mt targets. Consecutive workgroups are dispatched to the
+// chip's 8 XCDs in turn (each with its own L2), so when mt divides 8 the XCD of workgroup b serves
+// one target, b % 8 % mt: each L2 then holds that target's direction-cell lists only, not all
+// targets' (config 2: a quarter). Any other shape keeps the plain (b % M, b / M) order.
+__device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uint32_t& rb, int& t) {
+  if (8 % mt == 0 && ((unsigned long long)M * mt) % 8 == 0) {
+    const uint32_t x = b & 7u;
+    t = (int)(x % (uint32_t)mt);
+    rb = (b >> 3) * (8u / (uint32_t)mt) + x / (uint32_t)mt;
+  } else {
+    rb = b % M;
+    t = (int)(b / M);
+  }
+}
+
 template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
                                                      const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
-                                                     EchoFromHits eh) {
-  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x, (int)blockIdx.y, (int)gridDim.y);
+                                                     EchoFromHits eh, uint32_t mblocks, int mt) {
+  uint32_t rb = blockIdx.x;
+  int t = (int)blockIdx.y;
+  if (gridDim.y == 1) muffle_block(blockIdx.x, mblocks, mt, rb, t);  // (a 2-D grid: launches past 2^32 work-items)
+  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, rb, t, mt);
 }
 
 // One-hit frames with one batch slot and no path kernel (HM2): the echo traversal and the muffle
@@ -1190,8 +1219,219 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
     vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, nullptr, -1, block, eh);
     return;
   }
-  const uint32_t b = blockIdx.x - groups;
-  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, b % mblocks, (int)(b / mblocks), mt);
+  uint32_t rb;
+  int t;
+  muffle_block(blockIdx.x - groups, mblocks, mt, rb, t);  // (groups is a multiple of 8 in the bench shapes)
+  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, rb, t, mt);
+}
+
+// ------------------------------------------------------------------------------------------
+// Permeation job (AudioPermeationJobBatched.Execute :34-91) over the BVH. One wave per (batch slot,
+// fan), 16 quads:
+//   1. the slot's value is written by the highest-index ray of its last batch whose permeation
+//      first hit exists (each hitting ray overwrites it, :85; App. B Q7): quads cast the batch's
+//      rays from its end, 16 at a time (quad_nearest_core<PERM>: INFINITY sentinel, inverse OBB
+//      rotation, :101-141 / :172-179), and the highest-index hitting ray wins;
+//   2. its T loss rays (:61-85), one per quad: every collider whose widened box the ray enters at
+//      t >= 0 is visited (no pruning: the loss sums penetrations along the whole ray), its loss
+//      term evaluated (:225-328), the non-zero terms kept as (order code, term) in LDS, ranked by
+//      order code and summed serially in reference order (Sphere, AABB, OBB, ascending index).
+// Exactness: a collider the ray misses contributes exactly +0, and an entered-but-missed node's
+// colliders are missed (DESIGN.md §5 item 8 for the slab tests; the sphere loss test's b^2 - c
+// discriminant carries at most ~32 eps |oc|^2 of rounding, inside the sphere margin); +-0 terms never
+// change the running sum (it starts at +0 and is never -0), so only non-zero terms are summed. A loss
+// ray meeting more than kLossCap colliders is summed by the whole wave over every collider instead.
+// ------------------------------------------------------------------------------------------
+constexpr int kLossCap = 48;  // kept (code, term) entries per loss ray
+
+// Loss term of global collider g (Sphere, AABB, OBB ranges) for segment s and target t (0 when t
+// owns it), the reference expressions (:225-328).
+__device__ __forceinline__ float loss_term_global(const DevScene& sc, const Seg& s, int g, int t) {
+  if (g < sc.ns) {
+    const SphereRec r = sc.sph[g];
+    return r.tid != t ? perm_term_sphere(s, r, sc.sphc[g].density) : 0.0f;
+  }
+  g -= sc.ns;
+  if (g < sc.na) {
+    const AabbRec r = sc.aabb[g];
+    return r.tid != t ? perm_term_slab(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.mnx, r.mny, r.mnz, r.mxx, r.mxy,
+                                       r.mxz, sc.aabbc[g].density)
+                      : 0.0f;
+  }
+  g -= sc.na;
+  if (g >= sc.no) return 0.0f;
+  const ObbRec r = sc.obb[g];
+  if (r.tid == t) return 0.0f;
+  const quat q = stored_q(r);  // RayIntersectsOBBPermeation :294-300 rotates by the stored rotation
+  const vec3 lo = qmul(q, s.o - mk3(r.cx, r.cy, r.cz));
+  const vec3 ld = qmul(q, s.d);
+  return perm_term_slab(lo.x, lo.y, lo.z, 1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z, r.lmnx, r.lmny, r.lmnz, r.lmxx, r.lmxy, r.lmxz,
+                        sc.obbc[g].density);
+}
+
+// The whole wave over every collider in reference order (lanes over colliders, non-zero terms
+// added serially): the overflow path. Wave-uniform result.
+__device__ float loss_sum_wave(const DevScene& sc, const Seg& s, int t) {
+  const int lane = threadIdx.x & 63, ctot = sc.ns + sc.na + sc.no;
+  float sum = 0.0f;
+  for (int base = 0; base < ctot; base += 64) {
+    const float term = base + lane < ctot ? loss_term_global(sc, s, base + lane, t) : 0.0f;
+    for (unsigned long long m = __ballot(term != 0.0f); m; m &= m - 1ull)
+      sum += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, term), __builtin_ctzll(m)));
+  }
+  return sum;
+}
+
+// Loss term of leaf slot `slot` (its order code in cc; 0 for an empty slot or a collider t owns).
+template <bool OBB>
+__device__ __forceinline__ float leaf_loss_term(const DevScene& sc, const Seg& s, const BvhRes& br, int slot, int t, int& cc) {
+  auto ld = [&](int k) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(br.leaves, slot * (OBB ? 64 : 32) + 16 * k, 0, 0));
+  };
+  const float4 qa = ld(0), qb = ld(1);
+  cc = __float_as_int(qb.w);
+  if (cc < 0) return 0.0f;
+  const int type = cc >> 28, idx = cc & 0x0fffffff;
+  if (type == 0) {
+    if (__float_as_int(qb.z) == t) return 0.0f;
+    SphereRec r;
+    r.cx = qa.x; r.cy = qa.y; r.cz = qa.z; r.r2 = qa.w;
+    return perm_term_sphere(s, r, sc.sphc[idx].density);
+  }
+  if (type == 1 || !OBB) {
+    if (__float_as_int(qb.z) == t) return 0.0f;
+    return perm_term_slab(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, qa.x, qa.y, qa.z, qa.w, qb.x, qb.y,
+                          sc.aabbc[idx].density);
+  }
+  quat q;
+  q.x = qa.w; q.y = qb.x; q.z = qb.y; q.w = qb.z;
+  const vec3 ld3 = qmul(q, s.d);
+  const float ix = 1.0f / ld3.x, iy = 1.0f / ld3.y, iz = 1.0f / ld3.z;
+  const vec3 lo = qmul(q, s.o - mk3(qa.x, qa.y, qa.z));
+  const float4 qc = ld(2), qe = ld(3);
+  if (__float_as_int(qe.z) == t) return 0.0f;
+  return perm_term_slab(lo.x, lo.y, lo.z, ix, iy, iz, qc.x, qc.y, qc.z, qc.w, qe.x, qe.y, sc.obbc[idx].density);
+}
+
+template <bool OBB>
+__global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FrameParams fp, FanLayout L, const float* __restrict__ origins,
+                                                         uint8_t* __restrict__ block, const int2* __restrict__ slot_batch) {
+  __shared__ uint32_t s_stk[16 * kBvhStack];
+  __shared__ int s_bound[16];
+  __shared__ unsigned long long s_key[16];
+  __shared__ uint32_t s_code[16][kLossCap];
+  __shared__ float s_term[16][kLossCap], s_sorted[16][kLossCap];
+  const int fan = blockIdx.y, slot = blockIdx.x, lane = threadIdx.x, qd = lane & 3, wq = lane >> 2;
+  const int2 br = slot_batch[slot];
+  if (br.y <= br.x) return;  // no batch maps to this slot: the value stays (stale / uninitialized, Q7)
+  const vec3 O = load3(origins, fan);
+  uint32_t* const my = s_stk + wq * kBvhStack;
+  float* const ppr = reinterpret_cast<float*>(block + (size_t)fan * L.stride + L.perm_off);
+  const int T = fp.T;
+
+  // 1. the highest-index ray of [br.x, br.y) with a permeation first hit (ShootRayCast :58)
+  int found = -1, code = kNoHit;
+  float dist = 0.0f;
+  for (int r0 = br.y - 1; r0 >= br.x && found < 0; r0 -= 16) {  // (wave-uniform)
+    const int ray = r0 - wq;
+    const bool alive = ray >= br.x;
+    float best;
+    int c;
+    quad_nearest_core<false, OBB, true>(sc, make_seg(O, load_dir(sc.dirs, alive ? ray : br.x)), alive, lane, my, s_bound,
+                                        s_key, best, c, nullptr);
+    const unsigned long long hq = __ballot(qd == 0 && alive && c != kNoHit);
+    if (hq) {  // the lowest such quad holds the highest ray index
+      const int src = __builtin_ctzll(hq);
+      found = r0 - (src >> 2);
+      code = __builtin_amdgcn_readlane(c, src);
+      dist = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, best), src));
+    }
+  }
+  if (found < 0) {  // reset (:43-46) and no ray hit
+    for (int t = lane; t < T; t += 64) ppr[slot * T + t] = 0.0f;
+    return;
+  }
+  const vec3 d = load_dir(sc.dirs, found);
+  {  // the exact (Unity min / max) distance of a zero first hit: only its sign can differ
+    const Seg s0 = make_seg(O, d);
+    const int type = code >> 28, idx = code & 0x0fffffff;
+    if (dist == 0.0f) {
+      if (type == 0) sphere_hit_dist(s0, sc.sph[idx], dist);
+      else if (type == 1) aabb_test<true>(s0, sc.aabb[idx], dist);
+      else obb_test<true>(s0, sc.obb[idx], inverse_q(sc.obbc[idx]), dist);
+    }
+  }
+  const vec3 o = O + d * dist;  // :61
+  const vec3 off = o - d * kEps;
+
+  // 2. the T loss rays (:67-85), one per quad
+  const BvhRes bres = bvh_res(sc);
+  const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
+  for (int t0 = 0; t0 < T; t0 += 16) {  // (wave-uniform)
+    const int t = t0 + wq;
+    const bool valid = t < T;
+    const Seg s = make_seg(off, normalize(load3(sc.targets, valid ? t : 0) - off));
+    const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
+    const bool force = force_all(s, om);
+    int g = valid && sc.bvh_levels > 0 ? 0 : -1, sp = 0, n = 0;
+    while (__any(g >= 0)) {
+      while (g >= 0 && g < leaf0) {  // (quad-uniform) descend in index order, every entered child
+        const int c0 = 4 * g + 1;
+        const CullRec r = load_node(bres, c0 + qd);
+        float tn;
+        const bool h = node_entry(s, r, om, tn);
+        const bool enter = (r.lox <= r.hix) & (force | h);
+        const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
+        if (eb) {
+          const int first = __builtin_ctz(eb);
+          const uint32_t rest = eb & (eb - 1u);
+          if (enter && qd != first) my[sp + __popc(rest & ((1u << qd) - 1u))] = (uint32_t)(c0 + qd);
+          sp += __popc(rest);
+          g = c0 + first;
+        } else {
+          g = sp > 0 ? (int)my[--sp] : -1;
+        }
+      }
+      if (g >= leaf0) {
+        int cc;
+        const float term = leaf_loss_term<OBB>(sc, s, bres, (g - leaf0) * kBvhLeaf + qd, t, cc);
+        const uint32_t nz = (uint32_t)(__ballot(term != 0.0f) >> qshift) & 0xFu;
+        const int at = n + __popc(nz & ((1u << qd) - 1u));
+        if (term != 0.0f && at < kLossCap) { s_code[wq][at] = (uint32_t)cc; s_term[wq][at] = term; }
+        n += __popc(nz);
+        g = sp > 0 ? (int)my[--sp] : -1;
+      }
+    }
+    // rank the kept terms by order code (the four lanes of the quad share the entries), then sum
+    // them serially in that order in lane 0
+    const bool fits = n <= kLossCap;
+    if (valid && fits) {
+      for (int i = qd; i < n; i += 4) {
+        const uint32_t ci = s_code[wq][i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += s_code[wq][j] < ci ? 1 : 0;
+        s_sorted[wq][rank] = s_term[wq][i];
+      }
+      float sum = 0.0f;
+      for (int i = 0; i < n; ++i) sum += s_sorted[wq][i];
+      if (qd == 0) ppr[slot * T + t] = (float)fp.R * fp.perm_strength - sum;  // :260
+    }
+    for (unsigned long long ov = __ballot(qd == 0 && valid && !fits); ov; ov &= ov - 1ull) {  // (wave-uniform)
+      const int src = __builtin_ctzll(ov), tt = t0 + (src >> 2);
+      const Seg so = make_seg(off, normalize(load3(sc.targets, tt) - off));
+      const float sum = loss_sum_wave(sc, so, tt);
+      if (lane == 0) ppr[slot * T + tt] = (float)fp.R * fp.perm_strength - sum;
+    }
+  }
+}
+
+void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins, uint8_t* block,
+                     const int2* slot_batch, hipStream_t st) {
+  if (fp.S == 0) return;
+  if (sc.no > 0)
+    hipLaunchKernelGGL((permeate_bvh_kernel<true>), dim3(fp.TC, fp.S), dim3(64), 0, st, sc, fp, L, origins, block, slot_batch);
+  else
+    hipLaunchKernelGGL((permeate_bvh_kernel<false>), dim3(fp.TC, fp.S), dim3(64), 0, st, sc, fp, L, origins, block, slot_batch);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1288,10 +1528,12 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const bool fused = hm2;
   eh.no_path = hm2 ? 1 : 0;
   const unsigned mblocks = hm2 ? (groups + 3) / 4 : (unsigned)((hcap + 255) / 256);  // ray slots / hit records
-  const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over grid y (the rest looped)
+  const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over the grid (the rest looped)
+  // one dimension (XCD-aware target order, muffle_block) while it stays below 2^32 work-items
+  const dim3 mgrid = (unsigned long long)mblocks * mt * 256 < (1ull << 32) ? dim3(mblocks * mt) : dim3(mblocks, mt);
 #define ART_MUFFLE(S_, EX_, OBB_, HM_)                                                                                  \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, \
-                     muffle_acc, eh)
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), mgrid, dim3(256), 0, S_, sc, fp, pb.vp, pair_count, muffle_acc, eh, \
+                     mblocks, (int)mt)
 #define ART_MUFFLE_ANY(S_)                                                                                             \
   do {                                                                                                                 \
     if (hm2) {                                                                                                         \

@@ -61,8 +61,9 @@ def fib_dirs(R):
 
 
 def run(ctx, scene, org, H=2, T_owned=False):
+    # the permeation job too: its first-hit cast and loss rays run over the same BVH
     params = art.FrameParams(max_hits_per_ray=H, max_ray_life=1e4, max_muffle_hit_distance=1e5,
-                             stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
+                             stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_PERMEATE | abi.ART_STAGE_REDUCE)
     out, counts = gpu_vs_oracle(ctx, scene, params, org, hits=True, counts=False)
     return out
 
@@ -259,3 +260,48 @@ def test_cell_lists_threshold_real_size():
         assert T * sc.C > (1 << 23) if T == 256 else T * sc.C <= (1 << 23), sc.C
         with art.Context(1) as c:
             gpu_vs_oracle(c, sc, params, org, hits=False, counts=False)
+
+
+def test_permeation_loss_rays_through_many_colliders(ctx):
+    """Loss rays (AudioPermeationJobBatched.cs:61-85, :225-328) that cross far more colliders than
+    the BVH loss pass keeps per ray (kLossCap = 48): rows of overlapping spheres (radius 0.6 at
+    spacing 1) 128 long, boxes and OBBs among them, targets far out along the rows, owned
+    colliders skipped; the sum over every collider in reference order must equal the oracle's, for
+    the rays that fit and for the ones summed by the whole-wave overflow path."""
+    rng = np.random.default_rng(23)
+    xs = np.arange(-64, 64, dtype=np.float32)
+    yz = np.array([-1.0, 0.0, 1.0], np.float32)
+    c = np.array([(x, y, z) for x in xs for y in yz for z in yz], np.float32)
+    T = 6
+    tid = rng.integers(-1, T, len(c)).astype(np.int16)
+    sph = spheres(c, np.full(len(c), 0.6, np.float32), rng, tid=tid)
+    box = aabbs(c[::7] + np.float32(0.5), np.full((len(c[::7]), 3), 0.3, np.float32), rng)
+    ob = obbs(c[3::11] + np.float32(0.25), np.full((len(c[3::11]), 3), 0.35, np.float32), rng)
+    targets = np.array([[-1000, 0, 0], [1000, 0.2, 0.1], [-500, 3, 2], [300, -0.5, 0.4], [0, 0, 900], [-2000, 0.9, -0.9]],
+                       np.float32)
+    scene = art.Scene(dirs=fib_dirs(64), targets=targets, spheres=sph, aabbs=box, obbs=ob)
+    org = np.array([[0.5, 0.0, 0.0], [-20.3, 0.4, -0.2], [40.0, 0.0, 0.7], [0.0, 5.0, 0.0]], np.float32)
+    out = run(ctx, scene, org)
+    assert (out.perm != 0).any()
+
+
+def test_permeation_first_hit_far_from_batch_end():
+    """The permeation slot value comes from the highest-index ray of the batch whose first hit exists
+    (AudioPermeationJobBatched.cs:58, App. B Q7). One small box straight along ray 5 of 96: the BVH
+    permeation pass casts the batch's rays from its end 16 at a time, so several rounds find no hit
+    before the one holding ray 5's neighbours; TC = 1 and TC = 3 (three batch slots)."""
+    rng = np.random.default_rng(31)
+    dirs = fib_dirs(96)
+    d5 = dirs[5].view(np.float16).astype(np.float32)
+    d5 /= np.linalg.norm(d5)
+    box = aabbs((d5 * 20.0)[None, :], np.full((1, 3), 1.5, np.float32), rng)
+    scene = art.Scene(dirs=dirs, targets=np.array([[5, 5, 5], [-30, 2, 1]], np.float32), aabbs=box)
+    org = np.zeros((3, 3), np.float32)
+    org[1] = [0.1, -0.2, 0.05]
+    for tc in (1, 3):
+        params = art.FrameParams(max_hits_per_ray=1, max_ray_life=1e4, max_muffle_hit_distance=1e5,
+                                 stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_PERMEATE | abi.ART_STAGE_REDUCE)
+        params.thread_count = tc
+        with art.Context(1) as c:
+            out, _ = gpu_vs_oracle(c, scene, params, org, hits=True, counts=False, stale=4)
+        assert (out.perm != 0).any()
