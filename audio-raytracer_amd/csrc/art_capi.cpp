@@ -599,7 +599,10 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
     cb.ent_s = reinterpret_cast<uint2*>(soa + f.soa_cent_s);
     cb.keys = reinterpret_cast<uint32_t*>(soa + f.soa_ckeys);
     cb.cap = f.cells_cap;
-    cb.compact = (f.ns < (1 << 16) && f.na < (1 << 16) && f.no < (1 << 16)) ? 1u : 0u;  // 4-B list entries
+#ifndef ART_CELLS_COMPACT
+#define ART_CELLS_COMPACT 1
+#endif
+    cb.compact = (ART_CELLS_COMPACT && f.ns < (1 << 16) && f.na < (1 << 16) && f.no < (1 << 16)) ? 1u : 0u;  // 4-B entries
     cb.geo = soa + f.soa_cgeo;
     if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
     dv.sorted_sc = sc;

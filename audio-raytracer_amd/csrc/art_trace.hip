@@ -1179,12 +1179,18 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
   }
 }
 
-// Muffle workgroup b of M ray blocks x mt targets. Consecutive workgroups are dispatched to the
-// chip's 8 XCDs in turn (each with its own L2), so when mt divides 8 the XCD of workgroup b serves
-// one target, b % 8 % mt: each L2 then holds that target's direction-cell lists only, not all
-// targets' (config 2: a quarter). Any other shape keeps the plain (b % M, b / M) order.
+// Muffle workgroup b of M ray blocks x mt targets in echo_muffle_kernel. Consecutive workgroups are
+// dispatched to the chip's 8 XCDs in turn (each with its own L2), so when mt divides 8 the XCD of
+// workgroup b serves one target, b % 8 % mt: each L2 then holds that target's direction-cell lists
+// only, not all targets' (config 2: echo_muffle traffic 12.9 -> 10.8 MB per frame with the 4-B
+// entries). The muffle blocks there fill the echo traversal's tails; in the standalone muffle_kernel
+// the uneven work per target left XCDs idle (config 5: 171 -> 193 us), so it keeps the plain order.
+// Any other shape keeps the plain (b % M, b / M) order.
+#ifndef ART_MUFFLE_XCD
+#define ART_MUFFLE_XCD 1
+#endif
 __device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uint32_t& rb, int& t) {
-  if (8 % mt == 0 && ((unsigned long long)M * mt) % 8 == 0) {
+  if (ART_MUFFLE_XCD && 8 % mt == 0 && ((unsigned long long)M * mt) % 8 == 0) {
     const uint32_t x = b & 7u;
     t = (int)(x % (uint32_t)mt);
     rb = (b >> 3) * (8u / (uint32_t)mt) + x / (uint32_t)mt;
@@ -1197,11 +1203,8 @@ __device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uin
 template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
                                                      const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
-                                                     EchoFromHits eh, uint32_t mblocks, int mt) {
-  uint32_t rb = blockIdx.x;
-  int t = (int)blockIdx.y;
-  if (gridDim.y == 1) muffle_block(blockIdx.x, mblocks, mt, rb, t);  // (a 2-D grid: launches past 2^32 work-items)
-  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, rb, t, mt);
+                                                     EchoFromHits eh) {
+  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x, (int)blockIdx.y, (int)gridDim.y);
 }
 
 // One-hit frames with one batch slot and no path kernel (HM2): the echo traversal and the muffle
@@ -1529,11 +1532,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   eh.no_path = hm2 ? 1 : 0;
   const unsigned mblocks = hm2 ? (groups + 3) / 4 : (unsigned)((hcap + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over the grid (the rest looped)
-  // one dimension (XCD-aware target order, muffle_block) while it stays below 2^32 work-items
-  const dim3 mgrid = (unsigned long long)mblocks * mt * 256 < (1ull << 32) ? dim3(mblocks * mt) : dim3(mblocks, mt);
 #define ART_MUFFLE(S_, EX_, OBB_, HM_)                                                                                  \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), mgrid, dim3(256), 0, S_, sc, fp, pb.vp, pair_count, muffle_acc, eh, \
-                     mblocks, (int)mt)
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, \
+                     muffle_acc, eh)
 #define ART_MUFFLE_ANY(S_)                                                                                             \
   do {                                                                                                                 \
     if (hm2) {                                                                                                         \
