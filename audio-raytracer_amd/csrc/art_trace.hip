@@ -440,12 +440,128 @@ __device__ __forceinline__ uint32_t* echo_counts(float4* state, int ngroups) {
   return live_list(state, ngroups) + (size_t)ngroups * 64 + kLiveCounters;
 }
 
-// EX: count the executed tests (fp.exec); OBB: the scene has OBBs.
-template <bool EX, bool OBB>
+// Visibility work (struct of arrays, below): echo segments and outputs, hit records. `fixed`
+// (multi-hit frames with one batch slot and no hit outputs, nearest_first_kernel<..., FOLD>): the
+// records sit at fixed positions bounce * fixed + ray slot, an output index of kNoRecord / a hit
+// record destination of kNoRecord marking a slot with no echo / no muffle rays that bounce.
+constexpr uint32_t kNoRecord = 0xffffffffu;
+struct VisPairs {
+  float4* seg;
+  uint2* out;
+  float4* hrec;
+  uint32_t echo_cap;  // multiple of 64
+  uint32_t fixed;     // 0: records compacted in emission order; else ray slots per bounce
+};
+
+__device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
+  return type == kSphere ? sc.sphc[idx].echo : (type == kAabb ? sc.aabbc[idx].echo : sc.obbc[idx].echo);
+}
+
+// ReflectRay (:456-532) at hit point o of collider (type, idx), then the offset (:528) and the
+// absorption (:531); false when the ray's life runs out (:189).
+__device__ __forceinline__ bool reflect_at_hit(const DevScene& sc, const FrameParams& fp, int type, int idx, vec3& o, vec3& d,
+                                               float& life) {
+  vec3 n = mk3(0.0f, 0.0f, 0.0f);
+  float absorption = 0.0f;
+  if (type == kAabb) {
+    const AabbCold b = sc.aabbc[idx];
+    vec3 lp = o - mk3(b.cx, b.cy, b.cz);
+    vec3 ap = abs3(lp);
+    float dx = b.hx - ap.x, dy = b.hy - ap.y, dz = b.hz - ap.z;
+    if (dx < dy && dx < dz) n.x = usign(lp.x);
+    else if (dy < dx && dy < dz) n.y = usign(lp.y);
+    else n.z = usign(lp.z);
+    absorption = b.absorption;
+  } else if (type == kObb) {
+    const ObbRec b = sc.obb[idx];
+    const ObbCold bc2 = sc.obbc[idx];
+    vec3 lh = qmul(inverse_q(bc2), o - mk3(b.cx, b.cy, b.cz));  // :489 (Q5: inverse of the stored inverse)
+    vec3 ap = abs3(lh);
+    vec3 df = mk3(bc2.hx, bc2.hy, bc2.hz) - ap;
+    vec3 ln = mk3(0.0f, 0.0f, 0.0f);
+    if (df.x < df.y && df.x < df.z) ln.x = usign(lh.x);
+    else if (df.y < df.x && df.y < df.z) ln.y = usign(lh.y);
+    else ln.z = usign(lh.z);
+    n = qmul(stored_q(b), ln);                                 // :510
+    absorption = bc2.absorption;
+  } else {
+    const SphereRec c = sc.sph[idx];
+    n = normalize(o - mk3(c.cx, c.cy, c.cz));                  // :516
+    absorption = sc.sphc[idx].absorption;
+  }
+  d = reflect(d, n);                    // :525
+  o = o + d * kEps;                     // :528
+  life -= fp.max_life * absorption;     // :531
+  return !(life < 0.0f);
+}
+
+// The winner's collider from its order code, and the exact (Unity min / max) re-evaluation of a zero
+// distance (IEEE and Unity min / max differ only in the sign of an equal-magnitude zero pair).
+__device__ __forceinline__ void winner_of(const DevScene& sc, const Seg& s, int code, int& type, int& idx, float& dist) {
+  const int rank = code >> 28;
+  idx = code & 0x0fffffff;
+  type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
+  if (dist == 0.0f) {
+    if (type == kSphere) sphere_hit_dist(s, sc.sph[idx], dist);  // (a -0 the result key made +0)
+    if (type == kAabb) aabb_test<true>(s, sc.aabb[idx], dist);
+    if (type == kObb) { const ObbRec r = sc.obb[idx]; obb_test<true>(s, r, stored_q(r), dist); }
+  }
+}
+// FOLD (multi-hit frames with one batch slot and no hit outputs): the path kernel's work for each
+// ray runs in this kernel's epilogue (fold_path), every ray keeps its slot for all bounces (no live
+// list: a finished ray's quad only helps the others through work sharing), and the echo segments and
+// hit records go to fixed per-bounce slots (VisPairs::fixed): no path launch and no reservation
+// atomics per bounce.
+__device__ __forceinline__ void fold_path(const DevScene& sc, const FrameParams& fp, const FanLayout& L, uint8_t* block,
+                                          const float* origins, const VisPairs& vp, float4* state, int step, uint32_t sidx,
+                                          int fan, int ray,
+                                          bool slot_ok, vec3 o, vec3 d, float life, int hits, bool alive, float dist, int code,
+                                          bool lead) {
+  const int H = fp.H;
+  const vec3 O = load3(origins, fan);
+  const bool hit = alive && code != kNoHit;
+  int type = kNone, idx = 0;
+  if (hit) {
+    winner_of(sc, make_seg(o, d), code, type, idx, dist);
+    o = o + d * dist;  // :111
+    life -= dist;      // :112
+    hits += 1;         // :113
+  }
+  uint16_t* echo = reinterpret_cast<uint16_t*>(block + (size_t)fan * L.stride + L.echo_off);
+  const size_t rec = (size_t)step * vp.fixed + sidx;
+  if (lead) {  // this bounce's echo ray (:124-145) and the muffle rays' hit record (:150-173), or none
+    if (hit) {
+      const vec3 off = o - d * kEps;                 // :124, :158
+      const float dist0 = distance(O, o);            // :130 (un-offset hit point)
+      const vec3 qdir = normalize(O - off);
+      vp.seg[2 * rec] = make_float4(off.x, off.y, off.z, dist0);
+      vp.seg[2 * rec + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(kNoOwner));
+      vp.out[rec] = make_uint2((uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + hits - 1),
+                               f32tof16(dist0 * echo_of(sc, type, idx)));  // :142-144
+      vp.hrec[rec] = make_float4(off.x, off.y, off.z, __uint_as_float((uint32_t)fan * (uint32_t)fp.T));  // batch slot 0
+      echo[ray * H + hits - 1] = 0;  // a blocked echo keeps the reset value (:76); the echo traversal stores the rest
+    } else {
+      vp.out[rec] = make_uint2(kNoRecord, 0u);
+      vp.hrec[rec] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kNoRecord));
+    }
+  }
+  // termination / reflection (:179-193, ReflectRay :456-532)
+  bool next = hit;  // a miss ends the ray (:200-207)
+  if (hit) next = (hits >= H || life <= 0.0f) ? false : reflect_at_hit(sc, fp, type, idx, o, d, life);
+  if (lead && slot_ok) {
+    state[2 * (size_t)sidx] = make_float4(o.x, o.y, o.z, life);
+    state[2 * (size_t)sidx + 1] = make_float4(d.x, d.y, d.z, __int_as_float(hits | (next ? 256 : 0)));
+    if (alive && !next)  // the ray stops here: slots past its last hit keep the reset value 0 (:72-80)
+      for (int k = hits; k < H; ++k) echo[ray * H + k] = 0;
+  }
+}
+
+// EX: count the executed tests (fp.exec); OBB: the scene has OBBs; FOLD: fold_path above.
+template <bool EX, bool OBB, bool FOLD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWaves<EX, OBB>))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
-    uint32_t* __restrict__ counters) {
+    uint32_t* __restrict__ counters, FanLayout L, uint8_t* __restrict__ block, VisPairs vp) {
   __shared__ uint32_t s_stk[kBvhStack * 64];
   __shared__ int s_bound[64];
   __shared__ unsigned long long s_key[64];
@@ -461,7 +577,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   vec3 o, d;
   bool alive, write;
   uint32_t out;  // ray slot (< 2^31: fast_fans_per_launch)
-  if (step > 0) {  // the previous bounce's list of live ray slots
+  float life = fp.max_life;
+  int nhits = 0, fan = 0, ray = 0;
+  bool slot_ok = true;
+  if (FOLD) {  // every ray in its slot for every bounce
+    if (step == 0) {
+      for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
+      if (counters && blockIdx.x == 0 && threadIdx.x < 4) counters[threadIdx.x] = 0u;
+    }
+    fan = g / nrb;
+    const int sl = (g - fan * nrb) * 64 + rr;
+    slot_ok = sl < fp.R;
+    ray = slot_ok ? ray_order[sl] : 0;
+    out = (uint32_t)g * 64u + (uint32_t)rr;
+    if (step == 0) {
+      o = load3(origins, fan);
+      d = load_dir(sc.dirs, ray);
+      alive = slot_ok;
+    } else {
+      const float4 a = state[2 * (size_t)out], b = state[2 * (size_t)out + 1];
+      o = mk3(a.x, a.y, a.z);
+      life = a.w;
+      d = mk3(b.x, b.y, b.z);
+      nhits = __float_as_int(b.w) & 0xff;
+      alive = slot_ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
+    }
+    write = false;
+  } else if (step > 0) {  // the previous bounce's list of live ray slots
     const uint32_t* live = live_list(state, ngroups);
     const uint32_t cnt = live[(size_t)ngroups * 64 + step];
     if ((uint32_t)g * 64u >= cnt) return;  // the whole workgroup: past the list
@@ -497,6 +639,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   const unsigned long long t0 = clock64();
 #endif
   quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code, ex);
+  if (FOLD) {
+    // The ray's state is fetched again rather than kept live across the traversal (a memory
+    // clobber: the compiler may not reuse the values loaded before it): 64 VGPRs, no spills.
+    asm volatile("" ::: "memory");
+    {
+      const int rr2 = 16 * w + (lane >> 2);
+      fan = g / nrb;
+      const int sl = (g - fan * nrb) * 64 + rr2;
+      slot_ok = sl < fp.R;
+      ray = slot_ok ? ray_order[sl] : 0;
+      out = (uint32_t)g * 64u + (uint32_t)rr2;
+      if (step == 0) {
+        o = load3(origins, fan);
+        d = load_dir(sc.dirs, ray);
+        life = fp.max_life;
+        nhits = 0;
+        alive = slot_ok;
+      } else {
+        const float4 a = state[2 * (size_t)out], b = state[2 * (size_t)out + 1];
+        o = mk3(a.x, a.y, a.z);
+        life = a.w;
+        d = mk3(b.x, b.y, b.z);
+        nhits = __float_as_int(b.w) & 0xff;
+        alive = slot_ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
+      }
+    }
+    if (EX) exec_add(fp.exec, kExecEchoPairs, (unsigned long long)__popcll(__ballot(alive && code != kNoHit) & kQuad0));
+    fold_path(sc, fp, L, block, origins, vp, state, step, out, fan, ray, slot_ok, o, d, life, nhits, alive, best, code,
+              (lane & 3) == 0);
+    return;
+  }
   // (the ray slot stays a 32-bit value across the traversal: an opaque copy keeps the compiler from
   // widening it to a 64-bit offset before the loop, two more live VGPRs)
   asm volatile("" : "+v"(out));
@@ -519,12 +692,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
 //                           target 0; muffle_kernel casts its T rays
 // counts[0] / counts[1] = echo pairs / hit records emitted.
 // ------------------------------------------------------------------------------------------
-struct VisPairs {
-  float4* seg;
-  uint2* out;
-  float4* hrec;
-  uint32_t echo_cap;  // multiple of 64
-};
 
 __device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Seg& s, float& maxd, int& owner) {
   const float4 q0 = vp.seg[2 * (size_t)i], q1 = vp.seg[2 * (size_t)i + 1];
@@ -533,9 +700,7 @@ __device__ __forceinline__ void load_pair_seg(const VisPairs& vp, uint32_t i, Se
   owner = __float_as_int(q1.w);
 }
 
-__device__ __forceinline__ float echo_of(const DevScene& sc, int type, int idx) {
-  return type == kSphere ? sc.sphc[idx].echo : (type == kAabb ? sc.aabbc[idx].echo : sc.obbc[idx].echo);
-}
+
 
 // ------------------------------------------------------------------------------------------
 // Path kernel: everything of one bounce of AudioRaytracerJobBatched.Execute (:61-215) except the
@@ -638,16 +803,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
     int type = kNone, idx = 0;
     float dist = __int_as_float(ph.x);
     if (hit) {
-      const int rank = bc >> 28;
-      idx = bc & 0x0fffffff;
-      type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
-      // exact (Unity min/max) re-evaluation of a zero distance: IEEE and Unity min/max differ only
-      // in the sign of an equal-magnitude zero pair, so only a zero result can differ (its sign)
-      if (dist == 0.0f) {
-        if (type == kSphere) sphere_hit_dist(s, sc.sph[idx], dist);  // (a -0 the result key made +0)
-        if (type == kAabb) aabb_test<true>(s, sc.aabb[idx], dist);
-        if (type == kObb) { const ObbRec r = sc.obb[idx]; obb_test<true>(s, r, stored_q(r), dist); }
-      }
+      winner_of(sc, s, bc, type, idx, dist);
       o = o + d * dist;  // :111
       life -= dist;      // :112
       hits += 1;         // :113
@@ -694,38 +850,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       if (hits >= H || life <= 0.0f) {
         alive = false;
       } else {
-        vec3 n = mk3(0.0f, 0.0f, 0.0f);
-        float absorption = 0.0f;
-        if (type == kAabb) {
-          const AabbCold b = sc.aabbc[idx];
-          vec3 lp = o - mk3(b.cx, b.cy, b.cz);
-          vec3 ap = abs3(lp);
-          float dx = b.hx - ap.x, dy = b.hy - ap.y, dz = b.hz - ap.z;
-          if (dx < dy && dx < dz) n.x = usign(lp.x);
-          else if (dy < dx && dy < dz) n.y = usign(lp.y);
-          else n.z = usign(lp.z);
-          absorption = b.absorption;
-        } else if (type == kObb) {
-          const ObbRec b = sc.obb[idx];
-          const ObbCold bc2 = sc.obbc[idx];
-          vec3 lh = qmul(inverse_q(bc2), o - mk3(b.cx, b.cy, b.cz));  // :489 (Q5: inverse of the stored inverse)
-          vec3 ap = abs3(lh);
-          vec3 df = mk3(bc2.hx, bc2.hy, bc2.hz) - ap;
-          vec3 ln = mk3(0.0f, 0.0f, 0.0f);
-          if (df.x < df.y && df.x < df.z) ln.x = usign(lh.x);
-          else if (df.y < df.x && df.y < df.z) ln.y = usign(lh.y);
-          else ln.z = usign(lh.z);
-          n = qmul(stored_q(b), ln);                                 // :510
-          absorption = bc2.absorption;
-        } else {
-          const SphereRec c = sc.sph[idx];
-          n = normalize(o - mk3(c.cx, c.cy, c.cz));                  // :516
-          absorption = sc.sphc[idx].absorption;
-        }
-        d = reflect(d, n);                    // :525
-        o = o + d * kEps;                     // :528
-        life -= fp.max_life * absorption;     // :531
-        if (life < 0.0f) alive = false;
+        alive = reflect_at_hit(sc, fp, type, idx, o, d, life);
       }
     }
     if (MULTI) {
@@ -862,19 +987,26 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     }
     if (!__any(valid)) return;
   } else {
-    // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
-    uint32_t start = 0u, n;
-    if (bounce < 0) {
-      n = ldc(count, 0);
+    if (vp.fixed) {  // bounce `bounce`'s records at fixed slots: 64-slot group blk
+      p = (uint32_t)bounce * vp.fixed + blk * 64u + (uint32_t)slot;
+      valid = vp.out[p].x != kNoRecord;
+      if (!__any(valid)) return;
+      if (valid) load_pair_seg(vp, p, s, maxd, owner);
     } else {
-      for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
-      n = start + ldc(ecnt, bounce);
+      // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
+      uint32_t start = 0u, n;
+      if (bounce < 0) {
+        n = ldc(count, 0);
+      } else {
+        for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
+        n = start + ldc(ecnt, bounce);
+      }
+      const uint32_t base = start + blk * 64u;
+      if (base + (uint32_t)(w * 16) >= n) return;                // this wave's 16 segments are past the emitted pairs
+      valid = base + (uint32_t)slot < n;
+      p = valid ? base + (uint32_t)slot : base;
+      if (valid) load_pair_seg(vp, p, s, maxd, owner);
     }
-    const uint32_t base = start + blk * 64u;
-    if (base + (uint32_t)(w * 16) >= n) return;                // this wave's 16 segments are past the emitted pairs
-    valid = base + (uint32_t)slot < n;
-    p = valid ? base + (uint32_t)slot : base;
-    if (valid) load_pair_seg(vp, p, s, maxd, owner);
   }
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
   bool force = force_all(s, om);
@@ -1053,7 +1185,8 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
                                             const EchoFromHits& eh, uint32_t bx, int by, int gy) {
   const int lane = threadIdx.x & 63;
   const uint32_t i = bx * 256u + threadIdx.x;
-  const uint32_t n = HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u : ldc(count, 1);
+  // (fixed slots: every bounce's records, kNoRecord marking the slots with no hit)
+  const uint32_t n = HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u : (vp.fixed ? vp.fixed * (uint32_t)fp.H : ldc(count, 1));
   if (__builtin_amdgcn_readfirstlane(i - (uint32_t)lane) >= n) return;
   bool valid = i < n;
   vec3 off = mk3(0.0f, 0.0f, 0.0f);
@@ -1068,6 +1201,7 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
     const float4 r = vp.hrec[valid ? i : 0u];
     off = mk3(r.x, r.y, r.z);
     dbase = __float_as_uint(r.w);
+    valid = valid && dbase != kNoRecord;
   }
   unsigned nt[3] = {0u, 0u, 0u}, ne = 0u, nfb = 0u;  // tests, list entries scanned, fallback rays
   for (int t = by; t < fp.T; t += gy) {  // workgroup-uniform
@@ -1454,8 +1588,10 @@ static size_t echo_cap_of(const FrameParams& fp) { return ((size_t)fp.S * fp.R *
 
 static PairBufs pair_bufs(void* base, const FrameParams& fp) {
   PairBufs b{};
-  const size_t ecap = echo_cap_of(fp), hcap = (size_t)fp.S * fp.R * fp.H;
   const size_t slots = (size_t)fp.S * ((fp.R + 63) / 64) * 64;
+  // (multi-hit frames: room for the fixed per-bounce slots of the folded path, H * slots records)
+  const size_t ecap = std::max(echo_cap_of(fp), fp.H > 1 ? slots * fp.H : 0),
+               hcap = std::max((size_t)fp.S * fp.R * fp.H, fp.H > 1 ? slots * fp.H : 0);
   uint8_t* p = static_cast<uint8_t*>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) { uint8_t* q = p ? p + off : nullptr; off += align256(bytes); return q; };
@@ -1492,7 +1628,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf, uint32_t* pair_count,
                           hipStream_t st, const SideStream& echo, NearestMarks* marks) {
   if (fp.S == 0) return;
-  const PairBufs pb = pair_bufs(pair_buf, fp);
+  PairBufs pb = pair_bufs(pair_buf, fp);
   const unsigned groups = (unsigned)((size_t)fp.S * ((fp.R + 63) / 64));
   const unsigned path_blocks = (groups + kPathWaves - 1) / kPathWaves;
   const bool multi = fp.H > 1;
@@ -1514,6 +1650,10 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     return n > 0 ? n : 256;
   }();
   const bool hm = split && !multi && fp.TC == 1 && groups <= (unsigned)cus * 8u;
+  // Multi-hit frames with one batch slot and no hit outputs fold the path kernel into the nearest
+  // kernel (nearest_first_kernel<..., FOLD>): records at fixed per-bounce slots, no live list
+  const bool fold = split && multi && fp.TC == 1 && !L.has_hits;
+  pb.vp.fixed = fold ? groups * 64u : 0u;
   EchoFromHits eh;
   eh.fp = fp; eh.L = L; eh.origins = origins; eh.ray_order = ray_order; eh.pre = pb.pre;
 #define ART_VIS(S_, BLOCKS_, B_, EX_, OBB_, HM_)                                                                   \
@@ -1530,7 +1670,8 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // ... and the two as one launch on st (echo_muffle_kernel)
   const bool fused = hm2;
   eh.no_path = hm2 ? 1 : 0;
-  const unsigned mblocks = hm2 ? (groups + 3) / 4 : (unsigned)((hcap + 255) / 256);  // ray slots / hit records
+  const unsigned mblocks = hm2 ? (groups + 3) / 4
+                               : (unsigned)(((fold ? (size_t)groups * 64 * fp.H : hcap) + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over the grid (the rest looped)
 #define ART_MUFFLE(S_, EX_, OBB_, HM_)                                                                                  \
   hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, \
@@ -1554,13 +1695,18 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // fork costs ~10 us before the side stream starts). Without a side stream everything runs on st.
   const bool per_bounce = split && multi && ecnt;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
-#define ART_NEAREST(EX_, OBB_)                                                                                      \
-  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre, \
-                     pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr)
+#define ART_NEAREST(EX_, OBB_, F_)                                                                                  \
+  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order,      \
+                     pb.pre, pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr, L, block, pb.vp)
     const bool mark = marks && marks->used < marks->cap;
     if (mark) (void)hipEventRecord(marks->ev[2 * marks->used], st);
-    if (fp.exec) { if (obb) ART_NEAREST(true, true); else ART_NEAREST(true, false); }
-    else { if (obb) ART_NEAREST(false, true); else ART_NEAREST(false, false); }
+    if (fold) {
+      if (fp.exec) { if (obb) ART_NEAREST(true, true, true); else ART_NEAREST(true, false, true); }
+      else { if (obb) ART_NEAREST(false, true, true); else ART_NEAREST(false, false, true); }
+    } else {
+      if (fp.exec) { if (obb) ART_NEAREST(true, true, false); else ART_NEAREST(true, false, false); }
+      else { if (obb) ART_NEAREST(false, true, false); else ART_NEAREST(false, false, false); }
+    }
     if (mark) (void)hipEventRecord(marks->ev[2 * marks->used++ + 1], st);
 #undef ART_NEAREST
     hipStream_t pst = st;
@@ -1572,7 +1718,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
 #define ART_PATH(H_, M_)                                                                                              \
   hipLaunchKernelGGL((path_kernel<H_, M_>), dim3(path_blocks), dim3(64 * kPathWaves), 0, pst, sc, fp, L, origins, block, \
                      ray_order, pb.vp, pair_count, pb.pre, pb.state, k, (int)!hm)
-    if (hm2) {}
+    if (hm2 || fold) {}
     else if (L.has_hits) { if (multi) ART_PATH(true, true); else ART_PATH(true, false); }
     else { if (multi) ART_PATH(false, true); else ART_PATH(false, false); }
 #undef ART_PATH
