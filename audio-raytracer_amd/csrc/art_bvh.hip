@@ -122,6 +122,22 @@ __device__ __forceinline__ CullRec cull_empty() {
   return r;
 }
 
+// An empty node is stored as the box at +infinity (lo = hi = +inf, no margin): no finite ray enters
+// it (each axis' slab bounds are the same +-inf, so either the exit is -inf or the entry is +inf,
+// past every pruning bound and segment length), so the traversals need no emptiness test; a ray
+// that visits every node (non-finite or zero direction) enters it harmlessly (its slots are empty).
+__device__ __forceinline__ CullRec cull_stored(const CullRec& u) {
+  if (!(u.lox > u.hix)) return u;
+  CullRec r;
+  r.lox = r.loy = r.loz = r.hix = r.hiy = r.hiz = INFINITY;
+  r.scale = 0.0f; r.factor = 0.0f;
+  return r;
+}
+// union with a stored node (an empty one adds nothing)
+__device__ __forceinline__ void cull_union_stored(CullRec& a, const CullRec& b) {
+  if (!(b.lox == INFINITY && b.hix == INFINITY)) cull_union(a, b);
+}
+
 // Leaf j = sorted colliders [kBvhLeaf j, kBvhLeaf (j + 1)) (empty past the last); writes the
 // leaf references.
 // REFIT: the leaf order is kept (ref holds it) and only bounds and slots are recomputed.
@@ -178,7 +194,7 @@ __global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __r
     sl[0] = a; sl[1] = b;
     if (per == 4) { sl[2] = c; sl[3] = d; }
   }
-  leaves[j] = u;
+  leaves[j] = cull_stored(u);
 }
 
 // One inner level l (large trees: levels with more nodes than one workgroup handles quickly).
@@ -188,8 +204,8 @@ __global__ __launch_bounds__(256) void bvh_level_kernel(CullRec* __restrict__ no
   if (i >= cnt) return;
   const int g = first + i;
   CullRec u = cull_empty();
-  for (int k = 1; k <= 4; ++k) cull_union(u, nodes[4 * g + k]);
-  nodes[g] = u;
+  for (int k = 1; k <= 4; ++k) cull_union_stored(u, nodes[4 * g + k]);
+  nodes[g] = cull_stored(u);
 }
 
 // Inner levels top_level .. 0, bottom-up, in one workgroup (they hold a third of the leaf count).
@@ -199,8 +215,8 @@ __global__ __launch_bounds__(1024) void bvh_upper_kernel(CullRec* __restrict__ n
     for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
       const int g = first + i;
       CullRec u = cull_empty();
-      for (int k = 1; k <= 4; ++k) cull_union(u, nodes[4 * g + k]);
-      nodes[g] = u;
+      for (int k = 1; k <= 4; ++k) cull_union_stored(u, nodes[4 * g + k]);
+      nodes[g] = cull_stored(u);
     }
     __syncthreads();
   }

@@ -74,7 +74,7 @@ struct DevScene {
   // of node g at 4g + 1 .. 4g + 4) over a spatial order of the bounds' centres, kBvhLeaf colliders
   // per leaf; the leaves are nodes bvh_leaf0 .. bvh_leaf0 + 4^(levels - 1) - 1 (those past the
   // last collider are empty). A node's CullRec is the union of its colliders' bounds with their
-  // largest margin scale and factor; an empty node has lo > hi.
+  // largest margin scale and factor; an empty node is stored at +infinity (lo = hi = +inf, art_bvh.hip cull_stored).
   const CullRec* bvh;
   const uint32_t* bvh_ref;        // [ns + na + no] in leaf order: type rank << 30 | in-type index
   const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] slots in leaf order, 64 B (32 B when the

@@ -103,18 +103,17 @@ __device__ __forceinline__ int quad_perm(int v) { return __builtin_amdgcn_mov_dp
 constexpr int kQuadXor1 = 1 | (0 << 2) | (3 << 4) | (2 << 6), kQuadXor2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);
 constexpr int kQuadRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6), kQuadRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);
 
-// (distance, order) minimum over the quad's four lanes.
-__device__ __forceinline__ void quad_min(float& d, int& dc) {
+
+// (distance, order) keys (nearest_key) minimum over the quad: one 64-bit compare per DPP round.
+__device__ __forceinline__ unsigned long long quad_min_u64(unsigned long long v) {
   {
-    const float od = __int_as_float(quad_perm<kQuadXor1>(__float_as_int(d)));
-    const int oc = quad_perm<kQuadXor1>(dc);
-    if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
+    const unsigned long long o = ((unsigned long long)(uint32_t)quad_perm<kQuadXor1>((int)(v >> 32)) << 32) |
+                                 (uint32_t)quad_perm<kQuadXor1>((int)v);
+    v = o < v ? o : v;
   }
-  {
-    const float od = __int_as_float(quad_perm<kQuadXor2>(__float_as_int(d)));
-    const int oc = quad_perm<kQuadXor2>(dc);
-    if (od < d || (od == d && oc < dc)) { d = od; dc = oc; }
-  }
+  const unsigned long long o = ((unsigned long long)(uint32_t)quad_perm<kQuadXor2>((int)(v >> 32)) << 32) |
+                               (uint32_t)quad_perm<kQuadXor2>((int)v);
+  return o < v ? o : v;
 }
 
 // Quad reductions without ballots (the result lands in every lane of the quad).
@@ -301,8 +300,8 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
   float lim = FLT_MAX;   // pruning bound: best, and (shared work) the other quads' results for the ray
   bool shared = false;   // wave-uniform: work was shared in this wave
-  float mybest = FLT_MAX;  // this quad's own (distance, order) minimum over the leaves it tested
-  int mycode = kNoHit;
+  // this quad's own (distance, order) minimum over the leaves it tested, as a nearest_key (~0: none)
+  unsigned long long mykey = ~0ull;
   unsigned nsteps = 0;
   (void)nsteps;
   // branch-free pop of entries [bp, sp): the slot is read unconditionally (clamped), -1 when empty
@@ -323,7 +322,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     float tn;
     const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
-    const bool enter = (r.lox <= r.hix) & (force | (h & (en <= lim)));  // bitwise: no branch
+    const bool enter = force | (h & (en <= lim));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
     quad_descend(enter, en, force, qd, c0, my, g, sp);
     if (sp == bp) sp = bp = 0;
   };
@@ -333,14 +332,12 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     float dd;
     const bool h = leaf_slot_test<OBB, PERM>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, dd, tid, nt, sc.obbc);
     // no hit, NaN and FLT_MAX-or-more never win (strict < against float.MaxValue; the permeation
-    // cast: against INFINITY, so a hit at FLT_MAX counts)
-    float d = INFINITY;
-    int dc = kNoHit;
-    if (h && (PERM ? dd < INFINITY : dd < FLT_MAX)) { d = dd; dc = cc; }
-    quad_min(d, dc);
-    if (d < mybest || (d == mybest && dc < mycode)) {
-      mybest = d;
-      mycode = dc;
+    // cast: against INFINITY, so a hit at FLT_MAX counts). A hit distance is >= 0 or -0, so the key
+    // (distance bits, order code) orders as the reference's sequential strict-< first minimum.
+    const unsigned long long k = quad_min_u64(h && (PERM ? dd < INFINITY : dd < FLT_MAX) ? nearest_key(dd, cc) : ~0ull);
+    if (k < mykey) {
+      mykey = k;
+      const float d = __uint_as_float((uint32_t)(k >> 32));
       lim = fminf(lim, d);
       if (ART_NEAREST_STEAL && shared && qd == 0) atomicMin(s_bound + home, __float_as_int(d));
     }
@@ -379,7 +376,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
         const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
         const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
         const float dlim = __shfl(lim, src);
-        if (thief && mycode != kNoHit && qd == 0) atomicMin(s_key + home, nearest_key(mybest, mycode));
+        if (thief && mykey != ~0ull && qd == 0) atomicMin(s_key + home, mykey);
         if (thief) {  // the ray's derived values are recomputed as the home computed them
           g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
           sp = bp = 0;
@@ -388,7 +385,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
           om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
           force = force_all(s, om);
           lim = dlim;
-          mybest = FLT_MAX; mycode = kNoHit;  // (the finished ray's result went to its key above)
+          mykey = ~0ull;  // (the finished ray's result went to its key above)
         }
         if (robbed && ++bp == sp) sp = bp = 0;
       }
@@ -405,14 +402,13 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
 #ifdef ART_DIAG
   if (qd == 0 && alive) diag_add(2, nsteps);
 #endif
-  best = mybest;
-  code = mycode;
+  unsigned long long k = mykey;
   if (ART_NEAREST_STEAL && shared) {  // the ray's result: the minimum over the quads that traversed it
-    if (mycode != kNoHit && qd == 0) atomicMin(s_key + home, nearest_key(mybest, mycode));
-    const unsigned long long k = s_key[wq];
-    best = k == ~0ull ? FLT_MAX : __uint_as_float((uint32_t)(k >> 32));
-    code = k == ~0ull ? kNoHit : (int)(uint32_t)k;
+    if (mykey != ~0ull && qd == 0) atomicMin(s_key + home, mykey);
+    k = s_key[wq];
   }
+  best = k == ~0ull ? FLT_MAX : __uint_as_float((uint32_t)(k >> 32));
+  code = k == ~0ull ? kNoHit : (int)(uint32_t)k;
   if (ex) {
     exec_add(ex + kExecNearest, kExecSphere, wave_sum_u32(nt[0]));
     exec_add(ex + kExecNearest, kExecAabb, wave_sum_u32(nt[1]));
@@ -1064,7 +1060,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       const CullRec r = load_node(br, c0 + qd);
       float tn;
       const bool h = node_entry(s, r, om, tn);
-      const bool enter = (r.lox <= r.hix) & (force | (h & (tn <= maxd)));  // bitwise: no branch
+      const bool enter = force | (h & (tn <= maxd));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
       const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);
@@ -1517,7 +1513,7 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
         const CullRec r = load_node(bres, c0 + qd);
         float tn;
         const bool h = node_entry(s, r, om, tn);
-        const bool enter = (r.lox <= r.hix) & (force | h);
+        const bool enter = force | (h & (tn < INFINITY));  // (an empty node's entry is +inf: cull_stored)
         const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
         if (eb) {
           const int first = __builtin_ctz(eb);
