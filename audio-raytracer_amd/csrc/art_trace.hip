@@ -1107,6 +1107,41 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 
 // The echo traversal: one 64-pair batch per workgroup. EX: count the executed tests (fp.exec);
 // without it the counters compile out. 8 waves per SIMD.
+#ifdef ART_FUSE_ECHO
+// Experiment build only (the round-3 fused variant rebuilt): one-hit frames with one
+// batch slot and no hit outputs trace each wave's 16 echo rays right after their nearest hits, in
+// the same kernel (the muffle rays then run alone in muffle_kernel<..., HM>).
+#ifndef ART_FUSE_WAVES
+#define ART_FUSE_WAVES 8
+#endif
+template <bool OBB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FUSE_WAVES))) void nearest_echo_kernel(
+    DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order, int2* __restrict__ hits,
+    uint32_t* __restrict__ zero, uint32_t nzero, uint32_t* __restrict__ counters, VisPairs vp, uint8_t* __restrict__ block,
+    EchoFromHits eh) {
+  __shared__ uint32_t s_stk[kBvhStack * 64];
+  __shared__ int s_bound[64];
+  __shared__ unsigned long long s_key[64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nrb = (fp.R + 63) >> 6;
+  const int g = blockIdx.x;
+  const int rr = 16 * w + (lane >> 2);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
+  if (counters && blockIdx.x == 0 && threadIdx.x < 4) counters[threadIdx.x] = 0u;
+  const int fan = g / nrb;
+  const int slot = (g - fan * nrb) * 64 + rr;
+  const bool alive = slot < fp.R;
+  const int ray = alive ? ray_order[slot] : 0;
+  float best;
+  int code;
+  quad_nearest_core<false, OBB>(sc, make_seg(load3(origins, fan), load_dir(sc.dirs, ray)), alive, lane, s_stk + rr * kBvhStack,
+                                s_bound + 16 * w, s_key + 16 * w, best, code, nullptr);
+  if ((lane & 3) == 0) hits[(size_t)g * 64 + rr] = make_int2(__float_as_int(best), code);
+  __threadfence_block();  // (the echo traversal below reads this wave's own hit records)
+  vis_quad_body<OBB, true>(sc, vp, nullptr, nullptr, (uint32_t)g, s_stk, nullptr, -1, block, eh);
+}
+#endif
+
 template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEchoWaves<EX, OBB>)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, unsigned long long* ex,
@@ -1696,6 +1731,19 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                      pb.pre, pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr, L, block, pb.vp)
     const bool mark = marks && marks->used < marks->cap;
     if (mark) (void)hipEventRecord(marks->ev[2 * marks->used], st);
+#ifdef ART_FUSE_ECHO
+    if (hm2 && !fp.exec) {  // (experiment: nearest + echo in one kernel, then the muffle rays alone)
+      if (obb)
+        hipLaunchKernelGGL((nearest_echo_kernel<true>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre,
+                           muffle_acc, nacc, pair_count, pb.vp, block, eh);
+      else
+        hipLaunchKernelGGL((nearest_echo_kernel<false>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre,
+                           muffle_acc, nacc, pair_count, pb.vp, block, eh);
+      if (mark) (void)hipEventRecord(marks->ev[2 * marks->used++ + 1], st);
+      ART_MUFFLE_ANY(st);
+      return;
+    }
+#endif
     if (fold) {
       if (fp.exec) { if (obb) ART_NEAREST(true, true, true); else ART_NEAREST(true, false, true); }
       else { if (obb) ART_NEAREST(false, true, true); else ART_NEAREST(false, false, true); }

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Folded multi-bounce path + nearest leaf keys + stored-empty nodes: parity suite, then A/B
+# Folded multi-bounce path + nearest leaf keys + stored-empty nodes: parity suite, then A/B; the
+# rebuilt fused nearest+echo variant once at full size (parity + timing)
 set -uo pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r04d
@@ -7,5 +8,8 @@ mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; tail -3 $out/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" $out/pytest.log | head -20; exit $rc; }
 for c in 5 2 3; do bash tools/ab_rt.sh $c prefold fold base || exit 1; done
+ART_LIB=$PWD/variants/libart_fuse.so timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "full_size_bench_path_sampled" --timeout 200 --timeout-method thread > $out/fuse_pytest.log 2>&1
+rc=$?; echo "fused variant full-size parity rc=$rc"; tail -2 $out/fuse_pytest.log; [ $rc -eq 0 ] || exit $rc
+for c in 2 3; do bash tools/ab_rt.sh $c fuse || exit 1; done
 PMC_ARGS="--config 2" bash tools/pmc_sq.sh prefold || exit 1
 cp audio-raytracer_amd/lib/libart.so variants/libart_base.so && PMC_ARGS="--config 2" bash tools/pmc_sq.sh base || exit 1
