@@ -1697,7 +1697,11 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   } while (0)
   // One-hit frames with one batch slot, no hit outputs (HM2): no path kernel at all; the echo
   // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too.
-  const bool hm2 = hm && !L.has_hits;
+  // (ART_HM2_ANY: also frames past one round of echo waves, which have no path kernel to starve)
+#ifndef ART_HM2_ANY
+#define ART_HM2_ANY 0
+#endif
+  const bool hm2 = (hm || (ART_HM2_ANY && split && !multi && fp.TC == 1)) && !L.has_hits;
   // ... and the two as one launch on st (echo_muffle_kernel)
   const bool fused = hm2;
   eh.no_path = hm2 ? 1 : 0;

@@ -11,5 +11,7 @@ for c in 5 2 3; do bash tools/ab_rt.sh $c prefold fold base || exit 1; done
 ART_LIB=$PWD/variants/libart_fuse.so timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -x -q -m gpu -k "full_size_bench_path_sampled" --timeout 200 --timeout-method thread > $out/fuse_pytest.log 2>&1
 rc=$?; echo "fused variant full-size parity rc=$rc"; tail -2 $out/fuse_pytest.log; [ $rc -eq 0 ] || exit $rc
 for c in 2 3; do bash tools/ab_rt.sh $c fuse || exit 1; done
+bash tools/ab_rt.sh 4 base hm2any || exit 1
+bash tools/r04_rebuild.sh || exit 1
 PMC_ARGS="--config 2" bash tools/pmc_sq.sh prefold || exit 1
 cp audio-raytracer_amd/lib/libart.so variants/libart_base.so && PMC_ARGS="--config 2" bash tools/pmc_sq.sh base || exit 1
