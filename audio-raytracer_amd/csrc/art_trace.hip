@@ -252,9 +252,9 @@ template <bool EX, bool OBB>
 constexpr int kNearestWaves = EX ? 6 : (OBB ? ART_NEAREST_OBB_WAVES : 8);
 template <bool EX, bool OBB>
 constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
-// echo_muffle_kernel<false, true>: 7 waves per SIMD (67 VGPRs) without spills; at 8 it spills 2
+// echo_muffle_kernel<false, true>: 8 waves per SIMD (64 VGPRs) without spills
 #ifndef ART_ECHO_MUFFLE_OBB_WAVES
-#define ART_ECHO_MUFFLE_OBB_WAVES 7
+#define ART_ECHO_MUFFLE_OBB_WAVES 8
 #endif
 // k-th (0-based) set bit of m, k < popcount(m).
 __device__ __forceinline__ int select_bit(unsigned long long m, int k) {
@@ -376,14 +376,18 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
         const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
         const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
         const float dlim = __shfl(lim, src);
+        // the ray's derived values too (1/d, 2a, |o|_1, force: the home's own values, so no divisions)
+        const float ix = __shfl(s.inv.x, src), iy = __shfl(s.inv.y, src), iz = __shfl(s.inv.z, src);
+        const float da2 = __shfl(s.a2, src), dom = __shfl(om, src);
+        const int dforce = __shfl((int)force, src);
         if (thief && mykey != ~0ull && qd == 0) atomicMin(s_key + home, mykey);
-        if (thief) {  // the ray's derived values are recomputed as the home computed them
+        if (thief) {
           g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
           sp = bp = 0;
           home = dhome;
-          s = make_seg(mk3(ox, oy, oz), mk3(dx, dy, dz));
-          om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
-          force = force_all(s, om);
+          s.o = mk3(ox, oy, oz); s.d = mk3(dx, dy, dz); s.inv = mk3(ix, iy, iz); s.a2 = da2;
+          om = dom;
+          force = dforce != 0;
           lim = dlim;
           mykey = ~0ull;  // (the finished ray's result went to its key above)
         }
@@ -1043,13 +1047,17 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
       const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
       const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
       const float dmaxd = __shfl(maxd, src);
-      if (thief) {  // the segment's derived values are recomputed as the home computed them
+      // the segment's derived values too (1/d, 2a, |o|_1 + maxd, force: the home's own, no divisions)
+      const float ix = __shfl(s.inv.x, src), iy = __shfl(s.inv.y, src), iz = __shfl(s.inv.z, src), dom = __shfl(om, src);
+      const float da2 = __shfl(s.a2, src);
+      const int dforce = __shfl((int)force, src);
+      if (thief) {
         g = (int)s_wave[(src >> 2) * kBvhStack + dbp];
         sp = bp = 0;
         home = dhome; owner = downer; maxd = dmaxd;
-        s = make_seg(mk3(ox, oy, oz), mk3(dx, dy, dz));
-        om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
-        force = force_all(s, om);
+        s.o = mk3(ox, oy, oz); s.d = mk3(dx, dy, dz); s.inv = mk3(ix, iy, iz); s.a2 = da2;
+        om = dom;
+        force = dforce != 0;
       }
       if (robbed && ++bp == sp) sp = bp = 0;
     }
