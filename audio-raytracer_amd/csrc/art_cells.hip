@@ -183,13 +183,10 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, lon
 }
 
 // One work-item per (target, collider, face, cell row), grid-stride: tests the row's cells of the
-// pair's face rectangle. FILL = false counts per cell (and per target, for the capacity check);
-// FILL = true writes the entries of the targets whose lists fit (cells_fit_kernel).
-// The 6 * kCellG = 192 rows of a pair are 3 whole waves (the work-item count is a multiple of 64),
-// so a wave's target is uniform and its entries per target are summed before one atomic.
+// pair's face rectangle. FILL = false counts per cell; FILL = true writes the entries of the targets
+// whose lists fit (cells_fit_kernel).
 template <bool FILL>
 __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restrict__ geo, long long pairs, CellBufs cb, int n) {
-  static_assert((6 * kCellG) % 64 == 0, "a pair's rows are whole waves");
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < pairs * (6 * kCellG);
        k += (long long)gridDim.x * blockDim.x) {
     const long long p = k / (6 * kCellG);
@@ -197,7 +194,6 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
     const int t = (int)(p / n);
     const CellGeo G = geo[p];
     const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
-    uint32_t nhit = 0;
     // (rows outside the pair's face rectangle, and the dropped targets' rows in the fill pass, test nothing)
     const bool rows = !(j < j0 || j > j1 || i0 > i1) && (!FILL || cb.ok[t]);
     const uint32_t ty = G.code >> 28;  // one list per collider type
@@ -211,7 +207,6 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
       if (!hit) continue;
       if (!FILL) {
         atomicAdd(cnt + 3 * c, 1u);
-        ++nhit;
       } else {
         const uint32_t pos = atomicAdd(cur + 3 * c, 1u);
         if (pos < cb.cap) {  // the entry and its sort key (the segmented sort orders each cell by near bound)
@@ -223,11 +218,23 @@ __global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restric
         else cb.ok[t] = 0u;  // (cannot happen after the capacity check; kept as a guard)
       }
     }
-    if (!FILL) {  // wave-uniform target
-      const unsigned long long sum = wave_sum_u32(nhit);
-      if ((threadIdx.x & 63) == 0 && sum) atomicAdd(cb.tcount + t, sum);
-    }
   }
+}
+
+// Entries per target (64-bit sums of its cells' counts; one workgroup per target), for the
+// capacity check. (Per-entry atomics on T counters serialized the count pass: 90 -> 264 us.)
+__global__ __launch_bounds__(256) void cells_total_kernel(CellBufs cb) {
+  __shared__ unsigned long long s[256];
+  const uint32_t* c = cb.count + (size_t)blockIdx.x * kCells * 3;
+  unsigned long long v = 0;
+  for (int i = threadIdx.x; i < kCells * 3; i += 256) v += c[i];
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) s[threadIdx.x] += s[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cb.tcount[blockIdx.x] = s[0];
 }
 
 // Capacity check between the count and the fill: targets in order keep their lists while the
@@ -305,13 +312,13 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
     return 0;
   }
   if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
-  if (hipMemsetAsync(cb.tcount, 0, (size_t)T * sizeof(unsigned long long), st) != hipSuccess) return -1;
   const long long pairs = (long long)n * T;
   CellGeo* geo = reinterpret_cast<CellGeo*>(cb.geo);
   if (pairs > 0) {
     hipLaunchKernelGGL(cells_geo_kernel, dim3(stride_grid(pairs)), dim3(256), 0, st, sc, cb, T, geo);
     hipLaunchKernelGGL(cells_row_kernel<false>, dim3(stride_grid(pairs * 6 * kCellG)), dim3(256), 0, st, geo, pairs, cb, n);
   }
+  if (T > 0) hipLaunchKernelGGL(cells_total_kernel, dim3(T), dim3(256), 0, st, cb);
   hipLaunchKernelGGL(cells_fit_kernel, dim3(1), dim3(64), 0, st, cb, T);
   hipLaunchKernelGGL(cells_drop_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, cb, (uint32_t)cells);
   size_t bytes = cb.temp_bytes;

@@ -1704,10 +1704,11 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true, HM_); else ART_VIS(S_, BLOCKS_, B_, false, false, HM_); }       \
   } while (0)
   // One-hit frames with one batch slot, no hit outputs (HM2): no path kernel at all; the echo
-  // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too.
-  // (ART_HM2_ANY: also frames past one round of echo waves, which have no path kernel to starve)
+  // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too. Also
+  // frames past one round of echo waves, which have no path kernel to starve (config 4: 1.684 ->
+  // 1.660 ms/step; ART_HM2_ANY=0 restores the path-kernel plan for them)
 #ifndef ART_HM2_ANY
-#define ART_HM2_ANY 0
+#define ART_HM2_ANY 1
 #endif
   const bool hm2 = (hm || (ART_HM2_ANY && split && !multi && fp.TC == 1)) && !L.has_hits;
   // ... and the two as one launch on st (echo_muffle_kernel)
