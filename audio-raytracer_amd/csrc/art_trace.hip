@@ -1373,8 +1373,9 @@ __device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uin
   }
 }
 
+// 8 waves per SIMD; the counting OBB instantiations at 7, where they need no spills
 template <bool EX, bool OBB, bool HM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EX && OBB ? 7 : 8))) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
                                                      const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
                                                      EchoFromHits eh) {
   muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x, (int)blockIdx.y, (int)gridDim.y);

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 out=gpurun_out/r04_rebuild
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py --config 2 --no-cpu-baseline --frames 5 --steps 50 > $out/bench.log 2>&1 || exit 1
-tail -1 $out/bench.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); d=r['dynamic']; print('dynamic %.4f rebuild p50 %.4f' % (d['ms_per_step_dynamic'], d['p50_frame_ms_rebuild']))"
+grep '^{' $out/bench.log | tail -1 | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); d=r['dynamic']; print('dynamic %.4f rebuild p50 %.4f' % (d['ms_per_step_dynamic'], d['p50_frame_ms_rebuild']))"
 python3 - $out/trace/run_kernel_stats.csv <<'PY'
 import csv, sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: -float(r["TotalDurationNs"]))

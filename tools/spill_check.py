@@ -47,14 +47,14 @@ for k in kernels:
             loop = line.split(";", 1)[1].strip() if ("Loop" in line and ";" in line) else "not in a loop"
         elif "Loop Header" in line or "in Loop" in line or "Parent Loop" in line:
             loop = line.split(";", 1)[1].strip()
-        m = re.search(r"scratch_(store|load)_dword\w*\s.*?(offset:(\d+))?\s*;", line)
+        m = re.search(r"scratch_(store|load)_dword\w*\s", line)
         if m:
             off = re.search(r"offset:(\d+)", line)
             sites.append((m.group(1), int(off.group(1)) if off else 0, loop))
     name = demangle(k["name"])
     if not sites:
         continue
-    print(f"{name}: {len(sites)} scratch ops")
-    for kind, off, lp in sites:
+    print(f"{name[:160]}: {len(sites)} scratch ops")
+    for kind, off, lp in sites[:int(os.environ.get("SPILL_SITES", "1000"))]:
         print(f"   {kind:5s} slot {off:3d}  {lp}")
 print("kernels with scratch:", sum(1 for k in kernels if any("scratch_" in l for l in k["lines"])), "of", len(kernels))
