@@ -100,10 +100,25 @@ ART_HD void prep_obb(const art_obb& b, int i, int gi, ObbRec* __restrict__ oobb,
   c.pad0 = c.pad1 = 0.0f;
   oobb[i] = r;
   oobbc[i] = c;
-  // bounding sphere of the box (|h|_1 >= |h|_2), whatever the rotation
-  const float rho = (fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz)) * 1.001f;
+  // World bounds of the rotated box (round 4; round 3 used the cube of half-width |h|_1, up to 8x the
+  // volume). The tests map P - c to the local frame by the stored rotation R (ShootRayCast
+  // :314-320, permeation loss :294-300) or by its inverse R^T (permeation first hit :172-179), so a
+  // point reported inside the local box [-h, h] lies within half_i = max(sum_j |R_ji| h_j,
+  // sum_j |R_ij| h_j) of c on world axis i. Column i of R is qmul(q, e_i); the relative and absolute
+  // slack covers the rounding of these entries (each within ~10 eps), the margins the rest
+  // (the margin scale keeps |h|_1).
+  const float h1 = fabsf(c.hx) + fabsf(c.hy) + fabsf(c.hz);
+  const float rho = h1 * 1.001f;
   const bool qok = ufinite(q.x) && ufinite(q.y) && ufinite(q.z) && ufinite(q.w);
-  cull[gi] = make_cull(r.cx - rho, r.cy - rho, r.cz - rho, r.cx + rho, r.cy + rho, r.cz + rho,
+  const vec3 ax = qmul(q, mk3(1.0f, 0.0f, 0.0f)), ay = qmul(q, mk3(0.0f, 1.0f, 0.0f)), az = qmul(q, mk3(0.0f, 0.0f, 1.0f));
+  const vec3 ha = abs3(mk3(c.hx, c.hy, c.hz));
+  const vec3 cx = abs3(ax), cy = abs3(ay), cz = abs3(az);  // |columns| of R
+  const float slack = 1e-5f * h1;
+  const float wx = fmaxf(cx.x * ha.x + cx.y * ha.y + cx.z * ha.z, cx.x * ha.x + cy.x * ha.y + cz.x * ha.z);
+  const float wy = fmaxf(cy.x * ha.x + cy.y * ha.y + cy.z * ha.z, cx.y * ha.x + cy.y * ha.y + cz.y * ha.z);
+  const float wz = fmaxf(cz.x * ha.x + cz.y * ha.y + cz.z * ha.z, cx.z * ha.x + cy.z * ha.y + cz.z * ha.z);
+  const float bx = fminf(wx * 1.0001f + slack, rho), by = fminf(wy * 1.0001f + slack, rho), bz = fminf(wz * 1.0001f + slack, rho);
+  cull[gi] = make_cull(r.cx - bx, r.cy - by, r.cz - bz, r.cx + bx, r.cy + by, r.cz + bz,
                        qok ? fabsf(r.cx) + fabsf(r.cy) + fabsf(r.cz) + rho : INFINITY, kCullObb);
 }
 

@@ -386,14 +386,11 @@ def stage_kernels(cfg, S, has_obb):
     """The kernels of the timed raytrace stage as launch_raytrace_fast (csrc/art_trace.hip) picks
     them for this frame shape (no hit outputs, as the bench launches it)."""
     obb = "true" if has_obb else "false"
-    groups = S * ((cfg.R + 63) // 64)
-    if cfg.H > 1:
-        return (f"per bounce: nearest_first_kernel<false, {obb}> -> path_kernel<false, true>, that bounce's echo "
+    if cfg.H > 1:  # one batch slot, no hit outputs: the path kernel's work runs in the nearest kernel (FOLD)
+        return (f"per bounce: nearest_first_kernel<false, {obb}, true> (path epilogue folded in), that bounce's echo "
                 f"vis_kernel<false, {obb}, false> on the side stream; then muffle_kernel<false, {obb}, false>")
-    if groups <= 8 * 256:  # one round of echo waves on 256 CUs: echo + muffle from the nearest hits, one launch
-        return f"nearest_first_kernel<false, {obb}> -> echo_muffle_kernel<false, {obb}> (one stream, no path kernel)"
-    return (f"nearest_first_kernel<false, {obb}> -> path_kernel<false, false> -> echo vis_kernel<false, {obb}, false>; "
-            f"muffle_kernel<false, {obb}, false> on the side stream")
+    # one-hit frames, one batch slot, no hit outputs (any size): echo + muffle from the nearest hits, one launch
+    return f"nearest_first_kernel<false, {obb}, false> -> echo_muffle_kernel<false, {obb}> (one stream, no path kernel)"
 
 
 def jitter_records(rng, recs, scale):
@@ -725,7 +722,8 @@ def main():
         "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
         "allgather_note": "HIP events on the launch stream around the all-gather of every 8th timed step, max over "
                           "ranks; the step time includes it" if world > 1 else None,
-        "roofline": {"bound": "valu", "kernel": f"nearest_first_kernel<false, {'true' if scene.obbs.size > 0 else 'false'}>",
+        "roofline": {"bound": "valu", "kernel": f"nearest_first_kernel<false, {'true' if scene.obbs.size > 0 else 'false'}, "
+                                                    f"{'true' if cfg.H > 1 else 'false'}>",
                      "achieved": near_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": near_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": near_traffic,
                      "kernel_ms": near_ms, "launches_per_frame": ktimes["nearest_launches"] / n_rt,
