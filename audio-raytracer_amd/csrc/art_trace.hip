@@ -1218,12 +1218,12 @@ __device__ bool muffle_brute(const DevScene& sc, const Seg& s, float maxd, int t
 // HM: one-hit frames with one batch slot whose path kernel does not run: lane i is ray slot i
 // (64-ray group i / 64) and its muffle rays start from the nearest hit as the path kernel computes
 // it (hit_from_pre); the accumulator base is fan * T (TC == 1: batch slot 0).
+// i = this lane's hit record / ray slot (i - lane wave-uniform); targets by, by + gy, ...
 template <bool EX, bool OBB, bool HM>
 __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParams& fp, const VisPairs& vp,
                                             const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
-                                            const EchoFromHits& eh, uint32_t bx, int by, int gy) {
+                                            const EchoFromHits& eh, uint32_t i, int by, int gy) {
   const int lane = threadIdx.x & 63;
-  const uint32_t i = bx * 256u + threadIdx.x;
   // (fixed slots: every bounce's records, kNoRecord marking the slots with no hit)
   const uint32_t n = HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u : (vp.fixed ? vp.fixed * (uint32_t)fp.H : ldc(count, 1));
   if (__builtin_amdgcn_readfirstlane(i - (uint32_t)lane) >= n) return;
@@ -1378,7 +1378,7 @@ template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EX && OBB ? 7 : 8))) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
                                                      const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
                                                      EchoFromHits eh) {
-  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x, (int)blockIdx.y, (int)gridDim.y);
+  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x * 256u + threadIdx.x, (int)blockIdx.y, (int)gridDim.y);
 }
 
 // One-hit frames with one batch slot and no path kernel (HM2): the echo traversal and the muffle
@@ -1399,7 +1399,7 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
   uint32_t rb;
   int t;
   muffle_block(blockIdx.x - groups, mblocks, mt, rb, t);  // (groups is a multiple of 8 in the bench shapes)
-  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, rb, t, mt);
+  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, rb * 256u + threadIdx.x, t, mt);
 }
 
 // ------------------------------------------------------------------------------------------
