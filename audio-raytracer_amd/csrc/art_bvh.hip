@@ -333,7 +333,10 @@ __device__ __forceinline__ void kd_block_scan3(int v[3], int (*s_wave)[16]) {
 // Surface-area split costs on the upper binary levels (at most kKdSahSegs segments): for each
 // segment and axis, the bounds of the two halves the split on that axis would make, accumulated in
 // LDS as order-preserving integers (atomic min / max).
-constexpr int kKdSahSegs = 64;
+#ifndef ART_KD_SAH_SEGS
+#define ART_KD_SAH_SEGS 64
+#endif
+constexpr int kKdSahSegs = ART_KD_SAH_SEGS;
 __device__ __forceinline__ int kd_ord(float f) {  // monotone float -> int (for atomicMin / atomicMax)
   const int b = __float_as_int(f);
   return b >= 0 ? b : b ^ 0x7fffffff;

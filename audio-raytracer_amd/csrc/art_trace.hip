@@ -162,7 +162,11 @@ __device__ __forceinline__ void quad_descend(bool enter, float en, bool force, i
                  k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
   const int rank = (int)(k1 < key) + (int)(k2 < key) + (int)(k3 < key);
   const uint32_t kmin = min(min(key, k1), min(k2, k3));
+#if ART_NENT_BALLOT
+  const int nent = __popc((uint32_t)(__ballot(enter) >> (__lane_id() & ~3)) & 0xFu);
+#else
   const int nent = quad_max_i32(enter ? rank + 1 : 0);
+#endif
   if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
   if (nent) {
     g = c0 + (int)(kmin & 3u);
@@ -237,6 +241,12 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #endif
 #ifndef ART_NEAREST_STEAL
 #define ART_NEAREST_STEAL 1
+#endif
+#ifndef ART_STEAL_MIN_IDLE  // idle quads a wave waits for before it shares work (A/B knob)
+#define ART_STEAL_MIN_IDLE 1
+#endif
+#ifndef ART_NENT_BALLOT     // entered-children count by ballot instead of a quad DPP maximum (A/B knob)
+#define ART_NENT_BALLOT 0
 #endif
 constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
 
@@ -359,7 +369,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     }
     if (ART_NEAREST_STEAL) {
       const unsigned long long donors = __ballot(sp > bp) & kQuad0, idle = ~act & kQuad0;
-      if (donors && idle) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
+      if (donors && __popcll(idle) >= ART_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
         if (!shared) {       // publish every ray's bound once
           shared = true;
           if (qd == 0) s_bound[wq] = __float_as_int(lim);
