@@ -251,7 +251,6 @@ static void launch_bvh_upper(CullRec* nodes, int L, hipStream_t st) {
 // per level.
 // ------------------------------------------------------------------------------------------
 constexpr int kKdMaxColliders = 1 << 14;
-constexpr int kKdChunk = kKdMaxColliders / 1024;  // positions per thread
 
 struct KdBufs {
   float4* cen;          // [n] centre (non-finite components -> FLT_MAX)
@@ -347,18 +346,38 @@ __device__ __forceinline__ float kd_area(float ex, float ey, float ez) {
   return ex * ey + ey * ez + ez * ex;
 }
 
+// CAP: the largest scene of the instantiation. Up to kKdLdsBounds colliders the bounds live in LDS
+// too (6 floats each), so the surface-area pass and the axis choice read no global memory (round 4:
+// their dependent global gathers were most of the kernel's 144 us at 4096 colliders).
+constexpr int kKdLdsBounds = 4096;
+template <int CAP>
 __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap, int* __restrict__ perm) {
-  __shared__ uint16_t s_p[3][kKdMaxColliders];        // the three index arrays
-  __shared__ uint8_t s_side[kKdMaxColliders];         // 1: left half of its segment (by collider id)
-  __shared__ int8_t s_axis[kKdMaxColliders / 8];      // per segment: split axis, -1 = fits its left half
-  __shared__ uint16_t s_segpre[3][kKdMaxColliders / 8];  // left-flag prefix at each segment's start
+  constexpr bool LB = CAP <= kKdLdsBounds;
+  __shared__ uint16_t s_p[3][CAP];        // the three index arrays
+  __shared__ uint8_t s_side[CAP];         // 1: left half of its segment (by collider id)
+  __shared__ int8_t s_axis[CAP / 8];      // per segment: split axis, -1 = fits its left half
+  __shared__ uint16_t s_segpre[3][CAP / 8];  // left-flag prefix at each segment's start
   __shared__ int s_wave[3][16];
   __shared__ int s_box[2][3][kKdSahSegs][6];  // [half][axis][segment]: lo.xyz, hi.xyz (kd_ord)
+  __shared__ float s_bb[LB ? 6 : 1][LB ? CAP : 1];  // LB: lo.xyz, hi.xyz by collider id
   const int tid = threadIdx.x;
+  constexpr int kChunk = CAP / 1024;  // positions per thread
   const int chunk = (n + 1023) / 1024;
   const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
   for (int x = 0; x < 3; ++x)
     for (int i = tid; i < n; i += 1024) s_p[x][i] = (uint16_t)k.p[(size_t)x * n + i];
+  if (LB)
+    for (int i = tid; i < n; i += 1024) {
+      const CullRec c = k.cull[i];
+      s_bb[0][i] = c.lox; s_bb[1][i] = c.loy; s_bb[2][i] = c.loz;
+      s_bb[3][i] = c.hix; s_bb[4][i] = c.hiy; s_bb[5][i] = c.hiz;
+    }
+  // centre component a of collider v (kd_cen_kernel's value: non-finite -> FLT_MAX)
+  auto cen = [&](int v, int a) -> float {
+    if (!LB) return kd_comp(k.cen[v], a);
+    const float c = 0.5f * (s_bb[a][v] + s_bb[3 + a][v]);
+    return isfinite(c) ? c : FLT_MAX;
+  };
   __syncthreads();
   for (int lg = 31 - __builtin_clz(cap); lg > 2; --lg) {  // segments of seg = 2^lg positions (cap: a power of 4)
     const int seg = 1 << lg, half = seg >> 1, nseg = (n + seg - 1) >> lg;
@@ -385,9 +404,14 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
           const int kk = ((i >> lg) << 1) | ((i & (seg - 1)) >= half ? 1 : 0);
           if (kk != key && !wave_one) { flush(); }
           key = kk;
-          const CullRec c = k.cull[s_p[x][i]];
-          b[0] = fminf(b[0], c.lox); b[1] = fminf(b[1], c.loy); b[2] = fminf(b[2], c.loz);
-          b[3] = fmaxf(b[3], c.hix); b[4] = fmaxf(b[4], c.hiy); b[5] = fmaxf(b[5], c.hiz);
+          const int v = s_p[x][i];
+          if (LB) {
+            for (int q = 0; q < 3; ++q) { b[q] = fminf(b[q], s_bb[q][v]); b[3 + q] = fmaxf(b[3 + q], s_bb[3 + q][v]); }
+          } else {
+            const CullRec c = k.cull[v];
+            b[0] = fminf(b[0], c.lox); b[1] = fminf(b[1], c.loy); b[2] = fminf(b[2], c.loz);
+            b[3] = fmaxf(b[3], c.hix); b[4] = fmaxf(b[4], c.hiy); b[5] = fmaxf(b[5], c.hiz);
+          }
         }
         if (wave_one) {  // (wave-uniform) min / max over the wave, then lane 0 publishes
           for (int q = 0; q < 6; ++q)
@@ -421,7 +445,7 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       if (cnt > half && ax < 0) {
         float best = -1.0f;
         for (int x = 0; x < 3; ++x) {
-          const float e = kd_comp(k.cen[s_p[x][a0 + cnt - 1]], x) - kd_comp(k.cen[s_p[x][a0]], x);
+          const float e = cen(s_p[x][a0 + cnt - 1], x) - cen(s_p[x][a0], x);
           if (ax < 0 || e > best) { best = e; ax = x; }
         }
       }
@@ -433,13 +457,13 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       if (ax >= 0) s_side[s_p[ax][i]] = (i & (seg - 1)) < half ? 1 : 0;
     }
     __syncthreads();
-    uint32_t pk[3][kKdChunk / 2];  // the chunk's ids, two u16 per register
+    uint32_t pk[3][kChunk / 2];  // the chunk's ids, two u16 per register
     for (int x = 0; x < 3; ++x)
-      for (int j = 0; j < kKdChunk / 2; ++j) pk[x][j] = 0u;
+      for (int j = 0; j < kChunk / 2; ++j) pk[x][j] = 0u;
     uint32_t fl[3] = {0u, 0u, 0u};
     int c[3] = {0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < kKdChunk; ++j) {
+    for (int j = 0; j < kChunk; ++j) {
       const int i = i0 + j;
       if (i < i1) {
         const int ax = s_axis[i >> lg];
@@ -456,7 +480,7 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
     {
       int run[3] = {c[0], c[1], c[2]};
 #pragma unroll
-      for (int j = 0; j < kKdChunk; ++j) {
+      for (int j = 0; j < kChunk; ++j) {
         const int i = i0 + j;
         if (i < i1) {
           const bool start = (i & (seg - 1)) == 0;
@@ -471,7 +495,7 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
     {  // stable partition of every array: left half first
       int run[3] = {c[0], c[1], c[2]};
 #pragma unroll
-      for (int j = 0; j < kKdChunk; ++j) {
+      for (int j = 0; j < kChunk; ++j) {
         const int i = i0 + j;
         if (i < i1) {
           const int s = i >> lg, a0 = s << lg;
@@ -561,7 +585,10 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
                                              st) != hipSuccess)
         return -1;
     }
-    if (n <= kKdMaxColliders) hipLaunchKernelGGL(kd_split_kernel, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
+    if (n <= kKdLdsBounds)
+      hipLaunchKernelGGL(kd_split_kernel<kKdLdsBounds>, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
+    else if (n <= kKdMaxColliders)
+      hipLaunchKernelGGL(kd_split_kernel<kKdMaxColliders>, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
     else if (launch_kd_big(k, n, nleaf * kBvhLeaf, sb, st) != 0) return -1;
   } else {  // Morton order of the centres (larger scenes)
     hipLaunchKernelGGL(scene_box_kernel, dim3(1), dim3(1024), 0, st, sc.cull, n, sb.box);

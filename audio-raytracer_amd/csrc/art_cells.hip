@@ -99,16 +99,29 @@ struct alignas(16) CellGeo {
   uint32_t pad[2];
 };
 
+// Each pair's face rectangles also as one packed word per (target, face, collider), after the T * n
+// CellGeo records: the row passes read 4 coalesced bytes per item and fetch the 64-B record only
+// for the rows the rectangle covers.
+__device__ __forceinline__ uint32_t* cell_rects(CellGeo* geo, int T, int n) {
+  return reinterpret_cast<uint32_t*>(geo + (size_t)T * n);
+}
+__device__ __forceinline__ void cell_rects_write(CellGeo* geo, int T, int n, int t, int g, const CellGeo& G) {
+  uint32_t* r = cell_rects(geo, T, n);
+  for (int f = 0; f < 6; ++f)
+    r[((size_t)t * 6 + f) * n + g] = (uint32_t)G.rect[f][0] | ((uint32_t)G.rect[f][1] << 8) | ((uint32_t)G.rect[f][2] << 16) |
+                                     ((uint32_t)G.rect[f][3] << 24);
+}
+
 // One thread per (target, collider).
 // (grid-stride over the pairs: one launch stays far below HIP's 2^32 work-item limit)
-__device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, long long k, CellGeo* __restrict__ geo);
+__device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int T, long long k, CellGeo* __restrict__ geo);
 __global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb, int T, CellGeo* __restrict__ geo) {
   const int n = sc.ns + sc.na + sc.no;
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < (long long)n * T;
        k += (long long)gridDim.x * blockDim.x)
-    cells_geo_one(sc, cb, n, k, geo);
+    cells_geo_one(sc, cb, n, T, k, geo);
 }
-__device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, long long k, CellGeo* __restrict__ geo) {
+__device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int T, long long k, CellGeo* __restrict__ geo) {
   const int t = (int)(k / n), g = (int)(k - (long long)t * n);
   CellGeo G;
   for (int f = 0; f < 6; ++f) { G.rect[f][0] = 1; G.rect[f][1] = 0; G.rect[f][2] = 1; G.rect[f][3] = 0; }
@@ -120,7 +133,7 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, lon
   G.all = 0u;
   G.ux = G.uy = G.uz = G.sb = G.cb = G.near = 0.0f;
   // owned by the target (its muffle rays skip it, :413, :426, :439) or no lists: no cells
-  if (!cb.ok[t] || tid == t) { geo[k] = G; return; }
+  if (!cb.ok[t] || tid == t) { geo[k] = G; cell_rects_write(geo, T, n, t, g, G); return; }
   // The collider's bounding sphere and its error margin. Every test's rounding is relative to the
   // segment-start-to-collider vector (the operands o and the record are exact floats): a reported
   // blocking point lies within factor * (|o - c| + |h|_1) of the shape,
@@ -180,44 +193,72 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, lon
     G.rect[f][0] = (uint8_t)i0; G.rect[f][1] = (uint8_t)i1; G.rect[f][2] = (uint8_t)j0; G.rect[f][3] = (uint8_t)j1;
   }
   geo[k] = G;
+  cell_rects_write(geo, T, n, t, g, G);
 }
 
-// One work-item per (target, collider, face, cell row), grid-stride: tests the row's cells of the
-// pair's face rectangle. FILL = false counts per cell; FILL = true writes the entries of the targets
-// whose lists fit (cells_fit_kernel).
+// One workgroup per (target, face, cell row) and 256 colliders (grid-stride over these units): each
+// work-item tests the row's cells of its collider's face rectangle against the pair's cone, and the
+// workgroup aggregates its hits per (cell, collider type) in LDS, so the global counters see one
+// atomic per touched (cell, type) and workgroup instead of one per entry (round 4: the per-entry
+// atomics and the 64-B record per item set the passes' 96 + 107 us at config 2). FILL = false
+// counts per cell; FILL = true reserves each (cell, type)'s range once and writes the entries of the
+// targets whose lists fit (cells_fit_kernel).
 template <bool FILL>
-__global__ __launch_bounds__(256) void cells_row_kernel(const CellGeo* __restrict__ geo, long long pairs, CellBufs cb, int n) {
-  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < pairs * (6 * kCellG);
-       k += (long long)gridDim.x * blockDim.x) {
-    const long long p = k / (6 * kCellG);
-    const int fr = (int)(k - p * (6 * kCellG)), f = fr / kCellG, j = fr - f * kCellG;
-    const int t = (int)(p / n);
-    const CellGeo G = geo[p];
-    const int i0 = G.rect[f][0], i1 = G.rect[f][1], j0 = G.rect[f][2], j1 = G.rect[f][3];
-    // (rows outside the pair's face rectangle, and the dropped targets' rows in the fill pass, test nothing)
+__global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ geo, int T, CellBufs cb, int n) {
+  __shared__ uint32_t s_cnt[kCellG * 3], s_base[kCellG * 3];
+  const int tid = threadIdx.x;
+  const int chunks = (n + 255) >> 8;
+  const long long units = (long long)T * 6 * kCellG * chunks;
+  const uint32_t* rects = cell_rects(geo, T, n);
+  for (long long u = blockIdx.x; u < units; u += gridDim.x) {  // (workgroup-uniform)
+    const long long row = u / chunks;
+    const int gc = (int)(u - row * chunks);
+    const int t = (int)(row / (6 * kCellG)), fr = (int)(row - (long long)t * 6 * kCellG), f = fr / kCellG, j = fr - f * kCellG;
+    const int g = gc * 256 + tid;
+    if (tid < kCellG * 3) s_cnt[tid] = 0u;
+    __syncthreads();
+    const uint32_t rc = g < n ? rects[((size_t)t * 6 + f) * n + g] : 0x00000001u;  // (i0 1 > i1 0: empty)
+    const int i0 = (int)(rc & 0xffu), i1 = (int)((rc >> 8) & 0xffu), j0 = (int)((rc >> 16) & 0xffu), j1 = (int)(rc >> 24);
     const bool rows = !(j < j0 || j > j1 || i0 > i1) && (!FILL || cb.ok[t]);
-    const uint32_t ty = G.code >> 28;  // one list per collider type
-    uint32_t* cnt = cb.count + (size_t)t * kCells * 3 + ty;
-    uint32_t* cur = cb.cursor + (size_t)t * kCells * 3 + ty;
-    for (int i = i0; rows && i <= i1; ++i) {
-      const int c = (f * kCellG + j) * kCellG + i;
-      const CellCone cc = cb.cones[c];
-      // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
-      const bool hit = G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
-      if (!hit) continue;
-      if (!FILL) {
-        atomicAdd(cnt + 3 * c, 1u);
-      } else {
-        const uint32_t pos = atomicAdd(cur + 3 * c, 1u);
-        if (pos < cb.cap) {  // the entry and its sort key (the segmented sort orders each cell by near bound)
-          const uint32_t key = near_key(__float_as_uint(G.near));
-          if (cb.compact) reinterpret_cast<uint32_t*>(cb.ent)[pos] = (G.code & 0xffffu) | (key << 16);
-          else cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
-          cb.keys[pos] = key;
+    CellGeo G;
+    uint32_t ty = 0u;
+    if (rows) {
+      G = geo[(size_t)t * n + g];
+      ty = G.code >> 28;  // one list per collider type
+    }
+    // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
+    auto hit = [&](int i) {
+      const CellCone cc = cb.cones[(f * kCellG + j) * kCellG + i];
+      return G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
+    };
+    for (int i = i0; rows && i <= i1; ++i)
+      if (hit(i)) atomicAdd(&s_cnt[i * 3 + ty], 1u);
+    __syncthreads();
+    const size_t rbase = ((size_t)t * kCells + (size_t)(f * kCellG + j) * kCellG) * 3;  // the row's counters
+    if (!FILL) {
+      if (tid < kCellG * 3 && s_cnt[tid]) atomicAdd(cb.count + rbase + tid, s_cnt[tid]);
+    } else {
+      if (tid < kCellG * 3) {
+        s_base[tid] = s_cnt[tid] ? atomicAdd(cb.cursor + rbase + tid, s_cnt[tid]) : 0u;
+        s_cnt[tid] = 0u;
+      }
+      __syncthreads();
+      if (rows) {
+        const uint32_t key = near_key(__float_as_uint(G.near));
+        for (int i = i0; i <= i1; ++i) {
+          if (!hit(i)) continue;
+          const uint32_t pos = s_base[i * 3 + ty] + atomicAdd(&s_cnt[i * 3 + ty], 1u);
+          if (pos < cb.cap) {  // the entry and its sort key (the segmented sort orders each cell by near bound)
+            if (cb.compact) reinterpret_cast<uint32_t*>(cb.ent)[pos] = (G.code & 0xffffu) | (key << 16);
+            else cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
+            cb.keys[pos] = key;
+          } else {
+            cb.ok[t] = 0u;  // (cannot happen after the capacity check; kept as a guard)
+          }
         }
-        else cb.ok[t] = 0u;  // (cannot happen after the capacity check; kept as a guard)
       }
     }
+    __syncthreads();  // (s_cnt / s_base are reused by the next unit)
   }
 }
 
@@ -296,6 +337,11 @@ bool cells_enabled(int T, int C) {
 // grid of a grid-stride launch over `items` work-items (at most 2^16 workgroups of 256)
 static unsigned stride_grid(long long items) { return (unsigned)std::max(1ll, std::min((items + 255) / 256, 1ll << 16)); }
 
+// workgroups of a row pass: one per (target, face, row, 256 colliders), at most 2^16 (grid-stride)
+static unsigned row_grid(int T, int n) {
+  return (unsigned)std::max(1ll, std::min((long long)T * 6 * kCellG * ((n + 255) >> 8), 1ll << 16));
+}
+
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   const int T = sc.T, n = sc.ns + sc.na + sc.no;
   const int cells = T * kCells * 3;  // lists: (target, cell, collider type)
@@ -316,7 +362,7 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   CellGeo* geo = reinterpret_cast<CellGeo*>(cb.geo);
   if (pairs > 0) {
     hipLaunchKernelGGL(cells_geo_kernel, dim3(stride_grid(pairs)), dim3(256), 0, st, sc, cb, T, geo);
-    hipLaunchKernelGGL(cells_row_kernel<false>, dim3(stride_grid(pairs * 6 * kCellG)), dim3(256), 0, st, geo, pairs, cb, n);
+    hipLaunchKernelGGL(cells_row_kernel<false>, dim3(row_grid(T, n)), dim3(256), 0, st, geo, T, cb, n);
   }
   if (T > 0) hipLaunchKernelGGL(cells_total_kernel, dim3(T), dim3(256), 0, st, cb);
   hipLaunchKernelGGL(cells_fit_kernel, dim3(1), dim3(64), 0, st, cb, T);
@@ -326,7 +372,7 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   if (hipMemcpyAsync(cb.cursor, cb.start, (size_t)cells * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
     return -1;
   if (pairs > 0)
-    hipLaunchKernelGGL(cells_row_kernel<true>, dim3(stride_grid(pairs * 6 * kCellG)), dim3(256), 0, st, geo, pairs, cb, n);
+    hipLaunchKernelGGL(cells_row_kernel<true>, dim3(row_grid(T, n)), dim3(256), 0, st, geo, T, cb, n);
   // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its segment
   {
     const uint32_t span = (uint32_t)cells + 1;
@@ -352,8 +398,8 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-size_t cells_geo_bytes(int T, int C) {
-  return cells_enabled(T, C) ? (size_t)T * (size_t)(C > 0 ? C : 1) * sizeof(CellGeo) : 0;
+size_t cells_geo_bytes(int T, int C) {  // the CellGeo records, then the packed face rectangles (cell_rects)
+  return cells_enabled(T, C) ? (size_t)T * (size_t)(C > 0 ? C : 1) * (sizeof(CellGeo) + 6 * sizeof(uint32_t)) : 0;
 }
 
 }  // namespace art

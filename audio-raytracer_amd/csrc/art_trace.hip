@@ -245,6 +245,9 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #ifndef ART_STEAL_MIN_IDLE  // idle quads a wave waits for before it shares work (A/B knob)
 #define ART_STEAL_MIN_IDLE 1
 #endif
+#ifndef ART_VIS_STEAL_MIN_IDLE  // the same for the echo traversal
+#define ART_VIS_STEAL_MIN_IDLE 1
+#endif
 #ifndef ART_NENT_BALLOT     // entered-children count by ballot instead of a quad DPP maximum (A/B knob)
 #define ART_NENT_BALLOT 0
 #endif
@@ -1045,7 +1048,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     const unsigned long long act = __ballot(g >= 0) & kQuad0;
     if (!act) break;
     const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
-    if (ART_VIS_STEAL && donors && idle) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
+    if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
       int l4 = lane & ~3;
       asm volatile("" : "+v"(l4));  // (recomputed here, not hoisted out of the loop)
       const unsigned long long below = (1ull << l4) - 1ull;
