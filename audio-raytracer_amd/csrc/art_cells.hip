@@ -231,8 +231,12 @@ __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ ge
       const CellCone cc = cb.cones[(f * kCellG + j) * kCellG + i];
       return G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
     };
+    uint32_t hm = 0u;  // the row's cells this collider's cone touches (kCellG = 32 bits)
     for (int i = i0; rows && i <= i1; ++i)
-      if (hit(i)) atomicAdd(&s_cnt[i * 3 + ty], 1u);
+      if (hit(i)) {
+        hm |= 1u << i;
+        atomicAdd(&s_cnt[i * 3 + ty], 1u);
+      }
     __syncthreads();
     const size_t rbase = ((size_t)t * kCells + (size_t)(f * kCellG + j) * kCellG) * 3;  // the row's counters
     if (!FILL) {
@@ -243,10 +247,10 @@ __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ ge
         s_cnt[tid] = 0u;
       }
       __syncthreads();
-      if (rows) {
+      if (hm) {
         const uint32_t key = near_key(__float_as_uint(G.near));
-        for (int i = i0; i <= i1; ++i) {
-          if (!hit(i)) continue;
+        for (uint32_t m = hm; m; m &= m - 1u) {
+          const int i = __builtin_ctz(m);
           const uint32_t pos = s_base[i * 3 + ty] + atomicAdd(&s_cnt[i * 3 + ty], 1u);
           if (pos < cb.cap) {  // the entry and its sort key (the segmented sort orders each cell by near bound)
             if (cb.compact) reinterpret_cast<uint32_t*>(cb.ent)[pos] = (G.code & 0xffffu) | (key << 16);

@@ -242,14 +242,19 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #ifndef ART_NEAREST_STEAL
 #define ART_NEAREST_STEAL 1
 #endif
-#ifndef ART_STEAL_MIN_IDLE  // idle quads a wave waits for before it shares work (A/B knob)
-#define ART_STEAL_MIN_IDLE 1
+// Idle quads a wave waits for before it shares work (round 4: waiting for 3 in the nearest and 2 in
+// the echo traversal runs the steal sequence, 13 lane shuffles and a select, less often; config 2
+// nearest 55.4 -> 52.7 us, config 3 74.1 -> 70.5 us, config 5 91.4 -> 89.0 us per bounce).
+#ifndef ART_STEAL_MIN_IDLE
+#define ART_STEAL_MIN_IDLE 3
 #endif
-#ifndef ART_VIS_STEAL_MIN_IDLE  // the same for the echo traversal
-#define ART_VIS_STEAL_MIN_IDLE 1
+#ifndef ART_VIS_STEAL_MIN_IDLE
+#define ART_VIS_STEAL_MIN_IDLE 2
 #endif
-#ifndef ART_NENT_BALLOT     // entered-children count by ballot instead of a quad DPP maximum (A/B knob)
-#define ART_NENT_BALLOT 0
+// Entered children counted by one ballot instead of a quad DPP maximum (round 4, 1-3 % of the
+// nearest kernel)
+#ifndef ART_NENT_BALLOT
+#define ART_NENT_BALLOT 1
 #endif
 constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
 
