@@ -1038,8 +1038,22 @@ ART_API void art_destroy(art_ctx* c) {
 
 ART_API const char* art_last_error(const art_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+// Timing events a device keeps ready once ART_CTX_TIME_KERNELS is first set: the pool grows on the
+// host here, before any timed frame, so a timed frame never creates events (hipEventCreate inside a
+// caller's timed loop; 8 events per timed frame, 64 frames between art_kernel_timing calls).
+constexpr size_t kTimingEventsReserve = 512;
+
 ART_API int art_set_flags(art_ctx* c, uint32_t flags) {
   if (!c) return ART_E_INVALID;
+  if ((flags & ART_CTX_TIME_KERNELS) && !(c->flags & ART_CTX_TIME_KERNELS) && !c->devs.empty()) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    for (Device& dv : c->devs) {
+      (void)hipSetDevice(dv.id);
+      (void)pool_event(dv, kTimingEventsReserve - 1);
+    }
+    (void)hipSetDevice(prev);
+  }
   c->flags = flags;
   return ART_OK;
 }

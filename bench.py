@@ -579,7 +579,7 @@ def main():
     bf_ops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
 
     # the all-gather alone, timed with HIP events on the launch stream around the collective of
-    # every 8th timed step (BASELINE.md cfg 4: "all-gather time")
+    # every 8th of the first 512 timed steps (BASELINE.md cfg 4: "all-gather time")
     ag = {"ms": 0.0, "n": 0, "events": []}
 
     def step(timed=False):
@@ -610,6 +610,9 @@ def main():
     # Kernel durations come from HIP events on the launch stream around the stages of every 8th
     # timed step (event records between launches cost a few µs of GPU idle each; sampling keeps
     # that out of the other steps)
+    # (the first switch to ART_CTX_TIME_KERNELS creates the context's timing events on the host, here,
+    # outside the timed region; at most 64 sampled steps keep within them)
+    ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
     ctx.set_flags(0)
     ctx.kernel_timing()  # reset
     if world > 1:
@@ -617,10 +620,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        if i % 8 == 0:
+        sample = i % 8 == 0 and i < 8 * 64
+        if sample:
             ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
-        step(timed=i % 8 == 0)
-        if i % 8 == 0:
+        step(timed=sample)
+        if sample:
             ctx.set_flags(0)
     torch.cuda.synchronize()
     if world > 1:
@@ -681,7 +685,7 @@ def main():
                 b["cull_box"] * CULL_OPS["cull_box"] + b["cell_entries"] * CULL_OPS["cell_entries"]) / ex_launches
     by_kernel_ops = {k: kernel_ops(k) for k in abi.EXEC_KERNELS}
     # the dominant kernel: nearest_first_kernel, timed live by HIP events around its launches on the
-    # launch stream (art_kernel_times.nearest_ms, every 8th timed step)
+    # launch stream (art_kernel_times.nearest_ms, every 8th of the first 512 timed steps)
     near_ms = ktimes["nearest_ms"] / n_rt
     near_tflops = by_kernel_ops["nearest"] / (near_ms * 1e-3) / 1e12 if near_ms > 0 else 0.0
     # algorithmic HBM bytes of one raytrace launch: the decoded collider records, directions,
@@ -720,7 +724,7 @@ def main():
                                                               if world > 1 else "")},
         "allgather_ms": allgather_ms,
         "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
-        "allgather_note": "HIP events on the launch stream around the all-gather of every 8th timed step, max over "
+        "allgather_note": "HIP events on the launch stream around the all-gather of every 8th of the first 512 timed steps, max over "
                           "ranks; the step time includes it" if world > 1 else None,
         "roofline": {"bound": "valu", "kernel": f"nearest_first_kernel<false, {'true' if scene.obbs.size > 0 else 'false'}, "
                                                     f"{'true' if cfg.H > 1 else 'false'}>",
@@ -731,7 +735,7 @@ def main():
                      "note": "the dominant kernel (nearest-hit BVH traversal; FP32 VALU roof, no MFMA-shaped work). "
                              "achieved = ops it executed per frame (exact lane-tests x SURVEY.md 8(d) ops per test + "
                              "BVH box tests x 14, art_exec_counts.by_kernel[0]) / its duration per frame (HIP events "
-                             "around its launches on the launch stream, every 8th timed step); traffic = its HBM bytes "
+                             "around its launches on the launch stream, every 8th of the first 512 timed steps); traffic = its HBM bytes "
                              "per frame from same-build FETCH_SIZE / WRITE_SIZE passes (" + traffic_note + ")",
                      "single_issue": {"achieved": near_tflops, "peak": SINGLE_ISSUE_TLOPS, "unit": "T lane-op/s",
                                       "frac": near_tflops / SINGLE_ISSUE_TLOPS,
