@@ -305,3 +305,56 @@ def test_permeation_first_hit_far_from_batch_end():
         with art.Context(1) as c:
             out, _ = gpu_vs_oracle(c, scene, params, org, hits=True, counts=False, stale=4)
         assert (out.perm != 0).any()
+
+
+def _obb_world_points(ob, rng, m):
+    """m world points on the surfaces of random OBBs of `ob` (corners, edge points, face points), as
+    the tests map them: local = R (P - c) by the stored rotation R (halfQuaternion decode), so
+    P = c + R^T local."""
+    h2f = lambda a: np.asarray(a, np.uint16).view(np.float16).astype(np.float64)
+    out = []
+    for _ in range(m):
+        k = rng.integers(len(ob))
+        c = h2f(ob["center"][k]); h = np.abs(h2f(ob["size"][k]))
+        x, y, z = h2f(ob["rot"][k])
+        w2 = 1.0 - (x * x + y * y + z * z)
+        q = np.array([x, y, z, np.sqrt(w2) if w2 > 0 else 0.0])
+        q /= np.linalg.norm(q)
+        x, y, z, w = q
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                      [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+        kind = rng.integers(3)  # corner, edge point, face point
+        s = rng.choice([-1.0, 1.0], 3)
+        loc = s * h
+        if kind >= 1:
+            loc[0] = rng.uniform(-1, 1) * h[0]
+        if kind == 2:
+            loc[1] = rng.uniform(-1, 1) * h[1]
+        out.append(c + R.T @ loc)
+    return np.array(out)
+
+
+def test_obb_rotated_bounds_grazing(ctx):
+    """Rays aimed at the corners, edges and faces of rotated OBBs (round 4's OBB bounds are the
+    world box of the rotated box, tight exactly there), flat and long boxes included, through the
+    raytrace, echo, muffle and permeation casts (the permeation first hit rotates by the inverse)."""
+    rng = np.random.default_rng(41)
+    n = 400
+    c = rng.uniform(-25, 25, (n, 3)).astype(np.float32)
+    halves = rng.uniform(0.1, 3.0, (n, 3)).astype(np.float32)
+    halves[::5, 0] *= 12.0   # long boxes
+    halves[1::5, 1] = 0.02   # flat boxes
+    ob = obbs(c, halves, rng)
+    ob["rot"][::7] = f16bits(np.array([0.0, 0.0, 0.0]))          # identity
+    ob["rot"][3::7] = f16bits(np.array([0.7071, 0.0, 0.0]))       # 90 degrees about x
+    O = np.array([0.5, -0.25, 0.125], np.float32)
+    P = _obb_world_points(ob, rng, 256)
+    d = P - O.astype(np.float64)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    dirs = f16bits(d).reshape(-1, 3)
+    org = np.concatenate([O[None], rng.uniform(-20, 20, (3, 3))]).astype(np.float32)
+    targets = rng.uniform(-25, 25, (4, 3)).astype(np.float32)
+    scene = art.Scene(dirs=dirs, targets=targets, obbs=ob,
+                      spheres=spheres(c[:40] + 1.5, np.full(40, 0.4, np.float32), rng))
+    run(ctx, scene, org, H=3)
