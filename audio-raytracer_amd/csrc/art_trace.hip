@@ -1798,16 +1798,6 @@ static bool echo_decide() {
   return on;
 }
 
-// Folded multi-hit frames: each bounce's muffle rays on the side stream behind its echo rays
-// (ART_MUFFLE_PER_BOUNCE=1) instead of one muffle launch after the last bounce (A/B knob).
-static bool muffle_per_bounce() {
-  static const bool on = [] {
-    const char* e = getenv("ART_MUFFLE_PER_BOUNCE");
-    return e && *e ? atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
 // Fans per launch_raytrace_fast call: echo pairs and hit records (R*H per fan each) stay below
 // 2^31 (u32 indices), the muffle accumulator index (fan * TC + slot) * T + t fits 32 bits, and a
 // fan's echo halves stay addressable with a 32-bit half offset into the block
@@ -1950,24 +1940,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
       (void)hipEventRecord(echo.fork, st);
       (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
       ART_VIS_ANY(echo.st, groups, k, false);
-      if (fold && muffle_per_bounce()) {  // and its muffle rays, behind them on the side stream
-        VisPairs vk = pb.vp;
-        vk.hrec += (size_t)k * vk.fixed;
-        FrameParams fk = fp;
-        fk.H = 1;  // (muffle_body walks vk.fixed * H records)
-        const unsigned mb = (unsigned)((vk.fixed + 255) / 256);
-#define ART_MUFFLE_K(EX_, OBB_)                                                                                       \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, false>), dim3(mb, mt), dim3(256), 0, echo.st, sc, fk, vk, pair_count,   \
-                     muffle_acc, eh)
-        if (fp.exec) { if (obb) ART_MUFFLE_K(true, true); else ART_MUFFLE_K(true, false); }
-        else { if (obb) ART_MUFFLE_K(false, true); else ART_MUFFLE_K(false, false); }
-#undef ART_MUFFLE_K
-      }
     }
   }
-  if (per_bounce && fold && muffle_per_bounce()) {
-    // every bounce's muffle rays are on the side stream already
-  } else if (per_bounce) {
+  if (per_bounce) {
     ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
   } else if (fused) {
 #define ART_ECHO_MUFFLE(EX_, OBB_)                                                                                    \
