@@ -266,8 +266,8 @@ constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every
 #ifndef ART_NEAREST_OBB_WAVES
 #define ART_NEAREST_OBB_WAVES 8
 #endif
-template <bool EX, bool OBB, bool ED = false>  // (ED with OBBs: 7, where its epilogue needs no spills)
-constexpr int kNearestWaves = EX ? 6 : (OBB ? (ED ? 7 : ART_NEAREST_OBB_WAVES) : 8);
+template <bool EX, bool OBB>
+constexpr int kNearestWaves = EX ? 6 : (OBB ? ART_NEAREST_OBB_WAVES : 8);
 template <bool EX, bool OBB>
 constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
 // echo_muffle_kernel<false, true>: 8 waves per SIMD (64 VGPRs) without spills
@@ -285,17 +285,6 @@ __device__ __forceinline__ int select_bit(unsigned long long m, int k) {
   return pos;
 }
 
-// Echo verdicts from the nearest traversal (ED; one-hit frames with one batch slot and no hit
-// outputs): per wave, 16 rays' tested-leaf lists and counts in LDS, and the
-// hit distance up to which the traversal's margins cover the echo's.
-constexpr int kEdLeaves = 16;
-struct EdLds {
-  uint32_t* list = nullptr;  // [16][kEdLeaves] leaf node ids
-  uint32_t* cnt = nullptr;   // [16]
-  float lcap = 0.0f;
-};
-constexpr int kEdDecided = (int)0x80000000;  // hit record code bit: the echo is already stored
-
 // (distance, order) as one ordered 64-bit key; distances are >= 0 or -0, the two zeros equal
 __device__ __forceinline__ unsigned long long nearest_key(float d, int code) {
   return ((unsigned long long)(d == 0.0f ? 0u : __float_as_uint(d)) << 32) | (uint32_t)code;
@@ -311,31 +300,19 @@ __device__ __forceinline__ unsigned long long nearest_key(float d, int code) {
 // re-evaluates a zero distance).
 // PERM: the permeation job's first-hit cast (ShootRayCast :101-141: INFINITY sentinel, inverse OBB
 // rotation); otherwise the raytracer's (:225-280: float.MaxValue sentinel).
-// ED (echo verdicts from the traversal, one-hit frames: EchoDecide below): the node margins also
-// cover every collider that can block the ray's echo, and the quads record every leaf they test for
-// the ray in ed.list (the first kEdLeaves; ed.cnt counts them all).
-template <bool EX, bool OBB, bool PERM = false, bool ED = false>
+template <bool EX, bool OBB, bool PERM = false>
 __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint32_t* my,
                                                   int* s_bound, unsigned long long* s_key, float& best, int& code,
-                                                  unsigned long long* ex, EdLds ed = EdLds{}) {
+                                                  unsigned long long* ex) {
   const int qd = lane & 3, wq = lane >> 2;
   uint32_t* const s_wave = my - wq * kBvhStack;
   best = FLT_MAX;
   code = kNoHit;
-  if (ED && qd == 0) ed.cnt[wq] = 0u;
   if (sc.bvh_levels == 0) return;  // no colliders: every ray misses
   if (ART_NEAREST_STEAL && qd == 0) s_key[wq] = ~0ull;  // the ray's shared result key, opened before the loop
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
   bool force = force_all(s, om);
-  // ED margins: factor * (scale + om_ed), om_ed = 1.05 |o|_1 + 10 |d|_1 + 2.11 min(lim, lcap) |d|_1
-  float ed_om = 0.0f, ed_dn = 0.0f;
-  auto ed_ray = [&]() {
-    const float dn = fabsf(s.d.x) + fabsf(s.d.y) + fabsf(s.d.z);
-    ed_om = 1.05f * om + 10.0f * dn;
-    ed_dn = 2.11f * dn;
-  };
-  if (ED) ed_ray();
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
@@ -361,7 +338,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     ART_DIAG_STEP(nsteps);
     const CullRec r = load_node(br, c0 + qd);
     float tn;
-    const bool h = node_entry(s, r, ED ? __builtin_fmaf(fminf(lim, ed.lcap), ed_dn, ed_om) : om, tn);
+    const bool h = node_entry(s, r, om, tn);
     const float en = fmaxf(tn, 0.0f);
     const bool enter = force | (h & (en <= lim));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
     quad_descend(enter, en, force, qd, c0, my, g, sp);
@@ -369,10 +346,6 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   };
   auto leaf_step = [&](int leaf) {
     ART_DIAG_STEP(nsteps);
-    if (ED && qd == 0) {  // the ray's tested leaves, appended by whichever quad tests them
-      const uint32_t k = atomicAdd(ed.cnt + home, 1u);
-      if (k < (uint32_t)kEdLeaves) ed.list[home * kEdLeaves + k] = (uint32_t)leaf;
-    }
     int cc, tid;
     float dd;
     const bool h = leaf_slot_test<OBB, PERM>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, dd, tid, nt, sc.obbc);
@@ -435,7 +408,6 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
           force = dforce != 0;
           lim = dlim;
           mykey = ~0ull;  // (the finished ray's result went to its key above)
-          if (ED) ed_ray();
         }
         if (robbed && ++bp == sp) sp = bp = 0;
       }
@@ -603,85 +575,14 @@ __device__ __forceinline__ void fold_path(const DevScene& sc, const FrameParams&
 }
 
 // EX: count the executed tests (fp.exec); OBB: the scene has OBBs; FOLD: fold_path above.
-// ED epilogue (one-hit frames, bounce 0): the quad's own ray rr of 64-ray group g hit `code` at
-// `best`. Its echo segment is rebuilt exactly as hit_from_pre / echo_seg_from_hit build it, and when
-// the ray qualifies — a hit at most ed.lcap away, no degenerate direction or origin, at most
-// kEdLeaves tested leaves — every collider of the recorded leaves gets the reference's echo test
-// (CanRaySeePoint :365-397); the verdict is stored at once and the code marked kEdDecided, so the
-// echo traversal skips the ray. Exactness: DESIGN.md §5 item 13.
-template <bool EX, bool OBB>
-__device__ __forceinline__ bool ed_epilogue(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
-                                            uint8_t* block, int fan, int ray, bool alive, float best, int code, EdLds ed,
-                                            int wq, int qd, unsigned long long* ex) {
-  const bool hit = alive && code != kNoHit;
-  bool decided = false, blocked = false;
-  uint32_t out_at = 0u;
-  uint16_t out_val = 0;
-  Seg es;
-  float maxd = 0.0f;
-  const uint32_t nl = ed.cnt[wq];
-  if (hit) {
-    const vec3 O = load3(origins, fan);
-    const vec3 d = load_dir(sc.dirs, ray);
-    const Seg s0 = make_seg(O, d);
-    int type, idx;
-    float dist = best;
-    winner_of(sc, s0, code, type, idx, dist);  // (the zero-distance re-evaluation, as hit_from_pre)
-    const vec3 o = O + d * dist;               // :111
-    const vec3 off = o - d * kEps;             // :124
-    const float dist0 = distance(O, o);        // :130
-    es = make_seg(off, normalize(O - off));
-    maxd = dist0;
-    out_at = (uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)ray;  // ray * H + 0
-    out_val = (uint16_t)f32tof16(dist0 * echo_of(sc, type, idx));  // :142-144
-    const float om = fabsf(O.x) + fabsf(O.y) + fabsf(O.z);
-    decided = nl <= (uint32_t)kEdLeaves && best <= ed.lcap && !force_all(s0, om);
-  }
-  const BvhRes br = bvh_res(sc);
-  const int leaf0 = sc.bvh_leaf0;
-  unsigned nt[3] = {0u, 0u, 0u};
-  const int lane = threadIdx.x & 63;
-  for (uint32_t j = 0;; ++j) {  // (quad-uniform state; the wave leaves once no quad has a leaf left)
-    const bool more = decided && !blocked && j < nl;
-    if (!__any(more)) break;
-    if (more) {
-      const int leaf = (int)ed.list[wq * kEdLeaves + j];
-      int cc, tid;
-      float dd;
-      const bool h = leaf_slot_test<OBB>(es, br, (leaf - leaf0) * kBvhLeaf + qd, cc, dd, tid, nt);
-      blocked = ((uint32_t)(__ballot(h && dd < maxd) >> (lane & ~3)) & 0xFu) != 0u;  // any collider, no owner (:373-394)
-    }
-  }
-  if (decided && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = blocked ? (uint16_t)0 : out_val;  // :76, :142-144
-  if (ex) {
-    exec_add(ex + kExecEcho, kExecSphere, wave_sum_u32(nt[0]));
-    exec_add(ex + kExecEcho, kExecAabb, wave_sum_u32(nt[1]));
-    exec_add(ex + kExecEcho, kExecObb, wave_sum_u32(nt[2]));
-  }
-  return decided;
-}
-
-// The node margins' hit-distance cap of the ED traversal: kEdCapFrac of the scene box's diagonal.
-#ifndef ART_ED_CAP_FRAC
-#define ART_ED_CAP_FRAC 0.2f
-#endif
-__device__ __forceinline__ float ed_lcap(const DevScene& sc) {
-  if (sc.bvh_levels == 0) return 0.0f;
-  const CullRec r = sc.bvh[0];
-  const float dx = r.hix - r.lox, dy = r.hiy - r.loy, dz = r.hiz - r.loz;
-  const float v = ART_ED_CAP_FRAC * sqrtf(dx * dx + dy * dy + dz * dz);
-  return isfinite(v) ? v : 0.0f;
-}
-
-template <bool EX, bool OBB, bool FOLD, bool ED = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWaves<EX, OBB, ED>))) void nearest_first_kernel(
+template <bool EX, bool OBB, bool FOLD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWaves<EX, OBB>))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
     uint32_t* __restrict__ counters, FanLayout L, uint8_t* __restrict__ block, VisPairs vp) {
   __shared__ uint32_t s_stk[kBvhStack * 64];
   __shared__ int s_bound[64];
   __shared__ unsigned long long s_key[64];
-  __shared__ uint32_t s_ed_list[ED ? 64 * kEdLeaves : 1], s_ed_cnt[ED ? 64 : 1];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
   const int ngroups = fp.S * nrb;
@@ -755,22 +656,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
 #ifdef ART_DIAG
   const unsigned long long t0 = clock64();
 #endif
-  EdLds ed;
-  if (ED) {
-    ed.list = s_ed_list + 16 * w * kEdLeaves;
-    ed.cnt = s_ed_cnt + 16 * w;
-    ed.lcap = ed_lcap(sc);
-  }
-  quad_nearest_core<EX, OBB, false, ED>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code,
-                                        ex, ed);
-  if (ED) {
-    const int fan = g / nrb;
-    const int slot = (g - fan * nrb) * 64 + rr;
-    const int ray = slot < fp.R ? ray_order[slot] : 0;
-    const bool dec = ed_epilogue<EX, OBB>(sc, fp, L, origins, block, fan, ray, alive, best, code, ed, lane >> 2, lane & 3, ex);
-    if (EX) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__ballot(dec) & kQuad0));  // (the rest: the echo traversal)
-    if (dec) code |= kEdDecided;
-  }
+  quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code, ex);
   if (FOLD) {
     // The ray's state is fetched again rather than kept live across the traversal (a memory
     // clobber: the compiler may not reuse the values loaded before it): 64 VGPRs, no spills.
@@ -1054,10 +940,8 @@ struct EchoFromHits {
 // The hit of ray slot r of 64-ray group g from its nearest-hit record, as path_kernel computes it
 // (:111, :124, the zero-distance re-evaluation included): false for a slot past the fan's rays
 // (slot_ok false) or a miss.
-// (ed_done: the nearest kernel stored this hit's echo already, kEdDecided)
 __device__ __forceinline__ bool hit_from_pre(const DevScene& sc, const EchoFromHits& eh, uint32_t g, int r, bool& slot_ok,
-                                             int& fan, int& ray, vec3& O, vec3& o, vec3& off, int& type, int& idx,
-                                             bool* ed_done = nullptr) {
+                                             int& fan, int& ray, vec3& O, vec3& o, vec3& off, int& type, int& idx) {
   const FrameParams& fp = eh.fp;
   const int nrb = (fp.R + 63) >> 6;
   fan = (int)(g / (uint32_t)nrb);
@@ -1066,14 +950,12 @@ __device__ __forceinline__ bool hit_from_pre(const DevScene& sc, const EchoFromH
   if (!slot_ok) return false;
   ray = eh.ray_order[slot];
   const int2 ph = eh.pre[(size_t)g * 64 + r];
-  const int code = ph.y & ~kEdDecided;
-  if (ed_done) *ed_done = ph.y < 0;
-  if (code == kNoHit) return false;  // a miss: no echo ray, no muffle rays
+  if (ph.y == kNoHit) return false;  // a miss: no echo ray, no muffle rays
   O = load3(eh.origins, fan);
   const vec3 d = load_dir(sc.dirs, ray);
   const Seg s0 = make_seg(O, d);
-  const int rank = code >> 28;
-  idx = code & 0x0fffffff;
+  const int rank = ph.y >> 28;
+  idx = ph.y & 0x0fffffff;
   type = rank == 0 ? kSphere : (rank == 1 ? kAabb : kObb);
   float dist = __int_as_float(ph.x);
   if (dist == 0.0f) {  // as path_kernel
@@ -1085,15 +967,13 @@ __device__ __forceinline__ bool hit_from_pre(const DevScene& sc, const EchoFromH
   off = o - d * kEps;    // :124, :158
   return true;
 }
-// (ed_done: the nearest kernel stored this echo already: no segment, and nothing to write)
 __device__ __forceinline__ bool echo_seg_from_hit(const DevScene& sc, const EchoFromHits& eh, uint32_t g, int r, Seg& s,
-                                                  float& maxd, uint32_t& out_at, uint16_t& out_val, bool& slot_ok,
-                                                  bool& ed_done) {
+                                                  float& maxd, uint32_t& out_at, uint16_t& out_val, bool& slot_ok) {
   int fan = 0, ray = 0, type = kNone, idx = 0;
   vec3 O, o, off;
-  const bool hit = hit_from_pre(sc, eh, g, r, slot_ok, fan, ray, O, o, off, type, idx, &ed_done);
+  const bool hit = hit_from_pre(sc, eh, g, r, slot_ok, fan, ray, O, o, off, type, idx);
   out_at = slot_ok ? (uint32_t)(((size_t)fan * eh.L.stride + eh.L.echo_off) / 2) + (uint32_t)ray : 0u;  // ray * H + 0
-  if (!hit || ed_done) return false;
+  if (!hit) return false;
   const float dist0 = distance(O, o);            // :130
   s = make_seg(off, normalize(O - off));
   maxd = dist0;
@@ -1117,10 +997,10 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
   s.a2 = 0.0f;
   if (HM) {
-    bool slot_ok, ed_done = false;
-    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val, slot_ok, ed_done);
+    bool slot_ok;
+    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val, slot_ok);
     if (eh.no_path) {  // the path kernel's duties for this frame: a miss keeps the reset 0 (:76, :200-207)
-      if (slot_ok && !valid && !ed_done && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = 0;
+      if (slot_ok && !valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = 0;
       if (ex) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__ballot(valid) & 0x1111111111111111ull));
     }
     if (!__any(valid)) return;
@@ -1785,19 +1665,6 @@ static PairBufs pair_bufs(void* base, const FrameParams& fp) {
 
 size_t fast_pair_bytes(const FrameParams& fp) { return pair_bufs(nullptr, fp).total; }
 
-// One-hit frames of the joint echo+muffle plan: echo verdicts from the nearest traversal's tested
-// leaves (nearest_first_kernel<..., ED>; ART_ECHO_DECIDE=0 restores the full echo traversal).
-#ifndef ART_ECHO_DECIDE_DEFAULT
-#define ART_ECHO_DECIDE_DEFAULT 0
-#endif
-static bool echo_decide() {
-  static const bool on = [] {
-    const char* e = getenv("ART_ECHO_DECIDE");
-    return e && *e ? atoi(e) != 0 : ART_ECHO_DECIDE_DEFAULT != 0;
-  }();
-  return on;
-}
-
 // Fans per launch_raytrace_fast call: echo pairs and hit records (R*H per fan each) stay below
 // 2^31 (u32 indices), the muffle accumulator index (fan * TC + slot) * T + t fits 32 bits, and a
 // fan's echo halves stay addressable with a 32-bit half offset into the block
@@ -1891,10 +1758,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // fork costs ~10 us before the side stream starts). Without a side stream everything runs on st.
   const bool per_bounce = split && multi && ecnt;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
-#define ART_NEAREST_ED(EX_, OBB_, F_, ED_)                                                                           \
-  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_, ED_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, \
+#define ART_NEAREST(EX_, OBB_, F_)                                                                                  \
+  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order,      \
                      pb.pre, pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr, L, block, pb.vp)
-#define ART_NEAREST(EX_, OBB_, F_) ART_NEAREST_ED(EX_, OBB_, F_, false)
     const bool mark = marks && marks->used < marks->cap;
     if (mark) (void)hipEventRecord(marks->ev[2 * marks->used], st);
 #ifdef ART_FUSE_ECHO
@@ -1913,16 +1779,12 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (fold) {
       if (fp.exec) { if (obb) ART_NEAREST(true, true, true); else ART_NEAREST(true, false, true); }
       else { if (obb) ART_NEAREST(false, true, true); else ART_NEAREST(false, false, true); }
-    } else if (fused && echo_decide()) {  // echo verdicts from the traversal (one-hit frames)
-      if (fp.exec) { if (obb) ART_NEAREST_ED(true, true, false, true); else ART_NEAREST_ED(true, false, false, true); }
-      else { if (obb) ART_NEAREST_ED(false, true, false, true); else ART_NEAREST_ED(false, false, false, true); }
     } else {
       if (fp.exec) { if (obb) ART_NEAREST(true, true, false); else ART_NEAREST(true, false, false); }
       else { if (obb) ART_NEAREST(false, true, false); else ART_NEAREST(false, false, false); }
     }
     if (mark) (void)hipEventRecord(marks->ev[2 * marks->used++ + 1], st);
 #undef ART_NEAREST
-#undef ART_NEAREST_ED
     hipStream_t pst = st;
     if (hm && !hm2) {  // (HM2 forks the muffle rays below)
       (void)hipEventRecord(echo.fork, st);
