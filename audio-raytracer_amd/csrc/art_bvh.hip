@@ -386,11 +386,13 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       for (int e = tid; e < 2 * 3 * kKdSahSegs * 6; e += 1024)
         (&s_box[0][0][0][0])[e] = (e % 6) < 3 ? kd_ord(INFINITY) : kd_ord(-INFINITY);
       __syncthreads();
-      // a wave whose positions all lie in one half-segment (the upper levels) reduces its bounds
-      // across lanes first: one set of LDS atomics per wave instead of per thread
-      const int w0 = min(n, (tid & ~63) * chunk), w1 = min(n, w0 + 64 * chunk);
-      const bool wave_one = w1 > w0 && (((w0 >> lg) << 1) | ((w0 & (seg - 1)) >= half ? 1 : 0)) ==
-                                           ((((w1 - 1) >> lg) << 1) | (((w1 - 1) & (seg - 1)) >= half ? 1 : 0));
+      // lanes whose positions lie in one half-segment reduce their bounds across the group first
+      // (xor shuffles), so one lane per group does the LDS atomics: whole waves on the upper levels,
+      // aligned groups of half / chunk lanes below (round 4: the per-lane atomics on a few LDS words
+      // serialized the lower surface-area levels); chunks that are not a power of two keep per-lane
+      // atomics
+      const int per = (chunk & (chunk - 1)) == 0 ? half / chunk : 0;
+      const int gsz = per >= 64 ? 64 : (per >= 2 ? per : 1);  // lanes per half-segment group
       for (int x = 0; x < 3; ++x) {
         float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
         int key = -1;  // (segment << 1 | half) of the run accumulated in b
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
         };
         for (int i = i0; i < i1; ++i) {
           const int kk = ((i >> lg) << 1) | ((i & (seg - 1)) >= half ? 1 : 0);
-          if (kk != key && !wave_one) { flush(); }
+          if (kk != key && gsz == 1) { flush(); }
           key = kk;
           const int v = s_p[x][i];
           if (LB) {
@@ -413,14 +415,15 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
             b[3] = fmaxf(b[3], c.hix); b[4] = fmaxf(b[4], c.hiy); b[5] = fmaxf(b[5], c.hiz);
           }
         }
-        if (wave_one) {  // (wave-uniform) min / max over the wave, then lane 0 publishes
+        if (gsz > 1) {  // (block-uniform) min / max over each group, then its first lane publishes
           for (int q = 0; q < 6; ++q)
-            for (int off = 32; off > 0; off >>= 1) {
+            for (int off = gsz >> 1; off > 0; off >>= 1) {
               const float o = __shfl_xor(b[q], off, 64);
               b[q] = q < 3 ? fminf(b[q], o) : fmaxf(b[q], o);
             }
-          key = __shfl(key, 0, 64);  // (lane 0's chunk is not empty: w1 > w0)
-          if ((tid & 63) == 0) flush();
+          // the group's key is its first lane's (-1 when that chunk is empty: then every later one is)
+          key = __shfl(key, (tid & 63) & ~(gsz - 1), 64);
+          if ((tid & (gsz - 1)) == 0) flush();
         } else {
           flush();
         }
