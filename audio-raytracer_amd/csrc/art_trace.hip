@@ -251,6 +251,9 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #ifndef ART_VIS_STEAL_MIN_IDLE
 #define ART_VIS_STEAL_MIN_IDLE 2
 #endif
+#ifndef ART_VIS_PRIO
+#define ART_VIS_PRIO 0
+#endif
 // Entered children counted by one ballot instead of a quad DPP maximum (round 4, 1-3 % of the
 // nearest kernel)
 #ifndef ART_NENT_BALLOT
@@ -1052,6 +1055,13 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   for (;;) {
     const unsigned long long act = __ballot(g >= 0) & kQuad0;
     if (!act) break;
+    if (ART_VIS_PRIO) {  // wave priority by unfinished segments, as in the nearest traversal (A/B knob)
+      const int na = __popcll(act);
+      if (na > 12) __builtin_amdgcn_s_setprio(3);
+      else if (na > 8) __builtin_amdgcn_s_setprio(2);
+      else if (na > 4) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
     if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
       int l4 = lane & ~3;
