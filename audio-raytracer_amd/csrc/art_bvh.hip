@@ -306,7 +306,8 @@ __global__ void kd_key_kernel(const float4* __restrict__ cen, int n, int axis, u
 
 __device__ __forceinline__ float kd_comp(const float4& c, int a) { return a == 0 ? c.x : (a == 1 ? c.y : c.z); }
 
-// Block-wide exclusive scan of three counters per thread (1024 threads, 16 waves).
+// Block-wide exclusive scan of three counters per thread (NT threads, NT / 64 waves).
+template <int NT>
 __device__ __forceinline__ void kd_block_scan3(int v[3], int (*s_wave)[16]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int inc[3];
@@ -322,7 +323,7 @@ __device__ __forceinline__ void kd_block_scan3(int v[3], int (*s_wave)[16]) {
   __syncthreads();
   if (threadIdx.x < 3) {
     int run = 0;
-    for (int k = 0; k < 16; ++k) { const int t = s_wave[threadIdx.x][k]; s_wave[threadIdx.x][k] = run; run += t; }
+    for (int k = 0; k < NT / 64; ++k) { const int t = s_wave[threadIdx.x][k]; s_wave[threadIdx.x][k] = run; run += t; }
   }
   __syncthreads();
   for (int x = 0; x < 3; ++x) v[x] = s_wave[x][w] + inc[x] - v[x];
@@ -347,27 +348,35 @@ __device__ __forceinline__ float kd_area(float ex, float ey, float ez) {
 }
 
 // CAP: the largest scene of the instantiation. Up to kKdLdsBounds colliders the bounds live in LDS
-// too (6 floats each), so the surface-area pass and the axis choice read no global memory (round 4:
-// their dependent global gathers were most of the kernel's 144 us at 4096 colliders).
+// too (6 floats each), so the surface-area pass and the axis choice read no global memory.
+// One workgroup of NT threads splits the window of 2^lg_top positions starting at blockIdx.x << lg_top
+// through the binary levels lg_top .. lg_stop + 1 (round 4: the whole order in one 1024-thread
+// workgroup spent ~13 us per level on its barriers and block scans; the levels below 512 positions
+// now run as one 256-thread workgroup per 512-position window, side by side). `last`: the window's
+// first array is the leaf order (perm), otherwise the three arrays go back to k.p for the next pass.
 constexpr int kKdLdsBounds = 4096;
-template <int CAP>
-__global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap, int* __restrict__ perm) {
-  constexpr bool LB = CAP <= kKdLdsBounds;
-  __shared__ uint16_t s_p[3][CAP];        // the three index arrays
-  __shared__ uint8_t s_side[CAP];         // 1: left half of its segment (by collider id)
-  __shared__ int8_t s_axis[CAP / 8];      // per segment: split axis, -1 = fits its left half
-  __shared__ uint16_t s_segpre[3][CAP / 8];  // left-flag prefix at each segment's start
+constexpr int kKdWindowLg = 9;  // windows of the second pass: 512 positions
+template <int CAP, int NT, int MAXCHUNK, bool LB>
+__global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_top, int lg_stop, int last,
+                                                      int* __restrict__ perm) {
+  __shared__ uint16_t s_p[3][NT * MAXCHUNK];  // the window's three index arrays (relative positions)
+  __shared__ uint8_t s_side[CAP];             // 1: left half of its segment (by collider id)
+  __shared__ int8_t s_axis[NT * MAXCHUNK / 8];   // per segment of the window: split axis, -1 = fits its left half
+  __shared__ uint16_t s_segpre[3][NT * MAXCHUNK / 8];  // left-flag prefix at each segment's start
   __shared__ int s_wave[3][16];
   __shared__ int s_box[2][3][kKdSahSegs][6];  // [half][axis][segment]: lo.xyz, hi.xyz (kd_ord)
   __shared__ float s_bb[LB ? 6 : 1][LB ? CAP : 1];  // LB: lo.xyz, hi.xyz by collider id
   const int tid = threadIdx.x;
-  constexpr int kChunk = CAP / 1024;  // positions per thread
-  const int chunk = (n + 1023) / 1024;
-  const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
+  constexpr int kChunk = MAXCHUNK;  // positions per thread, at most
+  const int base = (int)blockIdx.x << lg_top;  // (the window's segments are aligned: base is a multiple of 2^lg)
+  const int nw = min(1 << lg_top, n - base);
+  if (nw <= 0) return;
+  const int chunk = (nw + NT - 1) / NT;
+  const int i0 = base + min(nw, tid * chunk), i1 = base + min(nw, tid * chunk + chunk);
   for (int x = 0; x < 3; ++x)
-    for (int i = tid; i < n; i += 1024) s_p[x][i] = (uint16_t)k.p[(size_t)x * n + i];
+    for (int r = tid; r < nw; r += NT) s_p[x][r] = (uint16_t)k.p[(size_t)x * n + base + r];
   if (LB)
-    for (int i = tid; i < n; i += 1024) {
+    for (int i = tid; i < n; i += NT) {
       const CullRec c = k.cull[i];
       s_bb[0][i] = c.lox; s_bb[1][i] = c.loy; s_bb[2][i] = c.loz;
       s_bb[3][i] = c.hix; s_bb[4][i] = c.hiy; s_bb[5][i] = c.hiz;
@@ -379,11 +388,11 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
     return isfinite(c) ? c : FLT_MAX;
   };
   __syncthreads();
-  for (int lg = 31 - __builtin_clz(cap); lg > 2; --lg) {  // segments of seg = 2^lg positions (cap: a power of 4)
-    const int seg = 1 << lg, half = seg >> 1, nseg = (n + seg - 1) >> lg;
-    const bool sah = nseg <= kKdSahSegs;
+  for (int lg = lg_top; lg > lg_stop; --lg) {  // segments of seg = 2^lg positions
+    const int seg = 1 << lg, half = seg >> 1, nseg = (nw + seg - 1) >> lg;  // (this window's segments)
+    const bool sah = ((n + seg - 1) >> lg) <= kKdSahSegs;  // (the policy counts the whole order's segments)
     if (sah) {  // bounds of both halves of every segment for a split on each axis
-      for (int e = tid; e < 2 * 3 * kKdSahSegs * 6; e += 1024)
+      for (int e = tid; e < 2 * 3 * kKdSahSegs * 6; e += NT)
         (&s_box[0][0][0][0])[e] = (e % 6) < 3 ? kd_ord(INFINITY) : kd_ord(-INFINITY);
       __syncthreads();
       // lanes whose positions lie in one half-segment reduce their bounds across the group first
@@ -403,10 +412,10 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
           for (int q = 0; q < 3; ++q) { b[q] = INFINITY; b[3 + q] = -INFINITY; }
         };
         for (int i = i0; i < i1; ++i) {
-          const int kk = ((i >> lg) << 1) | ((i & (seg - 1)) >= half ? 1 : 0);
+          const int kk = (((i - base) >> lg) << 1) | ((i & (seg - 1)) >= half ? 1 : 0);
           if (kk != key && gsz == 1) { flush(); }
           key = kk;
-          const int v = s_p[x][i];
+          const int v = s_p[x][i - base];
           if (LB) {
             for (int q = 0; q < 3; ++q) { b[q] = fminf(b[q], s_bb[q][v]); b[3 + q] = fmaxf(b[3 + q], s_bb[3 + q][v]); }
           } else {
@@ -430,8 +439,8 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       }
       __syncthreads();
     }
-    for (int s = tid; s < nseg; s += 1024) {  // each segment's axis: the cheapest split (SAH) or the widest spread of centres
-      const int a0 = s << lg, cnt = min(seg, n - a0);
+    for (int s = tid; s < nseg; s += NT) {  // each segment's axis: the cheapest split (SAH) or the widest spread of centres
+      const int a0 = s << lg, cnt = min(seg, nw - a0);  // (window-relative)
       int ax = -1;
       if (cnt > half && sah) {
         float best = INFINITY;
@@ -455,9 +464,9 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       s_axis[s] = (int8_t)ax;
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 1024) {  // side of each collider: its rank on its segment's axis
-      const int ax = s_axis[i >> lg];
-      if (ax >= 0) s_side[s_p[ax][i]] = (i & (seg - 1)) < half ? 1 : 0;
+    for (int r = tid; r < nw; r += NT) {  // side of each collider: its rank on its segment's axis
+      const int ax = s_axis[r >> lg];
+      if (ax >= 0) s_side[s_p[ax][r]] = (r & (seg - 1)) < half ? 1 : 0;
     }
     __syncthreads();
     uint32_t pk[3][kChunk / 2];  // the chunk's ids, two u16 per register
@@ -469,9 +478,9 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
     for (int j = 0; j < kChunk; ++j) {
       const int i = i0 + j;
       if (i < i1) {
-        const int ax = s_axis[i >> lg];
+        const int ax = s_axis[(i - base) >> lg];
         for (int x = 0; x < 3; ++x) {
-          const uint32_t v = s_p[x][i];
+          const uint32_t v = s_p[x][i - base];
           pk[x][j >> 1] |= v << (16 * (j & 1));
           const uint32_t f = ax < 0 ? 1u : s_side[v];
           fl[x] |= f << j;
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
         }
       }
     }
-    kd_block_scan3(c, s_wave);  // (its barriers also order every read of s_p above before the scatter)
+    kd_block_scan3<NT>(c, s_wave);  // (its barriers also order every read of s_p above before the scatter)
     {
       int run[3] = {c[0], c[1], c[2]};
 #pragma unroll
@@ -488,7 +497,7 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
         if (i < i1) {
           const bool start = (i & (seg - 1)) == 0;
           for (int x = 0; x < 3; ++x) {
-            if (start) s_segpre[x][i >> lg] = (uint16_t)run[x];
+            if (start) s_segpre[x][(i - base) >> lg] = (uint16_t)run[x];
             run[x] += (int)((fl[x] >> j) & 1u);
           }
         }
@@ -501,11 +510,11 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
       for (int j = 0; j < kChunk; ++j) {
         const int i = i0 + j;
         if (i < i1) {
-          const int s = i >> lg, a0 = s << lg;
+          const int r = i - base, s = r >> lg, a0 = s << lg;  // (window-relative)
           for (int x = 0; x < 3; ++x) {
             const bool left = ((fl[x] >> j) & 1u) != 0u;
             const int lr = run[x] - (int)s_segpre[x][s];
-            s_p[x][left ? a0 + lr : a0 + half + (i - a0 - lr)] = (uint16_t)(pk[x][j >> 1] >> (16 * (j & 1)));
+            s_p[x][left ? a0 + lr : a0 + half + (r - a0 - lr)] = (uint16_t)(pk[x][j >> 1] >> (16 * (j & 1)));
             run[x] += left ? 1 : 0;
           }
         }
@@ -513,7 +522,12 @@ __global__ __launch_bounds__(1024) void kd_split_kernel(KdBufs k, int n, int cap
     }
     __syncthreads();
   }
-  for (int i = tid; i < n; i += 1024) perm[i] = s_p[0][i];
+  if (last) {
+    for (int r = tid; r < nw; r += NT) perm[base + r] = s_p[0][r];
+  } else {
+    for (int x = 0; x < 3; ++x)
+      for (int r = tid; r < nw; r += NT) k.p[(size_t)x * n + base + r] = s_p[x][r];
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -588,10 +602,27 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
                                              st) != hipSuccess)
         return -1;
     }
-    if (n <= kKdLdsBounds)
-      hipLaunchKernelGGL(kd_split_kernel<kKdLdsBounds>, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
-    else if (n <= kKdMaxColliders)
-      hipLaunchKernelGGL(kd_split_kernel<kKdMaxColliders>, dim3(1), dim3(1024), 0, st, k, n, nleaf * kBvhLeaf, sb.perm);
+    if (n <= kKdMaxColliders) {
+      // one 1024-thread workgroup down to 512-position segments, then one 256-thread workgroup per
+      // 512-position window for the levels below
+      const int lg_top = 31 - __builtin_clz((unsigned)(nleaf * kBvhLeaf));  // (a power of 4)
+      const int lg_mid = lg_top > kKdWindowLg ? kKdWindowLg : 2;
+      if (n <= kKdLdsBounds)
+        hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 1024, kKdLdsBounds / 1024, true>), dim3(1), dim3(1024), 0, st, k, n,
+                           lg_top, lg_mid, lg_mid == 2 ? 1 : 0, sb.perm);
+      else
+        hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 1024, kKdMaxColliders / 1024, false>), dim3(1), dim3(1024), 0, st,
+                           k, n, lg_top, lg_mid, lg_mid == 2 ? 1 : 0, sb.perm);
+      if (lg_mid > 2) {
+        const unsigned windows = (unsigned)((n + (1 << kKdWindowLg) - 1) >> kKdWindowLg);
+        if (n <= kKdLdsBounds)
+          hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 256, (1 << kKdWindowLg) / 256, false>), dim3(windows), dim3(256), 0,
+                             st, k, n, kKdWindowLg, 2, 1, sb.perm);
+        else
+          hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 256, (1 << kKdWindowLg) / 256, false>), dim3(windows), dim3(256),
+                             0, st, k, n, kKdWindowLg, 2, 1, sb.perm);
+      }
+    }
     else if (launch_kd_big(k, n, nleaf * kBvhLeaf, sb, st) != 0) return -1;
   } else {  // Morton order of the centres (larger scenes)
     hipLaunchKernelGGL(scene_box_kernel, dim3(1), dim3(1024), 0, st, sc.cull, n, sb.box);
