@@ -113,12 +113,12 @@ __global__ void morton_all_kernel(const CullRec* __restrict__ cull, int n, const
 __device__ __forceinline__ void cull_union(CullRec& a, const CullRec& b) {
   a.lox = fminf(a.lox, b.lox); a.loy = fminf(a.loy, b.loy); a.loz = fminf(a.loz, b.loz);
   a.hix = fmaxf(a.hix, b.hix); a.hiy = fmaxf(a.hiy, b.hiy); a.hiz = fmaxf(a.hiz, b.hiz);
-  a.scale = fmaxf(a.scale, b.scale); a.factor = fmaxf(a.factor, b.factor);
+  a.fscale = fmaxf(a.fscale, b.fscale); a.factor = fmaxf(a.factor, b.factor);
 }
 
 __device__ __forceinline__ CullRec cull_empty() {
   CullRec r;
-  r.lox = r.loy = r.loz = INFINITY; r.hix = r.hiy = r.hiz = -INFINITY; r.scale = 0.0f; r.factor = 0.0f;
+  r.lox = r.loy = r.loz = INFINITY; r.hix = r.hiy = r.hiz = -INFINITY; r.fscale = 0.0f; r.factor = 0.0f;
   return r;
 }
 
@@ -130,7 +130,7 @@ __device__ __forceinline__ CullRec cull_stored(const CullRec& u) {
   if (!(u.lox > u.hix)) return u;
   CullRec r;
   r.lox = r.loy = r.loz = r.hix = r.hiy = r.hiz = INFINITY;
-  r.scale = 0.0f; r.factor = 0.0f;
+  r.fscale = 0.0f; r.factor = 0.0f;
   return r;
 }
 // union with a stored node (an empty one adds nothing)

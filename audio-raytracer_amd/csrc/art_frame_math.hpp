@@ -32,7 +32,7 @@ ART_HD CullRec make_cull(float lx, float ly, float lz, float hx, float hy, float
                    ufinite(scale);
   c.lox = fin ? lx : -INFINITY; c.loy = fin ? ly : -INFINITY; c.loz = fin ? lz : -INFINITY;
   c.hix = fin ? hx : INFINITY; c.hiy = fin ? hy : INFINITY; c.hiz = fin ? hz : INFINITY;
-  c.scale = fin ? scale : 0.0f;
+  c.fscale = fin ? factor * scale : 0.0f;
   c.factor = factor;
   return c;
 }

@@ -57,9 +57,11 @@ struct alignas(16) ObbCold {  // 48 B
 // Broad-phase bounds of one collider (global order: spheres, AABBs, OBBs). A segment set whose
 // bounding box B can be blocked by the collider only if [lo - m, hi + m] overlaps B, with the
 // error margin m = factor * (scale + Omax) (Omax bounds |o|_1 + maxd over the set): see
-// DESIGN.md §5 (broad phase). Non-finite colliders get infinite bounds (always candidates).
+// DESIGN.md §5 (broad phase). fscale = factor * scale, so a test computes m = fscale + factor * Omax
+// (one FMA); a node keeps the largest fscale and factor of its colliders. Non-finite colliders get
+// infinite bounds (always candidates).
 struct alignas(16) CullRec {
-  float lox, loy, loz, scale;
+  float lox, loy, loz, fscale;
   float hix, hiy, hiz, factor;
 };
 
@@ -74,7 +76,7 @@ struct DevScene {
   // of node g at 4g + 1 .. 4g + 4) over a spatial order of the bounds' centres, kBvhLeaf colliders
   // per leaf; the leaves are nodes bvh_leaf0 .. bvh_leaf0 + 4^(levels - 1) - 1 (those past the
   // last collider are empty). A node's CullRec is the union of its colliders' bounds with their
-  // largest margin scale and factor; an empty node is stored at +infinity (lo = hi = +inf, art_bvh.hip cull_stored).
+  // largest fscale and factor; an empty node is stored at +infinity (lo = hi = +inf, art_bvh.hip cull_stored).
   const CullRec* bvh;
   const uint32_t* bvh_ref;        // [ns + na + no] in leaf order: type rank << 30 | in-type index
   const float4* bvh_leaf;         // [4^(levels-1) * kBvhLeaf] slots in leaf order, 64 B (32 B when the

@@ -79,7 +79,7 @@ __device__ __forceinline__ bool force_all(const Seg& s, float om) {
 // The widened box of a BVH node / collider (margin factor * (scale + om)):
 // entry distance of the segment, or false when it misses the box.
 __device__ __forceinline__ bool node_entry(const Seg& s, const CullRec& r, float om, float& tn) {
-  const float m = r.factor * (r.scale + om);
+  const float m = __builtin_fmaf(r.factor, om, r.fscale);  // factor * (scale + om), fscale = factor * scale
   float tf;
   return slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m, r.hix + m, r.hiy + m,
                      r.hiz + m, tn, tf);
@@ -141,7 +141,7 @@ __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
   const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(b.nodes, i * 32, 0, 0));
   const float4 c = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(b.nodes, i * 32 + 16, 0, 0));
   CullRec r;
-  r.lox = a.x; r.loy = a.y; r.loz = a.z; r.scale = a.w;
+  r.lox = a.x; r.loy = a.y; r.loz = a.z; r.fscale = a.w;
   r.hix = c.x; r.hiy = c.y; r.hiz = c.z; r.factor = c.w;
   return r;
 }

@@ -15,7 +15,7 @@
 using namespace art;
 
 static bool node_hit(const Seg& s, const CullRec& r, float om, float frac, float& en) {
-  const float m = frac * r.factor * (r.scale + om);
+  const float m = frac * (r.factor * om + r.fscale);
   float tn, tf;
   const bool h = slab<false>(s.o.x, s.o.y, s.o.z, s.inv.x, s.inv.y, s.inv.z, r.lox - m, r.loy - m, r.loz - m, r.hix + m,
                              r.hiy + m, r.hiz + m, tn, tf);
