@@ -356,16 +356,22 @@ __device__ __forceinline__ float kd_area(float ex, float ey, float ez) {
 // first array is the leaf order (perm), otherwise the three arrays go back to k.p for the next pass.
 constexpr int kKdLdsBounds = 4096;
 constexpr int kKdWindowLg = 9;  // windows of the second pass: 512 positions
-template <int CAP, int NT, int MAXCHUNK, bool LB>
+// BM: where the surface-area pass and the axis choice read the bounds — 0 global memory, 1 LDS by
+// collider id (the whole scene, up to kKdLdsBounds colliders), 2 LDS by window position (the
+// window's colliders, through an id -> position map).
+template <int CAP, int NT, int MAXCHUNK, int BM>
 __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_top, int lg_stop, int last,
                                                       int* __restrict__ perm) {
+  constexpr bool LB = BM != 0;
   __shared__ uint16_t s_p[3][NT * MAXCHUNK];  // the window's three index arrays (relative positions)
   __shared__ uint8_t s_side[CAP];             // 1: left half of its segment (by collider id)
   __shared__ int8_t s_axis[NT * MAXCHUNK / 8];   // per segment of the window: split axis, -1 = fits its left half
   __shared__ uint16_t s_segpre[3][NT * MAXCHUNK / 8];  // left-flag prefix at each segment's start
   __shared__ int s_wave[3][16];
   __shared__ int s_box[2][3][kKdSahSegs][6];  // [half][axis][segment]: lo.xyz, hi.xyz (kd_ord)
-  __shared__ float s_bb[LB ? 6 : 1][LB ? CAP : 1];  // LB: lo.xyz, hi.xyz by collider id
+  constexpr int kBb = BM == 1 ? CAP : (BM == 2 ? NT * MAXCHUNK : 1);
+  __shared__ float s_bb[LB ? 6 : 1][kBb];               // lo.xyz, hi.xyz by collider id (BM 1) or window position (BM 2)
+  __shared__ uint16_t s_slot[BM == 2 ? CAP : 1];        // BM 2: a collider's position in the window (array 0)
   const int tid = threadIdx.x;
   constexpr int kChunk = MAXCHUNK;  // positions per thread, at most
   const int base = (int)blockIdx.x << lg_top;  // (the window's segments are aligned: base is a multiple of 2^lg)
@@ -375,16 +381,25 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
   const int i0 = base + min(nw, tid * chunk), i1 = base + min(nw, tid * chunk + chunk);
   for (int x = 0; x < 3; ++x)
     for (int r = tid; r < nw; r += NT) s_p[x][r] = (uint16_t)k.p[(size_t)x * n + base + r];
-  if (LB)
+  if (BM == 1)
     for (int i = tid; i < n; i += NT) {
       const CullRec c = k.cull[i];
       s_bb[0][i] = c.lox; s_bb[1][i] = c.loy; s_bb[2][i] = c.loz;
       s_bb[3][i] = c.hix; s_bb[4][i] = c.hiy; s_bb[5][i] = c.hiz;
     }
+  if (BM == 2)
+    for (int r = tid; r < nw; r += NT) {
+      const int v = k.p[base + r];  // (array 0's global copy: the LDS one is still being written)
+      const CullRec c = k.cull[v];
+      s_slot[v] = (uint16_t)r;
+      s_bb[0][r] = c.lox; s_bb[1][r] = c.loy; s_bb[2][r] = c.loz;
+      s_bb[3][r] = c.hix; s_bb[4][r] = c.hiy; s_bb[5][r] = c.hiz;
+    }
+  auto bb = [&](int q, int v) -> float { return s_bb[q][BM == 2 ? (int)s_slot[v] : v]; };
   // centre component a of collider v (kd_cen_kernel's value: non-finite -> FLT_MAX)
   auto cen = [&](int v, int a) -> float {
     if (!LB) return kd_comp(k.cen[v], a);
-    const float c = 0.5f * (s_bb[a][v] + s_bb[3 + a][v]);
+    const float c = 0.5f * (bb(a, v) + bb(3 + a, v));
     return isfinite(c) ? c : FLT_MAX;
   };
   __syncthreads();
@@ -417,7 +432,7 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
           key = kk;
           const int v = s_p[x][i - base];
           if (LB) {
-            for (int q = 0; q < 3; ++q) { b[q] = fminf(b[q], s_bb[q][v]); b[3 + q] = fmaxf(b[3 + q], s_bb[3 + q][v]); }
+            for (int q = 0; q < 3; ++q) { b[q] = fminf(b[q], bb(q, v)); b[3 + q] = fmaxf(b[3 + q], bb(3 + q, v)); }
           } else {
             const CullRec c = k.cull[v];
             b[0] = fminf(b[0], c.lox); b[1] = fminf(b[1], c.loy); b[2] = fminf(b[2], c.loz);
@@ -608,18 +623,18 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
       const int lg_top = 31 - __builtin_clz((unsigned)(nleaf * kBvhLeaf));  // (a power of 4)
       const int lg_mid = lg_top > kKdWindowLg ? kKdWindowLg : 2;
       if (n <= kKdLdsBounds)
-        hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 1024, kKdLdsBounds / 1024, true>), dim3(1), dim3(1024), 0, st, k, n,
+        hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 1024, kKdLdsBounds / 1024, 1>), dim3(1), dim3(1024), 0, st, k, n,
                            lg_top, lg_mid, lg_mid == 2 ? 1 : 0, sb.perm);
       else
-        hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 1024, kKdMaxColliders / 1024, false>), dim3(1), dim3(1024), 0, st,
+        hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 1024, kKdMaxColliders / 1024, 0>), dim3(1), dim3(1024), 0, st,
                            k, n, lg_top, lg_mid, lg_mid == 2 ? 1 : 0, sb.perm);
       if (lg_mid > 2) {
         const unsigned windows = (unsigned)((n + (1 << kKdWindowLg) - 1) >> kKdWindowLg);
         if (n <= kKdLdsBounds)
-          hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 256, (1 << kKdWindowLg) / 256, false>), dim3(windows), dim3(256), 0,
+          hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 256, (1 << kKdWindowLg) / 256, 2>), dim3(windows), dim3(256), 0,
                              st, k, n, kKdWindowLg, 2, 1, sb.perm);
         else
-          hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 256, (1 << kKdWindowLg) / 256, false>), dim3(windows), dim3(256),
+          hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 256, (1 << kKdWindowLg) / 256, 2>), dim3(windows), dim3(256),
                              0, st, k, n, kKdWindowLg, 2, 1, sb.perm);
       }
     }
