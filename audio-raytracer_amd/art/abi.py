@@ -199,6 +199,7 @@ SIGNATURES = {
     "art_count_device": (I32, [VP, VP, I32, VP, U32, VP, C.POINTER(art_test_counts)]),
     "art_kernel_timing": (I32, [VP, C.POINTER(art_kernel_times)]),
     "art_executed_counts": (I32, [VP, C.POINTER(art_exec_counts)]),
+    "art_debug_leaf_order": (I32, [VP, C.POINTER(U32), I32]),
     # art_dsp.h
     "art_dsp_process": (I32, [VP, C.POINTER(art_spatializer_settings), C.POINTER(art_audio_source), I32, I32]),
     "art_dsp_source_params_get": (I32, [C.POINTER(art_spatializer_settings), C.POINTER(art_audio_source), I32,

@@ -265,6 +265,14 @@ class Context:
         if rc:
             self._raise(rc)
 
+    def debug_leaf_order(self, cap: int = 1 << 24) -> np.ndarray:
+        """The bound scene's BVH leaf order (art_debug_leaf_order; diagnostics)."""
+        buf = np.zeros(cap, dtype=np.uint32)
+        rc = self.lib.art_debug_leaf_order(self.ptr, buf.ctypes.data_as(C.POINTER(C.c_uint32)), cap)
+        if rc < 0:
+            self._raise(rc)
+        return buf[:rc].copy()
+
     def launch_device(self, d_origins: int, fan_count: int, d_block: int, out_flags: int = 0, stream: int | None = None):
         rc = self.lib.art_launch_device(self.ptr, d_origins, fan_count, d_block, out_flags, stream)
         if rc:

@@ -5,6 +5,7 @@
 // phase is a complete 4-ary tree over all colliders in a spatial leaf order (the kd order below;
 // Morton above kKdMaxColliders), built once per scene upload on the device and refit in place when
 // a resident sync only moved colliders.
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include "art_device_fns.hpp"
@@ -261,6 +262,7 @@ struct KdBufs {
   int* flag;            // [3][n] 1: left half of its segment
   int* scan;            // [3][n] exclusive scan of flag
   uint8_t* side;        // [n] by collider id
+  uint32_t* keys;       // [3][n] radix keys of the centres per axis (kd_keys_kernel)
 };
 static size_t kd_al(size_t v) { return (v + 255) & ~(size_t)255; }
 static KdBufs kd_bufs(void* base, int n) {
@@ -269,6 +271,7 @@ static KdBufs kd_bufs(void* base, int n) {
   size_t o = 0;
   k.cen = reinterpret_cast<float4*>(b + o); o += kd_al(16 * (size_t)n);
   k.p = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
+  k.keys = reinterpret_cast<uint32_t*>(b + o); o += kd_al(12 * (size_t)n);
   if (n > kKdMaxColliders) {
     k.p2 = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
     k.flag = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
@@ -280,27 +283,24 @@ static KdBufs kd_bufs(void* base, int n) {
 }
 size_t kd_scratch_bytes(int n) {
   if (n <= 0) return 0;
-  const size_t base = kd_al(16 * (size_t)n) + kd_al(12 * (size_t)n);
+  const size_t base = kd_al(16 * (size_t)n) + 2 * kd_al(12 * (size_t)n);
   return n <= kKdMaxColliders ? base : base + 3 * kd_al(12 * (size_t)n) + kd_al((size_t)n);
 }
 
-__global__ void kd_cen_kernel(const CullRec* __restrict__ cull, int n, float4* __restrict__ cen) {
+// Centres (non-finite components -> FLT_MAX, sorting last) and their radix-sortable keys on the
+// three axes, with the identity values of the sorts (one launch; round 4: one centre launch and one
+// key launch per axis)
+__global__ void kd_keys_kernel(const CullRec* __restrict__ cull, int n, KdBufs k, int* __restrict__ vals) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const CullRec c = cull[i];
   float v[3] = {0.5f * (c.lox + c.hix), 0.5f * (c.loy + c.hiy), 0.5f * (c.loz + c.hiz)};
-  for (int a = 0; a < 3; ++a) v[a] = isfinite(v[a]) ? v[a] : FLT_MAX;
-  cen[i] = make_float4(v[0], v[1], v[2], 0.0f);
-}
-
-// radix-sortable key of centre component `axis` (FLT_MAX for non-finite ones sorts last)
-__global__ void kd_key_kernel(const float4* __restrict__ cen, int n, int axis, uint32_t* __restrict__ keys,
-                              int* __restrict__ vals) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 c = cen[i];
-  const uint32_t u = __float_as_uint(axis == 0 ? c.x : (axis == 1 ? c.y : c.z));
-  keys[i] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  for (int a = 0; a < 3; ++a) {
+    v[a] = isfinite(v[a]) ? v[a] : FLT_MAX;
+    const uint32_t u = __float_as_uint(v[a]);
+    k.keys[(size_t)a * n + i] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  }
+  k.cen[i] = make_float4(v[0], v[1], v[2], 0.0f);
   vals[i] = i;
 }
 
@@ -342,6 +342,24 @@ __device__ __forceinline__ int kd_ord(float f) {  // monotone float -> int (for 
   return b >= 0 ? b : b ^ 0x7fffffff;
 }
 __device__ __forceinline__ float kd_unord(int v) { return __int_as_float(v >= 0 ? v : v ^ 0x7fffffff); }
+// Min / max over aligned groups of gsz lanes (a power of two <= 64), the result in every lane of the
+// group: DPP within rows of 16 lanes (xor 1, xor 2, half-row mirror, row mirror), shuffles across
+// rows. (Round 4: shuffles at every step left the surface-area pass at ~12 us per level.)
+template <int CTRL>
+__device__ __forceinline__ float kd_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <bool MIN>
+__device__ __forceinline__ float kd_grp(float v, int gsz) {
+  auto op = [](float a, float b) { return MIN ? fminf(a, b) : fmaxf(a, b); };
+  if (gsz >= 2) v = op(v, kd_dpp<0xB1>(v));   // quad_perm [1, 0, 3, 2]
+  if (gsz >= 4) v = op(v, kd_dpp<0x4E>(v));   // quad_perm [2, 3, 0, 1]
+  if (gsz >= 8) v = op(v, kd_dpp<0x141>(v));  // row_half_mirror
+  if (gsz >= 16) v = op(v, kd_dpp<0x140>(v)); // row_mirror
+  if (gsz >= 32) v = op(v, __shfl_xor(v, 16, 64));
+  if (gsz >= 64) v = op(v, __shfl_xor(v, 32, 64));
+  return v;
+}
 __device__ __forceinline__ float kd_area(float ex, float ey, float ez) {
   ex = fmaxf(ex, 0.0f); ey = fmaxf(ey, 0.0f); ez = fmaxf(ez, 0.0f);
   return ex * ey + ey * ez + ez * ex;
@@ -379,30 +397,77 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
   if (nw <= 0) return;
   const int chunk = (nw + NT - 1) / NT;
   const int i0 = base + min(nw, tid * chunk), i1 = base + min(nw, tid * chunk + chunk);
-  for (int x = 0; x < 3; ++x)
-    for (int r = tid; r < nw; r += NT) s_p[x][r] = (uint16_t)k.p[(size_t)x * n + base + r];
-  if (BM == 1)
-    for (int i = tid; i < n; i += NT) {
-      const CullRec c = k.cull[i];
-      s_bb[0][i] = c.lox; s_bb[1][i] = c.loy; s_bb[2][i] = c.loz;
-      s_bb[3][i] = c.hix; s_bb[4][i] = c.hiy; s_bb[5][i] = c.hiz;
+  // the window's arrays (and bounds) into LDS: every load of a work-item issued before its first
+  // store, so the prologue waits for one round of memory latency per dependent step, not per
+  // element (round 4: the per-element loop serialized ~16 global round trips in the top pass)
+  {
+    int pv[3][kChunk];
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) {
+        const int r = tid + j * NT;
+        pv[x][j] = r < nw ? k.p[(size_t)x * n + base + r] : 0;
+      }
+    if (BM == 2) {  // bounds by window position (array 0's order)
+      CullRec cv[kChunk];
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) {
+        const int r = tid + j * NT;
+        if (r < nw) cv[j] = k.cull[pv[0][j]];
+      }
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) {
+        const int r = tid + j * NT;
+        if (r < nw) {
+          s_slot[pv[0][j]] = (uint16_t)r;
+          s_bb[0][r] = cv[j].lox; s_bb[1][r] = cv[j].loy; s_bb[2][r] = cv[j].loz;
+          s_bb[3][r] = cv[j].hix; s_bb[4][r] = cv[j].hiy; s_bb[5][r] = cv[j].hiz;
+        }
+      }
     }
-  if (BM == 2)
-    for (int r = tid; r < nw; r += NT) {
-      const int v = k.p[base + r];  // (array 0's global copy: the LDS one is still being written)
-      const CullRec c = k.cull[v];
-      s_slot[v] = (uint16_t)r;
-      s_bb[0][r] = c.lox; s_bb[1][r] = c.loy; s_bb[2][r] = c.loz;
-      s_bb[3][r] = c.hix; s_bb[4][r] = c.hiy; s_bb[5][r] = c.hiz;
+    if (BM == 1) {  // bounds by collider id (the whole scene: n <= CAP = NT * kChunk)
+      CullRec cv[kChunk];
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) {
+        const int i = tid + j * NT;
+        if (i < n) cv[j] = k.cull[i];
+      }
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) {
+        const int i = tid + j * NT;
+        if (i < n) {
+          s_bb[0][i] = cv[j].lox; s_bb[1][i] = cv[j].loy; s_bb[2][i] = cv[j].loz;
+          s_bb[3][i] = cv[j].hix; s_bb[4][i] = cv[j].hiy; s_bb[5][i] = cv[j].hiz;
+        }
+      }
     }
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) {
+        const int r = tid + j * NT;
+        if (r < nw) s_p[x][r] = (uint16_t)pv[x][j];
+      }
+  }
+#ifdef ART_KD_PROF  // diagnostics: per-phase wall clock of workgroup 0 (printf at the end)
+  unsigned long long kp_t[64];
+  int kp_n = 0;
+  auto kp = [&]() { if (kp_n < 64) kp_t[kp_n++] = wall_clock64(); };
+  kp();
+#define KP() kp()
+#else
+#define KP() (void)0
+#endif
   auto bb = [&](int q, int v) -> float { return s_bb[q][BM == 2 ? (int)s_slot[v] : v]; };
-  // centre component a of collider v (kd_cen_kernel's value: non-finite -> FLT_MAX)
+  // centre component a of collider v (kd_keys_kernel's value: non-finite -> FLT_MAX)
   auto cen = [&](int v, int a) -> float {
     if (!LB) return kd_comp(k.cen[v], a);
     const float c = 0.5f * (bb(a, v) + bb(3 + a, v));
     return isfinite(c) ? c : FLT_MAX;
   };
   __syncthreads();
+  KP();
   for (int lg = lg_top; lg > lg_stop; --lg) {  // segments of seg = 2^lg positions
     const int seg = 1 << lg, half = seg >> 1, nseg = (nw + seg - 1) >> lg;  // (this window's segments)
     const bool sah = ((n + seg - 1) >> lg) <= kKdSahSegs;  // (the policy counts the whole order's segments)
@@ -440,11 +505,7 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
           }
         }
         if (gsz > 1) {  // (block-uniform) min / max over each group, then its first lane publishes
-          for (int q = 0; q < 6; ++q)
-            for (int off = gsz >> 1; off > 0; off >>= 1) {
-              const float o = __shfl_xor(b[q], off, 64);
-              b[q] = q < 3 ? fminf(b[q], o) : fmaxf(b[q], o);
-            }
+          for (int q = 0; q < 6; ++q) b[q] = q < 3 ? kd_grp<true>(b[q], gsz) : kd_grp<false>(b[q], gsz);
           // the group's key is its first lane's (-1 when that chunk is empty: then every later one is)
           key = __shfl(key, (tid & 63) & ~(gsz - 1), 64);
           if ((tid & (gsz - 1)) == 0) flush();
@@ -454,6 +515,7 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
       }
       __syncthreads();
     }
+    KP();
     for (int s = tid; s < nseg; s += NT) {  // each segment's axis: the cheapest split (SAH) or the widest spread of centres
       const int a0 = s << lg, cnt = min(seg, nw - a0);  // (window-relative)
       int ax = -1;
@@ -479,6 +541,7 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
       s_axis[s] = (int8_t)ax;
     }
     __syncthreads();
+    KP();
     for (int r = tid; r < nw; r += NT) {  // side of each collider: its rank on its segment's axis
       const int ax = s_axis[r >> lg];
       if (ax >= 0) s_side[s_p[ax][r]] = (r & (seg - 1)) < half ? 1 : 0;
@@ -503,6 +566,7 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
         }
       }
     }
+    KP();
     kd_block_scan3<NT>(c, s_wave);  // (its barriers also order every read of s_p above before the scatter)
     {
       int run[3] = {c[0], c[1], c[2]};
@@ -536,13 +600,121 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
       }
     }
     __syncthreads();
+    KP();
   }
+#ifdef ART_KD_PROF
+  if (blockIdx.x == 0 && tid == 0) {
+    printf("[kd] NT %d BM %d nw %d lg %d..%d load %llu\n", NT, BM, nw, lg_top, lg_stop, (kp_t[1] - kp_t[0]) * 10ull);
+    for (int q = 1; q + 4 <= kp_n - 1; q += 4)
+      printf("[kd]   level: sah %llu axis %llu side %llu scan+part %llu ns\n", (kp_t[q + 1] - kp_t[q]) * 10ull,
+             (kp_t[q + 2] - kp_t[q + 1]) * 10ull, (kp_t[q + 3] - kp_t[q + 2]) * 10ull, (kp_t[q + 4] - kp_t[q + 3]) * 10ull);
+  }
+#endif
+#undef KP
   if (last) {
     for (int r = tid; r < nw; r += NT) perm[base + r] = s_p[0][r];
   } else {
     for (int x = 0; x < 3; ++x)
       for (int r = tid; r < nw; r += NT) k.p[(size_t)x * n + base + r] = s_p[x][r];
   }
+}
+
+// The binary levels of segments of at most 64 positions (lg_top <= 6), one wave per aligned block of
+// 64 positions and no workgroup barriers (round 4: below 512 positions the window pass spent its
+// time in block scans and barriers). The block's 64 colliders stay the same through these levels,
+// so the three arrays hold block-local slots (the collider's position in array 0 on entry) and the
+// bounds sit in LDS by slot. Per level: the split axis (the same surface-area cost or spread of
+// centres as kd_split_kernel, from half-segment reductions over xor shuffles), the side of each
+// slot by its rank on that axis, and a stable partition of every array from ballot ranks, moved
+// through a per-wave LDS row. Writes the leaf order (perm).
+constexpr int kKdWaveLg = 6;
+static bool kd_wave_enabled() {  // ART_KD_WAVE=0 (read per build): the block passes run every level (A/B, tests)
+  const char* e = getenv("ART_KD_WAVE");
+  return !(e && e[0] == '0');
+}
+template <int CAP>
+__global__ __launch_bounds__(256) void kd_wave_kernel(KdBufs k, int n, int lg_top, int* __restrict__ perm) {
+  __shared__ uint16_t s_slot[CAP];         // collider id -> slot (the block's array-0 position)
+  __shared__ int s_id[4][64];              // slot -> collider id
+  __shared__ float s_bb[4][6][64];         // slot -> lo.xyz, hi.xyz
+  __shared__ uint8_t s_side[4][64];        // slot -> 1: left half of its segment
+  __shared__ uint8_t s_row[4][3][64];      // the partition's destination rows
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int base = (int)blockIdx.x * 256 + wv * 64;
+  const int cnt = min(64, n - base);
+  if (cnt <= 0) return;  // (no workgroup barriers below: a wave may leave)
+  const bool live = lane < cnt;
+  int id[3] = {0, 0, 0};
+  for (int x = 0; x < 3; ++x) id[x] = live ? k.p[(size_t)x * n + base + lane] : 0;
+  CullRec c;
+  if (live) c = k.cull[id[0]];
+  if (live) {
+    s_slot[id[0]] = (uint16_t)lane;
+    s_id[wv][lane] = id[0];
+    s_bb[wv][0][lane] = c.lox; s_bb[wv][1][lane] = c.loy; s_bb[wv][2][lane] = c.loz;
+    s_bb[wv][3][lane] = c.hix; s_bb[wv][4][lane] = c.hiy; s_bb[wv][5][lane] = c.hiz;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  int v[3];  // this lane's slot in each array
+  v[0] = lane;
+  v[1] = live ? (int)s_slot[id[1]] : 0;
+  v[2] = live ? (int)s_slot[id[2]] : 0;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int lg = lg_top; lg > 2; --lg) {
+    const int seg = 1 << lg, half = seg >> 1;
+    const int s_lo = lane & ~(seg - 1), cnt_s = min(seg, max(0, cnt - s_lo));
+    const bool sah = ((n + seg - 1) >> lg) <= kKdSahSegs;  // (the policy counts the whole order's segments)
+    const bool left_half = (lane - s_lo) < half;
+    int ax = -1;
+    if (sah) {  // (wave-uniform) bounds of both halves of the segment for a split on each axis
+      float best = INFINITY;
+      for (int x = 0; x < 3; ++x) {
+        float b[6];
+        for (int q = 0; q < 3; ++q) {
+          b[q] = live ? s_bb[wv][q][v[x]] : INFINITY;
+          b[3 + q] = live ? s_bb[wv][3 + q][v[x]] : -INFINITY;
+        }
+        for (int q = 0; q < 6; ++q) b[q] = q < 3 ? kd_grp<true>(b[q], half) : kd_grp<false>(b[q], half);  // this half's bounds
+        float ob[6];  // the other half's
+        for (int q = 0; q < 6; ++q) ob[q] = __shfl_xor(b[q], half, 64);
+        const float* l = left_half ? b : ob;
+        const float* r = left_half ? ob : b;
+        const float cost = kd_area(l[3] - l[0], l[4] - l[1], l[5] - l[2]) * (float)half +
+                           kd_area(r[3] - r[0], r[4] - r[1], r[5] - r[2]) * (float)(cnt_s - half);
+        if (cnt_s > half && cost < best) { best = cost; ax = x; }  // (a non-finite cost never wins)
+      }
+    }
+    if (cnt_s > half && ax < 0) {  // the widest spread of centres (kd_keys_kernel's values)
+      float best = -1.0f;
+      for (int x = 0; x < 3; ++x) {
+        const int vf = __shfl(v[x], s_lo, 64), vl = __shfl(v[x], s_lo + max(cnt_s, 1) - 1, 64);
+        const float cf = 0.5f * (s_bb[wv][x][vf] + s_bb[wv][3 + x][vf]), cl = 0.5f * (s_bb[wv][x][vl] + s_bb[wv][3 + x][vl]);
+        const float e = (isfinite(cl) ? cl : FLT_MAX) - (isfinite(cf) ? cf : FLT_MAX);
+        if (ax < 0 || e > best) { best = e; ax = x; }
+      }
+    }  // (segment-uniform branch: the lanes read are live lanes of the same segment)
+    if (ax >= 0 && live) {
+      const int va = ax == 0 ? v[0] : (ax == 1 ? v[1] : v[2]);
+      s_side[wv][va] = left_half ? 1 : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t segmask = (seg == 64 ? ~0ull : (((1ull << seg) - 1ull) << s_lo));
+    for (int x = 0; x < 3; ++x) {
+      const bool left = ax < 0 ? true : s_side[wv][v[x]] != 0;
+      const uint64_t m = __ballot(live && left);
+      const int lr = __popcll(m & segmask & lt);
+      const int dst = left ? s_lo + lr : s_lo + half + (lane - s_lo - lr);
+      if (live) s_row[wv][x][dst] = (uint8_t)v[x];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int x = 0; x < 3; ++x) v[x] = live ? (int)s_row[wv][x][lane] : 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (live) perm[base + lane] = s_id[wv][v[0]];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -609,17 +781,38 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   if (sb.kd) {  // kd leaf order
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
-    hipLaunchKernelGGL(kd_cen_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k.cen);
+    hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
     for (int a = 0; a < 3; ++a) {
-      hipLaunchKernelGGL(kd_key_kernel, dim3((n + 255) / 256), dim3(256), 0, st, k.cen, n, a, sb.keys, sb.vals);
       size_t bytes = sb.temp_bytes;
-      if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, sb.keys, sb.keys_s, sb.vals, k.p + (size_t)a * n, n, 0, 32,
-                                             st) != hipSuccess)
+      if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
+                                             n, 0, 32, st) != hipSuccess)
         return -1;
     }
-    if (n <= kKdMaxColliders) {
+    if (n <= kKdMaxColliders && kd_wave_enabled()) {
       // one 1024-thread workgroup down to 512-position segments, then one 256-thread workgroup per
-      // 512-position window for the levels below
+      // 512-position window down to 64-position segments, then one wave per 64-position block
+      const int lg_top = 31 - __builtin_clz((unsigned)(nleaf * kBvhLeaf));  // (a power of 4)
+      const int lg_wave = lg_top < kKdWaveLg ? lg_top : kKdWaveLg;
+      const int lg_mid = lg_top > kKdWindowLg ? kKdWindowLg : lg_wave;
+      if (lg_top > lg_mid) {
+        if (n <= kKdLdsBounds)
+          hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 1024, kKdLdsBounds / 1024, 1>), dim3(1), dim3(1024), 0, st, k, n,
+                             lg_top, lg_mid, 0, sb.perm);
+        else
+          hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 1024, kKdMaxColliders / 1024, 0>), dim3(1), dim3(1024), 0, st,
+                             k, n, lg_top, lg_mid, 0, sb.perm);
+      }
+      if (lg_mid > lg_wave) {
+        const unsigned windows = (unsigned)((n + (1 << kKdWindowLg) - 1) >> kKdWindowLg);
+        if (n <= kKdLdsBounds)
+          hipLaunchKernelGGL((kd_split_kernel<kKdLdsBounds, 256, (1 << kKdWindowLg) / 256, 2>), dim3(windows), dim3(256), 0,
+                             st, k, n, kKdWindowLg, lg_wave, 0, sb.perm);
+        else
+          hipLaunchKernelGGL((kd_split_kernel<kKdMaxColliders, 256, (1 << kKdWindowLg) / 256, 2>), dim3(windows), dim3(256),
+                             0, st, k, n, kKdWindowLg, lg_wave, 0, sb.perm);
+      }
+      hipLaunchKernelGGL((kd_wave_kernel<kKdMaxColliders>), dim3((n + 255) / 256), dim3(256), 0, st, k, n, lg_wave, sb.perm);
+    } else if (n <= kKdMaxColliders) {  // (ART_KD_WAVE=0: the block passes down to 4-position segments)
       const int lg_top = 31 - __builtin_clz((unsigned)(nleaf * kBvhLeaf));  // (a power of 4)
       const int lg_mid = lg_top > kKdWindowLg ? kKdWindowLg : 2;
       if (n <= kKdLdsBounds)

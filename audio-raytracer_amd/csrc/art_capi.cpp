@@ -1357,6 +1357,19 @@ ART_API int art_executed_counts(art_ctx* c, art_exec_counts* out) {
   return ART_OK;
 }
 
+ART_API int art_debug_leaf_order(art_ctx* c, uint32_t* out, int32_t cap) {
+  if (!c || (!out && cap > 0) || cap < 0) return ART_E_INVALID;
+  if (c->devs.empty() || !c->devs[0].bound) return ART_E_STATE;
+  Device& dv = c->devs[0];
+  const int n = dv.sc.ns + dv.sc.na + dv.sc.no;
+  if (!dv.sc.bvh_ref || n <= 0) return 0;
+  const int m = n < cap ? n : cap;
+  HIP_TRY(c, hipSetDevice(dv.id));
+  HIP_TRY(c, hipDeviceSynchronize());
+  if (m > 0) HIP_TRY(c, hipMemcpy(out, dv.sc.bvh_ref, (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return m;
+}
+
 ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {
   if (!c || !out) return ART_E_INVALID;
   memset(out, 0, sizeof *out);

@@ -52,13 +52,10 @@ __device__ __forceinline__ float cells_far_of(const CullRec& root, vec3 tg) {
   return sqrtf(dx * dx + dy * dy + dz * dz) * 1.001f + 1e-3f;
 }
 
-__global__ void cells_prep_kernel(DevScene sc, int T, float* __restrict__ far, uint32_t* __restrict__ ok) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
-  float v = INFINITY;
-  if (sc.bvh_levels > 0) v = cells_far_of(sc.bvh[0], load3(sc.targets, t));
-  far[t] = v;
-  ok[t] = isfinite(v) ? 1u : 0u;  // non-finite colliders: every muffle ray tests every collider
+// far_t of target t, or INFINITY (no BVH or non-finite colliders: every muffle ray of t tests
+// every collider)
+__device__ __forceinline__ float cells_far_t(const DevScene& sc, int t) {
+  return sc.bvh_levels > 0 ? cells_far_of(sc.bvh[0], load3(sc.targets, t)) : INFINITY;
 }
 
 // Global collider g (spheres, AABBs, OBBs): its order code and AudioTargetId.
@@ -112,14 +109,24 @@ __device__ __forceinline__ void cell_rects_write(CellGeo* geo, int T, int n, int
                                      ((uint32_t)G.rect[f][3] << 24);
 }
 
-// One thread per (target, collider).
-// (grid-stride over the pairs: one launch stays far below HIP's 2^32 work-item limit)
+// One work-item per (target, collider), and per (target, cell, type) counter (zeroed, with the
+// sentinel); the first T also set each target's segment bound, list flag and entry total.
+// (grid-stride: one launch stays far below HIP's 2^32 work-item limit)
 __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int T, long long k, CellGeo* __restrict__ geo);
-__global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb, int T, CellGeo* __restrict__ geo) {
+__global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb, int T, CellGeo* __restrict__ geo,
+                                                        uint32_t counters) {
   const int n = sc.ns + sc.na + sc.no;
-  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < (long long)n * T;
-       k += (long long)gridDim.x * blockDim.x)
-    cells_geo_one(sc, cb, n, T, k, geo);
+  const long long items = std::max((long long)n * T, (long long)counters);
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < items; k += (long long)gridDim.x * blockDim.x) {
+    if (k < counters) cb.count[k] = 0u;
+    if (k < T) {
+      const float v = cells_far_t(sc, (int)k);
+      cb.far[k] = v;
+      cb.ok[k] = isfinite(v) ? 1u : 0u;
+      cb.tcount[k] = 0ull;
+    }
+    if (k < (long long)n * T) cells_geo_one(sc, cb, n, T, k, geo);
+  }
 }
 __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int T, long long k, CellGeo* __restrict__ geo) {
   const int t = (int)(k / n), g = (int)(k - (long long)t * n);
@@ -133,12 +140,12 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int
   G.all = 0u;
   G.ux = G.uy = G.uz = G.sb = G.cb = G.near = 0.0f;
   // owned by the target (its muffle rays skip it, :413, :426, :439) or no lists: no cells
-  if (!cb.ok[t] || tid == t) { geo[k] = G; cell_rects_write(geo, T, n, t, g, G); return; }
+  const float far = cells_far_t(sc, t);  // (cb.far[t], written by another work-item of this launch)
+  if (!isfinite(far) || tid == t) { geo[k] = G; cell_rects_write(geo, T, n, t, g, G); return; }
   // The collider's bounding sphere and its error margin. Every test's rounding is relative to the
   // segment-start-to-collider vector (the operands o and the record are exact floats): a reported
   // blocking point lies within factor * (|o - c| + |h|_1) of the shape,
   // and |o - c| <= maxd + rho <= far_t + rho for a collider the segment meets.
-  const float far = cb.far[t];
   const vec3 tg = load3(sc.targets, t);
   const CullRec cr = sc.cull[g];
   vec3 cc0;
@@ -197,15 +204,20 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int
 }
 
 // One workgroup per (target, face, cell row) and 256 colliders (grid-stride over these units): each
-// work-item tests the row's cells of its collider's face rectangle against the pair's cone, and the
-// workgroup aggregates its hits per (cell, collider type) in LDS, so the global counters see one
-// atomic per touched (cell, type) and workgroup instead of one per entry (round 4: the per-entry
-// atomics and the 64-B record per item set the passes' 96 + 107 us at config 2). FILL = false
-// counts per cell; FILL = true reserves each (cell, type)'s range once and writes the entries of the
-// targets whose lists fit (cells_fit_kernel).
+// work-item tests the row's cells of its collider's face rectangle against the pair's cone (the
+// row's 32 cones staged in LDS), and the workgroup aggregates its hits per (cell, collider type) in
+// LDS, so the global counters see one atomic per touched (cell, type) and workgroup instead of one
+// per entry (round 4: the per-entry atomics and the 64-B record per item set the passes' 96 + 107
+// us at config 2). FILL = false counts per cell; FILL = true reserves each (cell, type)'s range
+// once, counting the cell's counter down from its count (ranges start + [new, old) are disjoint and
+// fill the cell exactly), and writes the entries of the targets whose lists fit
+// (cells_drop_kernel). (Round 4 also measured one workgroup per (target, face): 128 + 256 us with
+// per-item load balancing over each wave — 32x fewer waves left every step's latency exposed.)
 template <bool FILL>
 __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ geo, int T, CellBufs cb, int n) {
-  __shared__ uint32_t s_cnt[kCellG * 3], s_base[kCellG * 3];
+  __shared__ uint32_t s_cnt[kCellG * 3];
+  __shared__ float4 s_cone[kCellG];  // axis, cos_a
+  __shared__ float s_sin[kCellG];
   const int tid = threadIdx.x;
   const int chunks = (n + 255) >> 8;
   const long long units = (long long)T * 6 * kCellG * chunks;
@@ -214,44 +226,48 @@ __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ ge
     const long long row = u / chunks;
     const int gc = (int)(u - row * chunks);
     const int t = (int)(row / (6 * kCellG)), fr = (int)(row - (long long)t * 6 * kCellG), f = fr / kCellG, j = fr - f * kCellG;
+    if (FILL && !cb.ok[t]) continue;  // (workgroup-uniform: a dropped target's lists stay empty)
     const int g = gc * 256 + tid;
     if (tid < kCellG * 3) s_cnt[tid] = 0u;
-    __syncthreads();
+    if (tid < kCellG) {
+      const CellCone cc = cb.cones[(f * kCellG + j) * kCellG + tid];
+      s_cone[tid] = make_float4(cc.ax, cc.ay, cc.az, cc.cos_a);
+      s_sin[tid] = cc.sin_a;
+    }
     const uint32_t rc = g < n ? rects[((size_t)t * 6 + f) * n + g] : 0x00000001u;  // (i0 1 > i1 0: empty)
     const int i0 = (int)(rc & 0xffu), i1 = (int)((rc >> 8) & 0xffu), j0 = (int)((rc >> 16) & 0xffu), j1 = (int)(rc >> 24);
-    const bool rows = !(j < j0 || j > j1 || i0 > i1) && (!FILL || cb.ok[t]);
+    const bool rows = !(j < j0 || j > j1 || i0 > i1);
     CellGeo G;
     uint32_t ty = 0u;
     if (rows) {
       G = geo[(size_t)t * n + g];
       ty = G.code >> 28;  // one list per collider type
     }
-    // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
-    auto hit = [&](int i) {
-      const CellCone cc = cb.cones[(f * kCellG + j) * kCellG + i];
-      return G.all || (G.ux * cc.ax + G.uy * cc.ay + G.uz * cc.az >= (cc.cos_a * G.cb - cc.sin_a * G.sb) - 1e-5f);
-    };
+    __syncthreads();
     uint32_t hm = 0u;  // the row's cells this collider's cone touches (kCellG = 32 bits)
-    for (int i = i0; rows && i <= i1; ++i)
-      if (hit(i)) {
+    for (int i = i0; rows && i <= i1; ++i) {
+      // angle(u, axis) <= alpha_c + beta  <=>  u . axis >= cos(alpha_c + beta)
+      const float4 cc = s_cone[i];
+      if (G.all || (G.ux * cc.x + G.uy * cc.y + G.uz * cc.z >= (cc.w * G.cb - s_sin[i] * G.sb) - 1e-5f)) {
         hm |= 1u << i;
         atomicAdd(&s_cnt[i * 3 + ty], 1u);
       }
+    }
     __syncthreads();
     const size_t rbase = ((size_t)t * kCells + (size_t)(f * kCellG + j) * kCellG) * 3;  // the row's counters
     if (!FILL) {
       if (tid < kCellG * 3 && s_cnt[tid]) atomicAdd(cb.count + rbase + tid, s_cnt[tid]);
     } else {
       if (tid < kCellG * 3) {
-        s_base[tid] = s_cnt[tid] ? atomicAdd(cb.cursor + rbase + tid, s_cnt[tid]) : 0u;
-        s_cnt[tid] = 0u;
+        const uint32_t c = s_cnt[tid];
+        if (c) s_cnt[tid] = cb.start[rbase + tid] + atomicSub(cb.count + rbase + tid, c) - c;
       }
       __syncthreads();
       if (hm) {
         const uint32_t key = near_key(__float_as_uint(G.near));
         for (uint32_t m = hm; m; m &= m - 1u) {
           const int i = __builtin_ctz(m);
-          const uint32_t pos = s_base[i * 3 + ty] + atomicAdd(&s_cnt[i * 3 + ty], 1u);
+          const uint32_t pos = atomicAdd(&s_cnt[i * 3 + ty], 1u);
           if (pos < cb.cap) {  // the entry and its sort key (the segmented sort orders each cell by near bound)
             if (cb.compact) reinterpret_cast<uint32_t*>(cb.ent)[pos] = (G.code & 0xffffu) | (key << 16);
             else cb.ent[pos] = make_uint2(G.code, __float_as_uint(G.near));
@@ -262,43 +278,52 @@ __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ ge
         }
       }
     }
-    __syncthreads();  // (s_cnt / s_base are reused by the next unit)
+    __syncthreads();  // (the LDS arrays are reused by the next unit)
   }
 }
 
-// Entries per target (64-bit sums of its cells' counts; one workgroup per target), for the
-// capacity check. (Per-entry atomics on T counters serialized the count pass: 90 -> 264 us.)
+// Entries per target (64-bit sums of its cells' counts) for the capacity check: one workgroup per
+// 256 counters (kCells * 3 = 72 of them per target), one atomic per workgroup. (Round 4: one
+// workgroup per target took 19 us at config 2; per-entry atomics on T counters serialized the count
+// pass, 90 -> 264 us.)
 __global__ __launch_bounds__(256) void cells_total_kernel(CellBufs cb) {
+  static_assert((kCells * 3) % 256 == 0, "a workgroup covers one target's counters");
   __shared__ unsigned long long s[256];
-  const uint32_t* c = cb.count + (size_t)blockIdx.x * kCells * 3;
-  unsigned long long v = 0;
-  for (int i = threadIdx.x; i < kCells * 3; i += 256) v += c[i];
-  s[threadIdx.x] = v;
+  s[threadIdx.x] = cb.count[(size_t)blockIdx.x * 256 + threadIdx.x];
   __syncthreads();
   for (int st = 128; st > 0; st >>= 1) {
     if ((int)threadIdx.x < st) s[threadIdx.x] += s[threadIdx.x + st];
     __syncthreads();
   }
-  if (threadIdx.x == 0) cb.tcount[blockIdx.x] = s[0];
+  if (threadIdx.x == 0 && s[0]) atomicAdd(cb.tcount + blockIdx.x / ((kCells * 3) / 256), s[0]);
 }
 
-// Capacity check between the count and the fill: targets in order keep their lists while the
-// running total of entries fits the capacity; a target that does not fit (or whose far bound is
-// non-finite) is dropped — ok = 0, its muffle rays test every collider. The kept targets' total is
-// at most the capacity (< 2^32), so the u32 scan of the cell counts cannot wrap.
-__global__ void cells_fit_kernel(CellBufs cb, int T) {
-  if (threadIdx.x != 0) return;
-  unsigned long long run = 0;
-  for (int t = 0; t < T; ++t) {
-    const unsigned long long c = cb.tcount[t];
-    if (cb.ok[t] && run + c <= (unsigned long long)cb.cap) run += c;
-    else cb.ok[t] = 0u;
-  }
-}
-// The dropped targets' cell counts are cleared before the scan.
-__global__ void cells_drop_kernel(CellBufs cb, uint32_t cells) {
+// Capacity check between the count and the fill, one work-item per (target, cell, type) counter:
+// targets in order keep their lists while the running total of entries fits the capacity; a
+// target that does not fit (or whose far bound is non-finite) is dropped — ok = 0, its counters
+// cleared, its muffle rays test every collider. Each workgroup's first work-item replays the
+// running total up to its target (kCells * 3 is a multiple of 256: a workgroup covers one target).
+// Another workgroup may clear ok[t'] of an earlier target while this one reads it: that happens
+// only for a target the replay leaves out either way. The kept targets' total is at most the
+// capacity (< 2^32), so the u32 scan of the counts cannot wrap and every start is <= cap.
+__global__ __launch_bounds__(256) void cells_drop_kernel(CellBufs cb, int T, uint32_t cells) {
+  static_assert((kCells * 3) % 256 == 0, "a workgroup covers one target's counters");
+  __shared__ uint32_t s_keep;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cells && !cb.ok[i / (kCells * 3)]) cb.count[i] = 0u;
+  const int t = min((int)(blockIdx.x * blockDim.x / (kCells * 3)), T - 1);
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    bool keep = false;
+    for (int u = 0; u <= t; ++u) {
+      const unsigned long long c = cb.tcount[u];
+      keep = cb.ok[u] && run + c <= (unsigned long long)cb.cap;
+      if (keep) run += c;
+    }
+    s_keep = keep ? 1u : 0u;
+    if (!keep && blockIdx.x * blockDim.x == (uint32_t)t * (kCells * 3)) cb.ok[t] = 0u;
+  }
+  __syncthreads();
+  if (i < cells && !s_keep) cb.count[i] = 0u;
 }
 
 size_t cells_scan_temp_bytes(int T, uint32_t cap) {
@@ -314,12 +339,6 @@ size_t cells_scan_temp_bytes(int T, uint32_t cap) {
                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, n - 1,
                                                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0, 16);
   return std::max(scan, std::max(sort, sort32));
-}
-
-// The sort's segment offsets, clamped to the capacity (the fill pass wrote the entries' keys).
-__global__ void cells_key_kernel(CellBufs cb, uint32_t total_cells) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i <= total_cells) cb.cursor[i] = min(cb.start[i], cb.cap);
 }
 
 // Entry capacity: 128 cells per (target, collider) on average (a collider near its target spans
@@ -349,7 +368,6 @@ static unsigned row_grid(int T, int n) {
 int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   const int T = sc.T, n = sc.ns + sc.na + sc.no;
   const int cells = T * kCells * 3;  // lists: (target, cell, collider type)
-  hipLaunchKernelGGL(cells_prep_kernel, dim3((T + 63) / 64), dim3(64), 0, st, sc, T, cb.far, cb.ok);
   sc.cell_start = cb.start;
   sc.cell_ent = cb.ent_s;
   sc.cell_ent32 = reinterpret_cast<const uint32_t*>(cb.ent_s);
@@ -361,36 +379,32 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
     if (T > 0 && hipMemsetAsync(cb.ok, 0, (size_t)T * sizeof(uint32_t), st) != hipSuccess) return -1;
     return 0;
   }
-  if (hipMemsetAsync(cb.count, 0, ((size_t)cells + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
   const long long pairs = (long long)n * T;
   CellGeo* geo = reinterpret_cast<CellGeo*>(cb.geo);
+  hipLaunchKernelGGL(cells_geo_kernel, dim3(stride_grid(std::max(pairs, (long long)cells + 1))), dim3(256), 0, st, sc, cb, T,
+                     geo, (uint32_t)cells + 1);
   if (pairs > 0) {
-    hipLaunchKernelGGL(cells_geo_kernel, dim3(stride_grid(pairs)), dim3(256), 0, st, sc, cb, T, geo);
     hipLaunchKernelGGL(cells_row_kernel<false>, dim3(row_grid(T, n)), dim3(256), 0, st, geo, T, cb, n);
   }
-  if (T > 0) hipLaunchKernelGGL(cells_total_kernel, dim3(T), dim3(256), 0, st, cb);
-  hipLaunchKernelGGL(cells_fit_kernel, dim3(1), dim3(64), 0, st, cb, T);
-  hipLaunchKernelGGL(cells_drop_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, cb, (uint32_t)cells);
+  if (T > 0) hipLaunchKernelGGL(cells_total_kernel, dim3((unsigned)cells / 256), dim3(256), 0, st, cb);
+  if (T > 0) hipLaunchKernelGGL(cells_drop_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, cb, T, (uint32_t)cells);
   size_t bytes = cb.temp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(cb.temp, bytes, cb.count, cb.start, cells + 1, st) != hipSuccess) return -1;
-  if (hipMemcpyAsync(cb.cursor, cb.start, (size_t)cells * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
-    return -1;
   if (pairs > 0)
     hipLaunchKernelGGL(cells_row_kernel<true>, dim3(row_grid(T, n)), dim3(256), 0, st, geo, T, cb, n);
-  // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its segment
+  // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its
+  // segment (the segments are the starts themselves: every start is <= cap after the drop pass)
   {
-    const uint32_t span = (uint32_t)cells + 1;
-    hipLaunchKernelGGL(cells_key_kernel, dim3((span + 255) / 256), dim3(256), 0, st, cb, (uint32_t)cells);
     size_t sbytes = cb.temp_bytes;
     const hipError_t e =
         cb.compact ? hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
                                                                  reinterpret_cast<const uint32_t*>(cb.ent),
                                                                  reinterpret_cast<uint32_t*>(cb.ent_s), (int)cb.cap, cells,
-                                                                 cb.cursor, cb.cursor + 1, 0, 16, st)
+                                                                 cb.start, cb.start + 1, 0, 16, st)
                    : hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
                                                                  reinterpret_cast<const unsigned long long*>(cb.ent),
                                                                  reinterpret_cast<unsigned long long*>(cb.ent_s), (int)cb.cap,
-                                                                 cells, cb.cursor, cb.cursor + 1, 0, 16, st);
+                                                                 cells, cb.start, cb.start + 1, 0, 16, st);
     if (e != hipSuccess) return -1;
   }
   if (env_ll("ART_DEBUG_CELLS", 0)) {  // diagnostics: the built lists' size (synchronizes the stream)

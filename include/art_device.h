@@ -107,6 +107,11 @@ ART_API int art_executed_counts(art_ctx* ctx, art_exec_counts* out);
 /* Sum of kernel times since the last call (needs ART_CTX_TIME_KERNELS); synchronizes. */
 ART_API int art_kernel_timing(art_ctx* ctx, art_kernel_times* out);
 
+/* Diagnostics (tests): the leaf order of the bound scene's BVH on the context's first device, one
+ * reference per leaf slot (type << 30 | in-type index), at most cap of them; returns the number
+ * written (the bound scene's collider count when cap allows) or a negative art error. Synchronizes. */
+ART_API int art_debug_leaf_order(art_ctx* ctx, uint32_t* out, int32_t cap);
+
 /* Context over an explicit list of HIP devices: fans of every art_schedule are sharded
  * contiguously over the list (one HIP stream, one scene copy and one set of buffers per entry).
  * An id may repeat: art_create_on({0, 0, 0}, 3, &ctx) runs the in-process multi-device split and
