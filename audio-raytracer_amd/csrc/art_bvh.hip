@@ -57,7 +57,13 @@ size_t sort_scene_temp_bytes(int n) {
     return 0;
   // (the multi-workgroup kd order scans 3 n side flags per binary level)
   if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, 3 * n) != hipSuccess) return 0;
-  return std::max(bytes, scan);
+  // (the kd order's three axis sorts as one segmented sort of 3 n keys)
+  size_t seg = 0;
+  if (hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, seg, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                  (const int*)nullptr, (int*)nullptr, 3 * n, 3, (const int*)nullptr,
+                                                  (const int*)nullptr, 0, 32) != hipSuccess)
+    return 0;
+  return std::max(std::max(bytes, scan), seg);
 }
 
 int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st);
@@ -263,6 +269,9 @@ struct KdBufs {
   int* scan;            // [3][n] exclusive scan of flag
   uint8_t* side;        // [n] by collider id
   uint32_t* keys;       // [3][n] radix keys of the centres per axis (kd_keys_kernel)
+  uint32_t* keys_s;     // [3][n] their sorted copies
+  int* vals;            // [3][n] collider ids (the sorts' values)
+  int* segs;            // [4] 0, n, 2 n, 3 n (the segmented sort's offsets)
 };
 static size_t kd_al(size_t v) { return (v + 255) & ~(size_t)255; }
 static KdBufs kd_bufs(void* base, int n) {
@@ -272,6 +281,9 @@ static KdBufs kd_bufs(void* base, int n) {
   k.cen = reinterpret_cast<float4*>(b + o); o += kd_al(16 * (size_t)n);
   k.p = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
   k.keys = reinterpret_cast<uint32_t*>(b + o); o += kd_al(12 * (size_t)n);
+  k.keys_s = reinterpret_cast<uint32_t*>(b + o); o += kd_al(12 * (size_t)n);
+  k.vals = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
+  k.segs = reinterpret_cast<int*>(b + o); o += kd_al(16);
   if (n > kKdMaxColliders) {
     k.p2 = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
     k.flag = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
@@ -283,7 +295,7 @@ static KdBufs kd_bufs(void* base, int n) {
 }
 size_t kd_scratch_bytes(int n) {
   if (n <= 0) return 0;
-  const size_t base = kd_al(16 * (size_t)n) + 2 * kd_al(12 * (size_t)n);
+  const size_t base = kd_al(16 * (size_t)n) + 4 * kd_al(12 * (size_t)n) + kd_al(16);
   return n <= kKdMaxColliders ? base : base + 3 * kd_al(12 * (size_t)n) + kd_al((size_t)n);
 }
 
@@ -292,6 +304,7 @@ size_t kd_scratch_bytes(int n) {
 // key launch per axis)
 __global__ void kd_keys_kernel(const CullRec* __restrict__ cull, int n, KdBufs k, int* __restrict__ vals) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 4) k.segs[i] = i * n;
   if (i >= n) return;
   const CullRec c = cull[i];
   float v[3] = {0.5f * (c.lox + c.hix), 0.5f * (c.loy + c.hiy), 0.5f * (c.loz + c.hiz)};
@@ -302,6 +315,7 @@ __global__ void kd_keys_kernel(const CullRec* __restrict__ cull, int n, KdBufs k
   }
   k.cen[i] = make_float4(v[0], v[1], v[2], 0.0f);
   vals[i] = i;
+  for (int a = 0; a < 3; ++a) k.vals[(size_t)a * n + i] = i;
 }
 
 __device__ __forceinline__ float kd_comp(const float4& c, int a) { return a == 0 ? c.x : (a == 1 ? c.y : c.z); }
@@ -628,6 +642,10 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
 // slot by its rank on that axis, and a stable partition of every array from ballot ranks, moved
 // through a per-wave LDS row. Writes the leaf order (perm).
 constexpr int kKdWaveLg = 6;
+static bool kd_segsort_enabled() {  // ART_KD_SEGSORT=0 (read per build): three device-wide sorts (A/B)
+  const char* e = getenv("ART_KD_SEGSORT");
+  return !(e && e[0] == '0');
+}
 static bool kd_wave_enabled() {  // ART_KD_WAVE=0 (read per build): the block passes run every level (A/B, tests)
   const char* e = getenv("ART_KD_WAVE");
   return !(e && e[0] == '0');
@@ -782,11 +800,18 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
     hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
-    for (int a = 0; a < 3; ++a) {
+    if (kd_segsort_enabled()) {  // the three axis orders in one segmented sort (stable: ties keep id order)
       size_t bytes = sb.temp_bytes;
-      if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
-                                             n, 0, 32, st) != hipSuccess)
+      if (hipcub::DeviceSegmentedRadixSort::SortPairs(sb.temp, bytes, k.keys, k.keys_s, k.vals, k.p, 3 * n, 3, k.segs,
+                                                      k.segs + 1, 0, 32, st) != hipSuccess)
         return -1;
+    } else {
+      for (int a = 0; a < 3; ++a) {
+        size_t bytes = sb.temp_bytes;
+        if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
+                                               n, 0, 32, st) != hipSuccess)
+          return -1;
+      }
     }
     if (n <= kKdMaxColliders && kd_wave_enabled()) {
       // one 1024-thread workgroup down to 512-position segments, then one 256-thread workgroup per
