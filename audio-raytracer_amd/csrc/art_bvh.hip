@@ -642,9 +642,12 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
 // slot by its rank on that axis, and a stable partition of every array from ballot ranks, moved
 // through a per-wave LDS row. Writes the leaf order (perm).
 constexpr int kKdWaveLg = 6;
-static bool kd_segsort_enabled() {  // ART_KD_SEGSORT=0 (read per build): three device-wide sorts (A/B)
+// ART_KD_SEGSORT=1 (read per build): the three axis orders as one segmented sort instead of three
+// device-wide sorts — measured slower (one 95 us launch vs 3 x 8.4 us sorts and their helper
+// launches, profiles/r04d_kd_segsort_ab.txt), kept as an experiment switch
+static bool kd_segsort_enabled() {
   const char* e = getenv("ART_KD_SEGSORT");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 static bool kd_wave_enabled() {  // ART_KD_WAVE=0 (read per build): the block passes run every level (A/B, tests)
   const char* e = getenv("ART_KD_WAVE");
@@ -800,7 +803,7 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
     hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
-    if (kd_segsort_enabled()) {  // the three axis orders in one segmented sort (stable: ties keep id order)
+    if (kd_segsort_enabled()) {  // (experiment) the three axis orders in one segmented sort (stable: ties keep id order)
       size_t bytes = sb.temp_bytes;
       if (hipcub::DeviceSegmentedRadixSort::SortPairs(sb.temp, bytes, k.keys, k.keys_s, k.vals, k.p, 3 * n, 3, k.segs,
                                                       k.segs + 1, 0, 32, st) != hipSuccess)
