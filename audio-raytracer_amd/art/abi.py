@@ -50,6 +50,7 @@ ART_CTX_TIME_KERNELS = 0x2
 ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
+ART_CTX_TIME_EACH_KERNEL = 0x200
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 # art_fan.ray_hit_ids: ColliderType (Enums/ColliderType.cs) << 30 | index in that type's array
@@ -109,7 +110,12 @@ class art_fan_layout(C.Structure):
 
 class art_kernel_times(C.Structure):
     _fields_ = [("raytrace_ms", C.c_double), ("permeate_ms", C.c_double), ("reduce_ms", C.c_double),
-                ("launches", C.c_int32), ("nearest_launches", C.c_int32), ("nearest_ms", C.c_double)]
+                ("launches", C.c_int32), ("kernel_marks_dropped", C.c_int32), ("kernel_ms", C.c_double * 4),
+                ("kernel_launches", C.c_int32 * 4)]
+
+
+# art_kernel_times.kernel_ms order (ART_KERNEL_*)
+KERNEL_FAMILIES = ("nearest_first_kernel", "echo_muffle_kernel", "vis_kernel", "muffle_kernel")
 
 
 class art_collider_sync_stats(C.Structure):

@@ -292,7 +292,9 @@ class Context:
         if rc:
             self._raise(rc)
         return {"raytrace_ms": t.raytrace_ms, "permeate_ms": t.permeate_ms, "reduce_ms": t.reduce_ms,
-                "launches": t.launches, "nearest_ms": t.nearest_ms, "nearest_launches": t.nearest_launches}
+                "launches": t.launches, "kernel_marks_dropped": t.kernel_marks_dropped,
+                "kernel_ms": {k: t.kernel_ms[i] for i, k in enumerate(abi.KERNEL_FAMILIES)},
+                "kernel_launches": {k: t.kernel_launches[i] for i, k in enumerate(abi.KERNEL_FAMILIES)}}
 
     def executed_counts(self) -> dict:
         """Work the throughput kernel executed since the last call (needs ART_CTX_COUNT_EXECUTED)."""

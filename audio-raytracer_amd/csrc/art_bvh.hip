@@ -271,7 +271,6 @@ struct KdBufs {
   uint32_t* keys;       // [3][n] radix keys of the centres per axis (kd_keys_kernel)
   uint32_t* keys_s;     // [3][n] their sorted copies
   int* vals;            // [3][n] collider ids (the sorts' values)
-  int* segs;            // [4] 0, n, 2 n, 3 n (the segmented sort's offsets)
 };
 static size_t kd_al(size_t v) { return (v + 255) & ~(size_t)255; }
 static KdBufs kd_bufs(void* base, int n) {
@@ -283,7 +282,6 @@ static KdBufs kd_bufs(void* base, int n) {
   k.keys = reinterpret_cast<uint32_t*>(b + o); o += kd_al(12 * (size_t)n);
   k.keys_s = reinterpret_cast<uint32_t*>(b + o); o += kd_al(12 * (size_t)n);
   k.vals = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
-  k.segs = reinterpret_cast<int*>(b + o); o += kd_al(16);
   if (n > kKdMaxColliders) {
     k.p2 = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
     k.flag = reinterpret_cast<int*>(b + o); o += kd_al(12 * (size_t)n);
@@ -295,7 +293,7 @@ static KdBufs kd_bufs(void* base, int n) {
 }
 size_t kd_scratch_bytes(int n) {
   if (n <= 0) return 0;
-  const size_t base = kd_al(16 * (size_t)n) + 4 * kd_al(12 * (size_t)n) + kd_al(16);
+  const size_t base = kd_al(16 * (size_t)n) + 4 * kd_al(12 * (size_t)n);
   return n <= kKdMaxColliders ? base : base + 3 * kd_al(12 * (size_t)n) + kd_al((size_t)n);
 }
 
@@ -304,7 +302,6 @@ size_t kd_scratch_bytes(int n) {
 // key launch per axis)
 __global__ void kd_keys_kernel(const CullRec* __restrict__ cull, int n, KdBufs k, int* __restrict__ vals) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 4) k.segs[i] = i * n;
   if (i >= n) return;
   const CullRec c = cull[i];
   float v[3] = {0.5f * (c.lox + c.hix), 0.5f * (c.loy + c.hiy), 0.5f * (c.loz + c.hiz)};
@@ -642,13 +639,6 @@ __global__ __launch_bounds__(NT) void kd_split_kernel(KdBufs k, int n, int lg_to
 // slot by its rank on that axis, and a stable partition of every array from ballot ranks, moved
 // through a per-wave LDS row. Writes the leaf order (perm).
 constexpr int kKdWaveLg = 6;
-// ART_KD_SEGSORT=1 (read per build): the three axis orders as one segmented sort instead of three
-// device-wide sorts — measured slower (one 95 us launch vs 3 x 8.4 us sorts and their helper
-// launches, profiles/r04d_kd_segsort_ab.txt), kept as an experiment switch
-static bool kd_segsort_enabled() {
-  const char* e = getenv("ART_KD_SEGSORT");
-  return e && e[0] == '1';
-}
 static bool kd_wave_enabled() {  // ART_KD_WAVE=0 (read per build): the block passes run every level (A/B, tests)
   const char* e = getenv("ART_KD_WAVE");
   return !(e && e[0] == '0');
@@ -803,18 +793,11 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
     hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
-    if (kd_segsort_enabled()) {  // (experiment) the three axis orders in one segmented sort (stable: ties keep id order)
+    for (int a = 0; a < 3; ++a) {  // the three axis orders (stable: ties keep id order)
       size_t bytes = sb.temp_bytes;
-      if (hipcub::DeviceSegmentedRadixSort::SortPairs(sb.temp, bytes, k.keys, k.keys_s, k.vals, k.p, 3 * n, 3, k.segs,
-                                                      k.segs + 1, 0, 32, st) != hipSuccess)
+      if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
+                                             n, 0, 32, st) != hipSuccess)
         return -1;
-    } else {
-      for (int a = 0; a < 3; ++a) {
-        size_t bytes = sb.temp_bytes;
-        if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
-                                               n, 0, 32, st) != hipSuccess)
-          return -1;
-      }
     }
     if (n <= kKdMaxColliders && kd_wave_enabled()) {
       // one 1024-thread workgroup down to 512-position segments, then one 256-thread workgroup per

@@ -45,7 +45,14 @@ static_assert(sizeof(art_dsp_params) == 24, "art_dsp_params");
 
 namespace {
 
-constexpr uint32_t kAbiVersion = (2u << 16) | 3u;  // 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1: art_exec_counts.cell_entries / muffle_fallback; 2.2: art_exec_counts.bounce_rays; 2.3: art_exec_counts.by_kernel, ART_CTX_GRAPH removed
+// ABI major.minor. A struct that grows is a major bump (a caller built against the older header
+// would be written past its end). 2.0: art_fan.ray_hit_ids, art_fan_layout.hit_ids_off; 2.1:
+// art_exec_counts.cell_entries / muffle_fallback; 2.2: art_exec_counts.bounce_rays; 2.3:
+// art_exec_counts.by_kernel (grew from 208 to 328 B), art_kernel_times.nearest_* (32 to 48 B),
+// art_debug_leaf_order, ART_CTX_GRAPH removed — a growth 2.3 should have made a major bump; 3.0:
+// art_kernel_times per kernel family (kernel_ms / kernel_launches / kernel_marks_dropped, 80 B),
+// ART_CTX_TIME_EACH_KERNEL.
+constexpr uint32_t kAbiVersion = (3u << 16) | 0u;
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
@@ -148,17 +155,9 @@ struct Device {
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   SideStream echo;  // the echo visibility beside the muffle kernel
-  // fan lanes: lane j > 0 runs its share of the frame's fans on its own stream (and echo side
-  // stream), forked from and joined to the launch stream, so one lane's traversal tails overlap
-  // the other lane's kernels; lane 0 is the launch stream with `echo`
-  struct Lane {
-    hipStream_t st = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    SideStream echo;
-  };
-  Lane lanes[kMaxFanLanes];
   std::vector<hipEvent_t> ev_pool;  // timing events (start/stop pairs)
-  std::vector<std::pair<int, size_t>> ev_used;  // (kernel kind, pool index of start)
+  std::vector<std::pair<int, size_t>> ev_used;  // (EvKind, pool index of start)
+  int marks_dropped = 0;                          // per-kernel marks past the pairs (art_kernel_timing)
 };
 
 }  // namespace
@@ -654,6 +653,10 @@ int check_resident(art_ctx* c, const art_frame_desc* d) {
   return ART_OK;
 }
 
+// What an event pair of Device::ev_used times: a stage of the frame, or one kernel of the raytrace
+// stage (kEvKernel0 + MarkKind, ART_CTX_TIME_EACH_KERNEL).
+enum EvKind { kEvRaytrace = 0, kEvPermeate = 1, kEvReduce = 2, kEvKernel0 = 3 };
+
 hipEvent_t pool_event(Device& dv, size_t i) {
   while (dv.ev_pool.size() <= i) {
     hipEvent_t e;
@@ -661,16 +664,6 @@ hipEvent_t pool_event(Device& dv, size_t i) {
     dv.ev_pool.push_back(e);
   }
   return dv.ev_pool[i];
-}
-
-// Fan lanes per frame (ART_FAN_LANES, 1..kMaxFanLanes; counting frames use 1).
-int fan_lanes() {
-  static const int n = [] {
-    const char* e = getenv("ART_FAN_LANES");
-    const int v = e ? atoi(e) : kDefaultFanLanes;
-    return std::max(1, std::min(v, kMaxFanLanes));
-  }();
-  return n;
 }
 
 // Enqueue the kernels of one frame for fan_count fans on stream st.
@@ -688,7 +681,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   // muffle accumulators, then (16-B aligned) the visibility pair counters: cleared by the first
   // nearest_first_kernel of each fast-path chunk, by one memset before the reference-order kernel
   const size_t acc_words = ((size_t)fan_count * f.TC * f.T + 3) & ~(size_t)3;
-  const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16 * kMaxFanLanes;  // + 4 pair counters per lane
+  const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16;  // + 4 pair counters
   if (!dv.acc.reserve(acc_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   uint32_t* acc = static_cast<uint32_t*>(dv.acc.p);
   uint32_t* pair_count = acc + acc_words;
@@ -728,24 +721,10 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       HIP_TRY(c, hipEventCreateWithFlags(&dv.echo.join, hipEventDisableTiming));
     }
   }
-  const int nlanes = fast ? std::min(fan_lanes(), fan_count) : 1;
-  const int lane_fans = (fan_count + nlanes - 1) / nlanes;
-  size_t lane_pair_bytes = 0;
   if (fast) {
-    for (int j = 1; j < nlanes; ++j) {
-      Device::Lane& ln = dv.lanes[j];
-      if (ln.st) continue;
-      HIP_TRY(c, hipStreamCreateWithFlags(&ln.st, hipStreamNonBlocking));
-      HIP_TRY(c, hipEventCreateWithFlags(&ln.fork, hipEventDisableTiming));
-      HIP_TRY(c, hipEventCreateWithFlags(&ln.join, hipEventDisableTiming));
-      HIP_TRY(c, hipStreamCreateWithFlags(&ln.echo.st, hipStreamNonBlocking));
-      HIP_TRY(c, hipEventCreateWithFlags(&ln.echo.fork, hipEventDisableTiming));
-      HIP_TRY(c, hipEventCreateWithFlags(&ln.echo.join, hipEventDisableTiming));
-    }
     FrameParams fps = fp;
-    fps.S = std::min(lane_fans, chunk);
-    lane_pair_bytes = (fast_pair_bytes(fps) + 255) & ~(size_t)255;
-    if (!dv.pairs.reserve(lane_pair_bytes * nlanes)) return fail(c, ART_E_NOMEM, "device allocation failed");
+    fps.S = std::min(fan_count, chunk);
+    if (!dv.pairs.reserve(fast_pair_bytes(fps))) return fail(c, ART_E_NOMEM, "device allocation failed");
   }
   // The permeation job (read-only scene and origins, writes only the fans' permeation sections)
   // runs on the side stream concurrently with the raytrace stage, whose kernels leave CUs idle in
@@ -774,7 +753,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     drain.side = dv.side;
     HIP_TRY(c, hipEventRecord(pfork, st));
     HIP_TRY(c, hipStreamWaitEvent(dv.side, pfork, 0));
-    size_t ti = timing ? tstart(1, dv.side) : 0;
+    size_t ti = timing ? tstart(kEvPermeate, dv.side) : 0;
     (perm_bvh ? launch_permeate : launch_permeate_sweep)(dv.sc, fp, f.L, d_origins, d_block, slot_batch, dv.side);
     if (timing) tstop(ti, dv.side);
     HIP_TRY(c, hipGetLastError());
@@ -782,7 +761,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   }
 
   if (f.stages & ART_STAGE_RAYTRACE) {
-    size_t ti = timing ? tstart(0, st) : 0;
+    size_t ti = timing ? tstart(kEvRaytrace, st) : 0;
     // The counting variant sweeps colliders in exact reference order per lane (its per-lane
     // test counts are the metric's numerator); the throughput kernel splits the sweep over waves.
     const int* order = reinterpret_cast<const int*>(raw + f.off_order);
@@ -793,44 +772,35 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
       FrameParams fpx = fp;
       fpx.exec = exec_ctr;
       // The pair arrays index pairs with 32-bit slots (below 2^31) and the echo outputs with 32-bit
-      // half offsets into the block: larger frames run as consecutive fan chunks on a lane's
-      // stream (the lane's pair buffer and counters are reused, the muffle accumulators offset per
-      // chunk). Lanes > 0 fork from st before any lane's kernels and join back before the reduce job.
-      for (int j = 1; j < nlanes; ++j) {
-        HIP_TRY(c, hipEventRecord(dv.lanes[j].fork, st));
-        HIP_TRY(c, hipStreamWaitEvent(dv.lanes[j].st, dv.lanes[j].fork, 0));
-      }
-      // nearest-kernel marks (timed frames): pool pairs after the stage's own, kept for those recorded
-      NearestMarks marks;
+      // half offsets into the block: larger frames run as consecutive fan chunks on st (the pair
+      // buffer and counters are reused, the muffle accumulators offset per chunk).
+      // per-kernel marks (ART_CTX_TIME_EACH_KERNEL): pool pairs after the stage's own, kept for
+      // those recorded; a frame has at most 3H + 2 stage kernels per fan chunk
+      KernelMarks marks;
       std::vector<hipEvent_t> mev;
-      if (timing) {
+      std::vector<int> mkind;
+      if (timing && (c->flags & ART_CTX_TIME_EACH_KERNEL)) {
         const size_t base = dv.ev_used.size() * 2;
-        marks.cap = std::min(f.H * ((lane_fans + chunk - 1) / chunk), 64);
+        marks.cap = (3 * f.H + 2) * ((fan_count + chunk - 1) / chunk);
         for (int k = 0; k < 2 * marks.cap; ++k) {
           hipEvent_t e = pool_event(dv, base + k);
           if (!e) { marks.cap = k / 2; break; }
           mev.push_back(e);
         }
+        mkind.assign((size_t)marks.cap, 0);
         marks.ev = mev.data();
+        marks.kind = mkind.data();
       }
-      for (int j = 0; j < nlanes; ++j) {
-        const int l0 = std::min(fan_count, j * lane_fans), l1 = std::min(fan_count, l0 + lane_fans);
-        Device::Lane& ln = dv.lanes[j];
-        hipStream_t ls = j == 0 ? st : ln.st;
-        void* pairs = static_cast<uint8_t*>(dv.pairs.p) + (size_t)j * lane_pair_bytes;
-        for (int b0 = l0; b0 < l1; b0 += chunk) {
-          FrameParams fpc = fpx;
-          fpc.S = std::min(chunk, l1 - b0);
-          launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
-                               acc + (size_t)b0 * f.TC * f.T, order, pairs, pair_count + 4 * j, ls,
-                               j == 0 ? echo : ln.echo, j == 0 && timing ? &marks : nullptr);
-        }
-        if (j > 0) {
-          HIP_TRY(c, hipEventRecord(ln.join, ls));
-          HIP_TRY(c, hipStreamWaitEvent(st, ln.join, 0));
-        }
+      for (int b0 = 0; b0 < fan_count; b0 += chunk) {
+        FrameParams fpc = fpx;
+        fpc.S = std::min(chunk, fan_count - b0);
+        launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
+                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, echo,
+                             marks.cap ? &marks : nullptr);
       }
-      for (int k = 0; k < marks.used; ++k) dv.ev_used.push_back({3, dv.ev_used.size() * 2});  // = base + 2 k
+      for (int k = 0; k < marks.used; ++k)  // pool index base + 2 k
+        dv.ev_used.push_back({kEvKernel0 + mkind[(size_t)k], dv.ev_used.size() * 2});
+      dv.marks_dropped += marks.dropped;
     }
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
@@ -840,7 +810,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     drain.side = nullptr;  // joined: stream order covers it from here
   }
   if ((f.stages & ART_STAGE_PERMEATE) && !overlap) {
-    size_t ti = timing ? tstart(1, st) : 0;
+    size_t ti = timing ? tstart(kEvPermeate, st) : 0;
     (perm_bvh ? launch_permeate : launch_permeate_sweep)(dv.sc, fp, f.L, d_origins, d_block, slot_batch, st);
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
@@ -850,7 +820,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
     }
   }
   if (f.stages & (ART_STAGE_RAYTRACE | ART_STAGE_REDUCE)) {
-    size_t ti = timing ? tstart(2, st) : 0;
+    size_t ti = timing ? tstart(kEvReduce, st) : 0;
     launch_reduce(dv.sc, fp, f.L, d_block, acc, muffle_reset, st);
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
@@ -1019,14 +989,6 @@ ART_API void art_destroy(art_ctx* c) {
     if (dv.echo.fork) (void)hipEventDestroy(dv.echo.fork);
     if (dv.echo.join) (void)hipEventDestroy(dv.echo.join);
     if (dv.echo.st) (void)hipStreamDestroy(dv.echo.st);
-    for (Device::Lane& ln : dv.lanes) {
-      for (hipStream_t q : {ln.st, ln.echo.st})
-        if (q) (void)hipStreamSynchronize(q);
-      for (hipEvent_t e : {ln.fork, ln.join, ln.echo.fork, ln.echo.join})
-        if (e) (void)hipEventDestroy(e);
-      for (hipStream_t q : {ln.st, ln.echo.st})
-        if (q) (void)hipStreamDestroy(q);
-    }
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
   }
   c->h_in.release();
@@ -1039,9 +1001,10 @@ ART_API void art_destroy(art_ctx* c) {
 ART_API const char* art_last_error(const art_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 // Timing events a device keeps ready once ART_CTX_TIME_KERNELS is first set: the pool grows on the
-// host here, before any timed frame, so a timed frame never creates events (hipEventCreate inside a
-// caller's timed loop; 8 events per timed frame, 64 frames between art_kernel_timing calls).
-constexpr size_t kTimingEventsReserve = 512;
+// host here, before any timed frame, so a timed frame of up to 5 bounces never creates events
+// (hipEventCreate inside a caller's timed loop): 6 stage events + 2 (3H + 2) per-kernel events
+// (ART_CTX_TIME_EACH_KERNEL) per frame, 64 frames between art_kernel_timing calls.
+constexpr size_t kTimingEventsReserve = 64 * (6 + 2 * (3 * 5 + 2));
 
 ART_API int art_set_flags(art_ctx* c, uint32_t flags) {
   if (!c) return ART_E_INVALID;
@@ -1161,9 +1124,6 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
         (void)hipStreamSynchronize(e.stream);
         if (e.side) (void)hipStreamSynchronize(e.side);  // a forked stage may not have joined
         if (e.echo.st) (void)hipStreamSynchronize(e.echo.st);
-        for (Device::Lane& ln : e.lanes)
-          for (hipStream_t q : {ln.st, ln.echo.st})
-            if (q) (void)hipStreamSynchronize(q);
       }
       return rc;
     }
@@ -1381,13 +1341,18 @@ ART_API int art_kernel_timing(art_ctx* c, art_kernel_times* out) {
       HIP_TRY(c, hipEventSynchronize(b));
       float ms = 0.0f;
       HIP_TRY(c, hipEventElapsedTime(&ms, a, b));
-      if (u.first == 0) { out->raytrace_ms += ms; frames++; }
-      else if (u.first == 1) out->permeate_ms += ms;
-      else if (u.first == 3) { out->nearest_ms += ms; out->nearest_launches++; }
-      else out->reduce_ms += ms;
+      if (u.first == kEvRaytrace) { out->raytrace_ms += ms; frames++; }
+      else if (u.first == kEvPermeate) out->permeate_ms += ms;
+      else if (u.first == kEvReduce) out->reduce_ms += ms;
+      else if (u.first - kEvKernel0 < kMarkKinds) {
+        out->kernel_ms[u.first - kEvKernel0] += ms;
+        out->kernel_launches[u.first - kEvKernel0]++;
+      }
     }
     dv.ev_used.clear();
     out->launches += frames;
+    out->kernel_marks_dropped += dv.marks_dropped;
+    dv.marks_dropped = 0;
   }
   return ART_OK;
 }

@@ -230,21 +230,23 @@ int fast_fans_per_launch(int R, int H, int T, int TC, uint32_t stride);
 // (+ the bounce's echo vis_kernel), then muffle_kernel. Any target count, every DevScene with a BVH
 // and cell lists. echo_st (optional, with two events): the echo traversals run there, beside the
 // next bounces and the muffle kernel on st, joined at the end.
-constexpr int kMaxFanLanes = 4;      // fan lanes per device (art_capi.cpp)
-constexpr int kDefaultFanLanes = 1;
 struct SideStream {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
-// Timing marks (ART_CTX_TIME_KERNELS): event pairs recorded on the launch stream around each
-// nearest_first_kernel launch, while pairs are left (art_kernel_times.nearest_ms).
-struct NearestMarks {
+// Per-kernel timing marks (ART_CTX_TIME_EACH_KERNEL): an event pair recorded around each kernel of
+// the raytrace stage on the stream it is launched on, with its kernel family (art_kernel_times
+// kernel_ms order). Marks stop being recorded once the pairs run out (used counts those recorded).
+enum MarkKind { kMarkNearest = 0, kMarkEchoMuffle = 1, kMarkEcho = 2, kMarkMuffle = 3, kMarkKinds = 4 };
+struct KernelMarks {
   hipEvent_t* ev = nullptr;  // [2 * cap]
+  int* kind = nullptr;       // [cap]
   int cap = 0, used = 0;
+  int dropped = 0;           // launches that found no pair left (their family's time is then incomplete)
 };
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf,
-                          uint32_t* pair_count, hipStream_t st, const SideStream& echo, NearestMarks* marks = nullptr);
+                          uint32_t* pair_count, hipStream_t st, const SideStream& echo, KernelMarks* marks = nullptr);
 void launch_permeate(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                      uint8_t* block, const int2* slot_batch, hipStream_t st);
 // (the collider sweep of every loss ray, art_kernels.hip: the reference-order and counting frames)

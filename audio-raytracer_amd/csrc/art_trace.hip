@@ -121,10 +121,6 @@ __device__ __forceinline__ uint32_t quad_min_u32(uint32_t v) {
   v = min(v, (uint32_t)quad_perm<kQuadXor1>((int)v));
   return min(v, (uint32_t)quad_perm<kQuadXor2>((int)v));
 }
-__device__ __forceinline__ int quad_max_i32(int v) {
-  v = max(v, quad_perm<kQuadXor1>(v));
-  return max(v, quad_perm<kQuadXor2>(v));
-}
 
 // The BVH node and leaf arrays as buffer resources (wave-uniform bases, 32-bit lane offsets).
 struct BvhRes {
@@ -162,11 +158,7 @@ __device__ __forceinline__ void quad_descend(bool enter, float en, bool force, i
                  k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
   const int rank = (int)(k1 < key) + (int)(k2 < key) + (int)(k3 < key);
   const uint32_t kmin = min(min(key, k1), min(k2, k3));
-#if ART_NENT_BALLOT
-  const int nent = __popc((uint32_t)(__ballot(enter) >> (__lane_id() & ~3)) & 0xFu);
-#else
-  const int nent = quad_max_i32(enter ? rank + 1 : 0);
-#endif
+  const int nent = __popc((uint32_t)(__ballot(enter) >> (__lane_id() & ~3)) & 0xFu);  // entered children (one ballot)
   if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
   if (nent) {
     g = c0 + (int)(kmin & 3u);
@@ -250,14 +242,6 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #endif
 #ifndef ART_VIS_STEAL_MIN_IDLE
 #define ART_VIS_STEAL_MIN_IDLE 2
-#endif
-#ifndef ART_VIS_PRIO
-#define ART_VIS_PRIO 0
-#endif
-// Entered children counted by one ballot instead of a quad DPP maximum (round 4, 1-3 % of the
-// nearest kernel)
-#ifndef ART_NENT_BALLOT
-#define ART_NENT_BALLOT 1
 #endif
 constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
 
@@ -1055,13 +1039,6 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   for (;;) {
     const unsigned long long act = __ballot(g >= 0) & kQuad0;
     if (!act) break;
-    if (ART_VIS_PRIO) {  // wave priority by unfinished segments, as in the nearest traversal (A/B knob)
-      const int na = __popcll(act);
-      if (na > 12) __builtin_amdgcn_s_setprio(3);
-      else if (na > 8) __builtin_amdgcn_s_setprio(2);
-      else if (na > 4) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
     const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
     if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
       int l4 = lane & ~3;
@@ -1143,41 +1120,6 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
 
 // The echo traversal: one 64-pair batch per workgroup. EX: count the executed tests (fp.exec);
 // without it the counters compile out. 8 waves per SIMD.
-#ifdef ART_FUSE_ECHO
-// Experiment build only (the round-3 fused variant rebuilt): one-hit frames with one
-// batch slot and no hit outputs trace each wave's 16 echo rays right after their nearest hits, in
-// the same kernel (the muffle rays then run alone in muffle_kernel<..., HM>).
-#ifndef ART_FUSE_WAVES
-#define ART_FUSE_WAVES 8
-#endif
-template <bool OBB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ART_FUSE_WAVES))) void nearest_echo_kernel(
-    DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order, int2* __restrict__ hits,
-    uint32_t* __restrict__ zero, uint32_t nzero, uint32_t* __restrict__ counters, VisPairs vp, uint8_t* __restrict__ block,
-    EchoFromHits eh) {
-  __shared__ uint32_t s_stk[kBvhStack * 64];
-  __shared__ int s_bound[64];
-  __shared__ unsigned long long s_key[64];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int nrb = (fp.R + 63) >> 6;
-  const int g = blockIdx.x;
-  const int rr = 16 * w + (lane >> 2);
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
-  if (counters && blockIdx.x == 0 && threadIdx.x < 4) counters[threadIdx.x] = 0u;
-  const int fan = g / nrb;
-  const int slot = (g - fan * nrb) * 64 + rr;
-  const bool alive = slot < fp.R;
-  const int ray = alive ? ray_order[slot] : 0;
-  float best;
-  int code;
-  quad_nearest_core<false, OBB>(sc, make_seg(load3(origins, fan), load_dir(sc.dirs, ray)), alive, lane, s_stk + rr * kBvhStack,
-                                s_bound + 16 * w, s_key + 16 * w, best, code, nullptr);
-  if ((lane & 3) == 0) hits[(size_t)g * 64 + rr] = make_int2(__float_as_int(best), code);
-  __threadfence_block();  // (the echo traversal below reads this wave's own hit records)
-  vis_quad_body<OBB, true>(sc, vp, nullptr, nullptr, (uint32_t)g, s_stk, nullptr, -1, block, eh);
-}
-#endif
-
 template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEchoWaves<EX, OBB>)))
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, unsigned long long* ex,
@@ -1610,6 +1552,10 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
     // rank the kept terms by order code (the four lanes of the quad share the entries), then sum
     // them serially in that order in lane 0
     const bool fits = n <= kLossCap;
+    // (lanes of the quad read each other's LDS entries: order the leaf loop's writes before the
+    // ranking and the ranks' scatter before the sum, as kd_wave_kernel does)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     if (valid && fits) {
       for (int i = qd; i < n; i += 4) {
         const uint32_t ci = s_code[wq][i];
@@ -1617,6 +1563,10 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
         for (int j = 0; j < n; ++j) rank += s_code[wq][j] < ci ? 1 : 0;
         s_sorted[wq][rank] = s_term[wq][i];
       }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (valid && fits) {
       float sum = 0.0f;
       for (int i = 0; i < n; ++i) sum += s_sorted[wq][i];
       if (qd == 0) ppr[slot * T + t] = (float)fp.R * fp.perm_strength - sum;  // :260
@@ -1692,9 +1642,19 @@ int fast_fans_per_launch(int R, int H, int T, int TC, uint32_t stride) {
   return (int)std::max(1ull, n);
 }
 
+// An event pair around one launch (marks may be null); a launch past the pairs is counted as dropped.
+template <class F>
+static void marked(KernelMarks* marks, int kind, hipStream_t s, F&& launch) {
+  const bool m = marks && marks->used < marks->cap;
+  if (marks && !m) marks->dropped++;
+  if (m) { marks->kind[marks->used] = kind; (void)hipEventRecord(marks->ev[2 * marks->used], s); }
+  launch();
+  if (m) { (void)hipEventRecord(marks->ev[2 * marks->used + 1], s); marks->used++; }
+}
+
 void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLayout& L, const float* origins,
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf, uint32_t* pair_count,
-                          hipStream_t st, const SideStream& echo, NearestMarks* marks) {
+                          hipStream_t st, const SideStream& echo, KernelMarks* marks) {
   if (fp.S == 0) return;
   PairBufs pb = pair_bufs(pair_buf, fp);
   const unsigned groups = (unsigned)((size_t)fp.S * ((fp.R + 63) / 64));
@@ -1733,13 +1693,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     else { if (obb) ART_VIS(S_, BLOCKS_, B_, false, true, HM_); else ART_VIS(S_, BLOCKS_, B_, false, false, HM_); }       \
   } while (0)
   // One-hit frames with one batch slot, no hit outputs (HM2): no path kernel at all; the echo
-  // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too. Also
-  // frames past one round of echo waves, which have no path kernel to starve (config 4: 1.684 ->
-  // 1.660 ms/step; ART_HM2_ANY=0 restores the path-kernel plan for them)
-#ifndef ART_HM2_ANY
-#define ART_HM2_ANY 1
-#endif
-  const bool hm2 = (hm || (ART_HM2_ANY && split && !multi && fp.TC == 1)) && !L.has_hits;
+  // traversal writes the misses' reset and the muffle kernel starts from the nearest hits too, at
+  // any frame size (no path kernel is left to starve; config 4 1.684 -> 1.660 ms/step)
+  const bool hm2 = split && !multi && fp.TC == 1 && !L.has_hits;
   // ... and the two as one launch on st (echo_muffle_kernel)
   const bool fused = hm2;
   eh.no_path = hm2 ? 1 : 0;
@@ -1771,29 +1727,15 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
 #define ART_NEAREST(EX_, OBB_, F_)                                                                                  \
   hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order,      \
                      pb.pre, pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr, L, block, pb.vp)
-    const bool mark = marks && marks->used < marks->cap;
-    if (mark) (void)hipEventRecord(marks->ev[2 * marks->used], st);
-#ifdef ART_FUSE_ECHO
-    if (hm2 && !fp.exec) {  // (experiment: nearest + echo in one kernel, then the muffle rays alone)
-      if (obb)
-        hipLaunchKernelGGL((nearest_echo_kernel<true>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre,
-                           muffle_acc, nacc, pair_count, pb.vp, block, eh);
-      else
-        hipLaunchKernelGGL((nearest_echo_kernel<false>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order, pb.pre,
-                           muffle_acc, nacc, pair_count, pb.vp, block, eh);
-      if (mark) (void)hipEventRecord(marks->ev[2 * marks->used++ + 1], st);
-      ART_MUFFLE_ANY(st);
-      return;
-    }
-#endif
-    if (fold) {
-      if (fp.exec) { if (obb) ART_NEAREST(true, true, true); else ART_NEAREST(true, false, true); }
-      else { if (obb) ART_NEAREST(false, true, true); else ART_NEAREST(false, false, true); }
-    } else {
-      if (fp.exec) { if (obb) ART_NEAREST(true, true, false); else ART_NEAREST(true, false, false); }
-      else { if (obb) ART_NEAREST(false, true, false); else ART_NEAREST(false, false, false); }
-    }
-    if (mark) (void)hipEventRecord(marks->ev[2 * marks->used++ + 1], st);
+    marked(marks, kMarkNearest, st, [&] {
+      if (fold) {
+        if (fp.exec) { if (obb) ART_NEAREST(true, true, true); else ART_NEAREST(true, false, true); }
+        else { if (obb) ART_NEAREST(false, true, true); else ART_NEAREST(false, false, true); }
+      } else {
+        if (fp.exec) { if (obb) ART_NEAREST(true, true, false); else ART_NEAREST(true, false, false); }
+        else { if (obb) ART_NEAREST(false, true, false); else ART_NEAREST(false, false, false); }
+      }
+    });
 #undef ART_NEAREST
     hipStream_t pst = st;
     if (hm && !hm2) {  // (HM2 forks the muffle rays below)
@@ -1811,33 +1753,35 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     if (per_bounce) {  // this bounce's echoes (at most one per ray slot: `groups` batches)
       (void)hipEventRecord(echo.fork, st);
       (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-      ART_VIS_ANY(echo.st, groups, k, false);
+      marked(marks, kMarkEcho, echo.st, [&] { ART_VIS_ANY(echo.st, groups, k, false); });
     }
   }
   if (per_bounce) {
-    ART_MUFFLE_ANY(st);  // the bounces' echoes are already on the side stream
+    marked(marks, kMarkMuffle, st, [&] { ART_MUFFLE_ANY(st); });  // the bounces' echoes are already on the side stream
   } else if (fused) {
 #define ART_ECHO_MUFFLE(EX_, OBB_)                                                                                    \
   hipLaunchKernelGGL((echo_muffle_kernel<EX_, OBB_>), dim3(groups + mblocks * mt), dim3(256), 0, st, sc, fp, pb.vp,   \
                      pair_count, EX_ ? fp.exec : nullptr, block, eh, muffle_acc, groups, mblocks, (int)mt)
-    if (fp.exec) { if (obb) ART_ECHO_MUFFLE(true, true); else ART_ECHO_MUFFLE(true, false); }
-    else { if (obb) ART_ECHO_MUFFLE(false, true); else ART_ECHO_MUFFLE(false, false); }
+    marked(marks, kMarkEchoMuffle, st, [&] {
+      if (fp.exec) { if (obb) ART_ECHO_MUFFLE(true, true); else ART_ECHO_MUFFLE(true, false); }
+      else { if (obb) ART_ECHO_MUFFLE(false, true); else ART_ECHO_MUFFLE(false, false); }
+    });
 #undef ART_ECHO_MUFFLE
   } else if (hm) {
     if (hm2) {  // no path kernel: fork the muffle rays here
       (void)hipEventRecord(echo.fork, st);
       (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
     }
-    ART_MUFFLE_ANY(echo.st);           // after the path kernel there (HM2: the only kernel there)
-    ART_VIS_ANY(st, groups, -1, true);  // one 64-ray group per workgroup
+    marked(marks, kMarkMuffle, echo.st, [&] { ART_MUFFLE_ANY(echo.st); });  // after the path kernel there
+    marked(marks, kMarkEcho, st, [&] { ART_VIS_ANY(st, groups, -1, true); });  // one 64-ray group per workgroup
   } else if (split) {
     (void)hipEventRecord(echo.fork, st);
     (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
-    ART_MUFFLE_ANY(echo.st);
-    ART_VIS_ANY(st, eb, -1, false);
+    marked(marks, kMarkMuffle, echo.st, [&] { ART_MUFFLE_ANY(echo.st); });
+    marked(marks, kMarkEcho, st, [&] { ART_VIS_ANY(st, eb, -1, false); });
   } else {
-    ART_VIS_ANY(st, eb, -1, false);
-    ART_MUFFLE_ANY(st);
+    marked(marks, kMarkEcho, st, [&] { ART_VIS_ANY(st, eb, -1, false); });
+    marked(marks, kMarkMuffle, st, [&] { ART_MUFFLE_ANY(st); });
   }
 #undef ART_MUFFLE_ANY
 #undef ART_MUFFLE

@@ -43,6 +43,7 @@ FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md "Peak FP32 (vector)"
 # one non-FMA wave64 VALU op issues over 2 cycles per SIMD-32 (MI355X_MICROARCH.md:54, :473):
 # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-op/s (SURVEY.md 8(d)'s 64 lanes/CU/clk undercounts 2x)
 SINGLE_ISSUE_TLOPS = 78.6
+SINGLE_ISSUE_TLOPS_64 = 39.3   # 256 CU x 64 lanes/clk x 2.4 GHz (SURVEY.md 8(d)'s figure), reported beside it
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW" (spec)
 
 
@@ -382,15 +383,20 @@ def read_traffic(cfg_index):
             f"PMC pass on this build (lib sha256 {t['lib_sha256'][:12]})")
 
 
-def stage_kernels(cfg, S, has_obb):
+def stage_kernels(cfg, thread_count, has_obb):
     """The kernels of the timed raytrace stage as launch_raytrace_fast (csrc/art_trace.hip) picks
     them for this frame shape (no hit outputs, as the bench launches it)."""
     obb = "true" if has_obb else "false"
-    if cfg.H > 1:  # one batch slot, no hit outputs: the path kernel's work runs in the nearest kernel (FOLD)
+    if cfg.H > 1 and thread_count == 1:  # one batch slot, no hit outputs: the path kernel's work folds into the nearest kernel
         return (f"per bounce: nearest_first_kernel<false, {obb}, true> (path epilogue folded in), that bounce's echo "
                 f"vis_kernel<false, {obb}, false> on the side stream; then muffle_kernel<false, {obb}, false>")
-    # one-hit frames, one batch slot, no hit outputs (any size): echo + muffle from the nearest hits, one launch
-    return f"nearest_first_kernel<false, {obb}, false> -> echo_muffle_kernel<false, {obb}> (one stream, no path kernel)"
+    if cfg.H > 1:
+        return (f"per bounce: nearest_first_kernel<false, {obb}, false> -> path_kernel<false, true>, that bounce's echo "
+                f"vis_kernel<false, {obb}, false> on the side stream; then muffle_kernel<false, {obb}, false>")
+    if thread_count == 1:  # one-hit frames, one batch slot, no hit outputs (any size): echo + muffle from the nearest hits
+        return f"nearest_first_kernel<false, {obb}, false> -> echo_muffle_kernel<false, {obb}> (one stream, no path kernel)"
+    return (f"nearest_first_kernel<false, {obb}, false> -> path_kernel<false, false> -> echo vis_kernel<false, {obb}, false>, "
+            f"muffle_kernel<false, {obb}, false> on the side stream")
 
 
 def jitter_records(rng, recs, scale):
@@ -578,20 +584,10 @@ def main():
     tests_rank = sum(counts.values())
     bf_ops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
 
-    # the all-gather alone, timed with HIP events on the launch stream around the collective of
-    # every 8th of the first 512 timed steps (BASELINE.md cfg 4: "all-gather time")
-    ag = {"ms": 0.0, "n": 0, "events": []}
-
-    def step(timed=False):
+    def step():
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
         if world > 1:
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
             art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
-            if timed:
-                e1.record(stream)
-                ag["events"].append((e0, e1))
 
     torch.cuda.synchronize()
     for _ in range(a.warmup):
@@ -607,33 +603,47 @@ def main():
         steps = int(min(5000, max(20, 1.5 / max(per, 1e-6))))
         if world > 1:
             steps = int(allreduce(steps, torch.int64, dist.ReduceOp.MAX))
-    # Kernel durations come from HIP events on the launch stream around the stages of every 8th
-    # timed step (event records between launches cost a few µs of GPU idle each; sampling keeps
-    # that out of the other steps)
-    # (the first switch to ART_CTX_TIME_KERNELS creates the context's timing events on the host, here,
-    # outside the timed region; at most 64 sampled steps keep within them)
-    ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
-    ctx.set_flags(0)
-    ctx.kernel_timing()  # reset
+    # The timed region: K frames and nothing else between them (no event records, each of which
+    # costs a few us of GPU idle: kernel durations are measured in the passes after it).
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        sample = i % 8 == 0 and i < 8 * 64
-        if sample:
-            ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
-        step(timed=sample)
-        if sample:
-            ctx.set_flags(0)
+    for _ in range(steps):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+
+    # Kernel durations: untimed passes of the same launches after the timed region, HIP events on
+    # the streams the kernels run on. Pass 1: the frame's stages only (raytrace stage, permeation
+    # job, reduce: 6 events per frame). Pass 2: also every kernel of the raytrace stage
+    # (ART_CTX_TIME_EACH_KERNEL: two more events per launch, so pass 2's stage times are not used).
+    n_pass = 64
+    ctx.set_flags(abi.ART_CTX_TIME_KERNELS)
+    ctx.kernel_timing()  # reset
+    for _ in range(n_pass):
+        ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
     ktimes = ctx.kernel_timing()
+    ctx.set_flags(abi.ART_CTX_TIME_KERNELS | abi.ART_CTX_TIME_EACH_KERNEL)
+    for _ in range(n_pass):
+        ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+    keach = ctx.kernel_timing()
+    ctx.set_flags(0)
+    # the all-gather alone: HIP events on the launch stream around the collective of n_pass frames
     allgather_ms = None
-    if ag["events"]:
-        allgather_ms = sum(e0.elapsed_time(e1) for e0, e1 in ag["events"]) / len(ag["events"])
+    if world > 1:
+        evs = []
+        for _ in range(n_pass):
+            ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
+            e1.record(stream)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        allgather_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
         allgather_ms = allreduce(allgather_ms, torch.float64, dist.ReduceOp.MAX)
     # work the kernels actually executed in one frame (broad phase: far fewer exact tests)
     ctx.set_flags(abi.ART_CTX_COUNT_EXECUTED)
@@ -684,17 +694,37 @@ def main():
         return (b["sphere"] * OPS["rt_sphere"] + b["aabb"] * OPS["rt_aabb"] + b["obb"] * OPS["rt_obb"] +
                 b["cull_box"] * CULL_OPS["cull_box"] + b["cell_entries"] * CULL_OPS["cell_entries"]) / ex_launches
     by_kernel_ops = {k: kernel_ops(k) for k in abi.EXEC_KERNELS}
-    # the dominant kernel: nearest_first_kernel, timed live by HIP events around its launches on the
-    # launch stream (art_kernel_times.nearest_ms, every 8th of the first 512 timed steps)
-    near_ms = ktimes["nearest_ms"] / n_rt
-    near_tflops = by_kernel_ops["nearest"] / (near_ms * 1e-3) / 1e12 if near_ms > 0 else 0.0
+    # Every kernel family of the raytrace stage: its duration per frame (pass 2's HIP events around
+    # each launch, on the stream it runs on) and the ops it executed per frame; the roofline line is
+    # the family with the longest measured time per frame (the dominant kernel), the others beside it.
+    fam_ops = {"nearest_first_kernel": by_kernel_ops["nearest"],
+               "echo_muffle_kernel": by_kernel_ops["echo"] + by_kernel_ops["muffle"],
+               "vis_kernel": by_kernel_ops["echo"], "muffle_kernel": by_kernel_ops["muffle"]}
+    obb_s = "true" if scene.obbs.size > 0 else "false"
+    fam_inst = {"nearest_first_kernel": f"nearest_first_kernel<false, {obb_s}, {'true' if cfg.H > 1 else 'false'}>",
+                "echo_muffle_kernel": f"echo_muffle_kernel<false, {obb_s}>",
+                "vis_kernel": f"vis_kernel<false, {obb_s}, false>", "muffle_kernel": f"muffle_kernel<false, {obb_s}, false>"}
+    traffic, traffic_by_kernel, traffic_note = read_traffic(cfg.index)
+    n_each = max(1, keach["launches"])
+    kernels = {}
+    for fam in abi.KERNEL_FAMILIES:
+        n_l = keach["kernel_launches"][fam]
+        if n_l == 0:
+            continue
+        k_ms = keach["kernel_ms"][fam] / n_each  # per frame (all its launches)
+        tf = fam_ops[fam] / (k_ms * 1e-3) / 1e12 if k_ms > 0 else 0.0
+        kernels[fam] = {"instantiation": fam_inst[fam], "ms_per_frame": k_ms, "launches_per_frame": n_l / n_each,
+                        "ms_per_launch": keach["kernel_ms"][fam] / n_l, "ops_per_frame": fam_ops[fam],
+                        "achieved": tf, "frac": tf / FP32_VALU_PEAK_TFLOPS,
+                        "traffic": next((v for k, v in traffic_by_kernel.items() if k.startswith(fam)), None)}
+    dom = max(kernels, key=lambda k: kernels[k]["ms_per_frame"]) if kernels else "nearest_first_kernel"
+    dk = kernels.get(dom, {"ms_per_frame": 0.0, "achieved": 0.0, "frac": 0.0, "traffic": None, "ops_per_frame": 0.0,
+                           "launches_per_frame": 0.0, "instantiation": fam_inst[dom]})
     # algorithmic HBM bytes of one raytrace launch: the decoded collider records, directions,
     # origins and the fans' result blocks (everything else is L2-resident scratch)
     rec_bytes = scene.spheres.size * 32 + scene.aabbs.size * 32 + scene.obbs.size * 64  # hot records
     alg_bytes = rec_bytes + cfg.R * 6 + S * 12 + S * lay["stride"]
     hbm_gbs = alg_bytes / (rt_ms * 1e-3) / 1e9
-    traffic, traffic_by_kernel, traffic_note = read_traffic(cfg.index)
-    near_traffic = next((v for k, v in traffic_by_kernel.items() if k.startswith("nearest_first_kernel")), None)
 
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
@@ -724,23 +754,30 @@ def main():
                                                               if world > 1 else "")},
         "allgather_ms": allgather_ms,
         "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
-        "allgather_note": "HIP events on the launch stream around the all-gather of every 8th of the first 512 timed steps, max over "
-                          "ranks; the step time includes it" if world > 1 else None,
-        "roofline": {"bound": "valu", "kernel": f"nearest_first_kernel<false, {'true' if scene.obbs.size > 0 else 'false'}, "
-                                                    f"{'true' if cfg.H > 1 else 'false'}>",
-                     "achieved": near_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": near_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": near_traffic,
-                     "kernel_ms": near_ms, "launches_per_frame": ktimes["nearest_launches"] / n_rt,
-                     "ops_per_frame": by_kernel_ops["nearest"],
-                     "note": "the dominant kernel (nearest-hit BVH traversal; FP32 VALU roof, no MFMA-shaped work). "
-                             "achieved = ops it executed per frame (exact lane-tests x SURVEY.md 8(d) ops per test + "
-                             "BVH box tests x 14, art_exec_counts.by_kernel[0]) / its duration per frame (HIP events "
-                             "around its launches on the launch stream, every 8th of the first 512 timed steps); traffic = its HBM bytes "
-                             "per frame from same-build FETCH_SIZE / WRITE_SIZE passes (" + traffic_note + ")",
-                     "single_issue": {"achieved": near_tflops, "peak": SINGLE_ISSUE_TLOPS, "unit": "T lane-op/s",
-                                      "frac": near_tflops / SINGLE_ISSUE_TLOPS,
-                                      "note": "one non-FMA lane-op per lane per issue: 256 CU x 128 lanes/clk x 2.4 GHz"},
-                     "stage": {"kernels": stage_kernels(cfg, S, scene.obbs.size > 0), "kernel_ms": rt_ms, "achieved": ex_tflops,
+        "allgather_note": f"HIP events on the launch stream around the all-gather of {n_pass} untimed frames after the "
+                          "timed region, max over ranks; the step time includes it" if world > 1 else None,
+        "roofline": {"bound": "valu", "kernel": dk["instantiation"],
+                     "achieved": dk["achieved"], "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": dk["frac"], "traffic": dk["traffic"],
+                     "kernel_ms": dk["ms_per_frame"], "launches_per_frame": dk["launches_per_frame"],
+                     "ops_per_frame": dk["ops_per_frame"],
+                     "note": "the dominant kernel: the stage's kernel family with the longest measured time per frame "
+                             "(FP32 VALU roof: branchy intersection math, no MFMA-shaped work). achieved = ops it executed "
+                             "per frame (exact lane-tests x SURVEY.md 8(d) ops per test + BVH box tests x 14 + cell entries "
+                             "x 2, art_exec_counts.by_kernel) / its duration per frame (HIP events around each of its "
+                             f"launches on the stream it runs on, {n_pass} untimed frames after the timed region, "
+                             "ART_CTX_TIME_EACH_KERNEL); traffic = its HBM bytes per frame from same-build FETCH_SIZE / "
+                             "WRITE_SIZE passes (" + traffic_note + ")",
+                     "kernels": kernels,
+                     "single_issue": {"achieved": dk["achieved"], "peak": SINGLE_ISSUE_TLOPS, "unit": "T lane-op/s",
+                                      "frac": dk["achieved"] / SINGLE_ISSUE_TLOPS,
+                                      "frac_at_64_lanes_per_clk": dk["achieved"] / SINGLE_ISSUE_TLOPS_64,
+                                      "note": "one non-FMA lane-op per lane per issue. peak assumes a wave64 VALU op issues "
+                                              "over 2 cycles per SIMD (32 lanes/clk/SIMD, MI355X_MICROARCH.md line 54): "
+                                              "256 CU x 128 lanes/clk x 2.4 GHz = 78.6 T; frac_at_64_lanes_per_clk is the "
+                                              "fraction of 39.3 T (64 lanes/clk/CU, SURVEY.md 8(d)) if that issue rate is "
+                                              "not reached without packed math"},
+                     "stage": {"kernels": stage_kernels(cfg, params.thread_count, scene.obbs.size > 0), "kernel_ms": rt_ms, "achieved": ex_tflops,
                                "frac": ex_tflops / FP32_VALU_PEAK_TFLOPS,
                                "single_issue_frac": ex_ops / (rt_ms * 1e-3) / 1e12 / SINGLE_ISSUE_TLOPS,
                                "traffic": traffic, "traffic_by_kernel": traffic_by_kernel, "traffic_note": traffic_note,
@@ -763,8 +800,10 @@ def main():
                              "counter_frac": traffic / (rt_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                              "note": "achieved = algorithmic bytes / stage time; counter_gbs = the stage's PMC HBM bytes "
                                      "(2 x FETCH_SIZE + WRITE_SIZE, same build) / stage time"}},
-        "kernel_ms": {"raytrace": rt_ms, "nearest": near_ms, "permeate": ktimes["permeate_ms"] / n_rt,
-                      "reduce": ktimes["reduce_ms"] / n_rt},
+        "kernel_ms": {"raytrace": rt_ms, "permeate": ktimes["permeate_ms"] / n_rt, "reduce": ktimes["reduce_ms"] / n_rt,
+                      **{k: v["ms_per_frame"] for k, v in kernels.items()},
+                      "frames_timed": n_rt, "note": f"pass 1 (stage events only, {n_pass} untimed frames after the timed "
+                                                    "region); per kernel family: pass 2 (ART_CTX_TIME_EACH_KERNEL)"},
         "lib_sha256": lib_sha256(),
         "cpu_baseline": cpu,
     }

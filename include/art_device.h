@@ -34,15 +34,28 @@ typedef struct {
     uint32_t hit_ids_off;     /* uint32_t[R*H]  (iff ART_OUT_HIT_RESULTS): ART_HIT_ID / ART_HIT_NONE */
 } art_fan_layout;
 
+/* Kernel families of the raytrace stage (art_kernel_times.kernel_ms order). */
+#define ART_KERNEL_NEAREST     0 /* nearest_first_kernel (per bounce; multi-hit frames: the path epilogue folded in) */
+#define ART_KERNEL_ECHO_MUFFLE 1 /* echo_muffle_kernel (one-hit frames: echo traversal + muffle rays, one launch) */
+#define ART_KERNEL_ECHO        2 /* vis_kernel, the echo any-hit traversal (multi-hit frames: per bounce, side stream) */
+#define ART_KERNEL_MUFFLE      3 /* muffle_kernel (multi-hit frames: once, after the last bounce) */
+
+/* ABI 3.0 (80 B; 2.3 had 48 B). */
 typedef struct {
-    double raytrace_ms, permeate_ms, reduce_ms; /* summed hipEvent durations */
+    double raytrace_ms, permeate_ms, reduce_ms; /* summed hipEvent durations of the frame's stages */
     int32_t launches;                           /* frames timed */
-    int32_t nearest_launches;                   /* nearest_first_kernel launches timed (ABI 2.3) */
-    double nearest_ms;                          /* summed durations of those launches (ABI 2.3) */
+    int32_t kernel_marks_dropped;               /* ART_CTX_TIME_EACH_KERNEL launches left unmarked (out of event pairs) */
+    double kernel_ms[4];                        /* ART_CTX_TIME_EACH_KERNEL: summed durations per ART_KERNEL_* family */
+    int32_t kernel_launches[4];                 /*   and the launches timed per family */
 } art_kernel_times;
 
-/* Record hipEvents around every kernel of art_launch_device (art_set_flags). */
+/* Record hipEvents around the stages of every frame of art_launch_device (art_set_flags). An event
+ * record costs a few microseconds of GPU idle, so timed frames run slower than untimed ones: time
+ * in a pass of its own, outside the frames whose wall time is measured. */
 #define ART_CTX_TIME_KERNELS 0x2u
+/* With ART_CTX_TIME_KERNELS: also an event pair around each kernel of the raytrace stage, on the
+ * stream it runs on (art_kernel_times.kernel_ms). */
+#define ART_CTX_TIME_EACH_KERNEL 0x200u
 /* Frame outputs from the reference-order raytrace kernel (one ray per lane, every collider in
  * reference order; the kernel the test counts come from) instead of the throughput stage. */
 #define ART_CTX_FORCE_REFERENCE_ORDER 0x4u

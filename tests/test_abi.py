@@ -55,11 +55,29 @@ def test_struct_sizes_match_csharp_layouts():
     assert offs["ray_hit_counts"] == 64 and offs["ray_hit_ids"] == 72  # appended after the editor arrays
     assert C.sizeof(abi.art_fan_layout) == 9 * 4
     assert C.sizeof(abi.art_exec_counts) == 8 * 8 + 16 * 8 + 3 * 5 * 8  # 2.3: by_kernel appended
+    assert C.sizeof(abi.art_kernel_times) == 3 * 8 + 2 * 4 + 4 * 8 + 4 * 4  # 3.0: per kernel family
+
+
+def test_header_struct_sizes_match_bindings(tmp_path):
+    """The C compiler's view of include/*.h (what a P/Invoke or cgo caller builds against) equals
+    the ctypes mirror, struct by struct."""
+    import subprocess
+    structs = {"art_fan": abi.art_fan, "art_fan_layout": abi.art_fan_layout, "art_exec_counts": abi.art_exec_counts,
+               "art_kernel_times": abi.art_kernel_times, "art_test_counts": abi.art_test_counts,
+               "art_collider_sync_stats": abi.art_collider_sync_stats}
+    src = tmp_path / "sizes.c"
+    src.write_text('#include <stdio.h>\n#include "art_device.h"\n#include "art_colliders.h"\nint main(void) {\n' +
+                   "".join(f'  printf("{n} %zu\\n", sizeof({n}));\n' for n in structs) + "  return 0;\n}\n")
+    exe = tmp_path / "sizes"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(l.split() for l in subprocess.check_output([str(exe)], text=True).splitlines())
+    for n, t in structs.items():
+        assert int(got[n]) == C.sizeof(t), (n, got[n], C.sizeof(t))
 
 
 def test_version():
     v = art.load_library().art_version()
-    assert v >> 16 == 2 and v & 0xffff >= 3  # 2.0: art_fan.ray_hit_ids; 2.3: art_exec_counts.by_kernel
+    assert v >> 16 == 3 and v & 0xffff >= 0  # 3.0: art_kernel_times per kernel family (a grown struct: major bump)
 
 
 def test_no_gpu_fails_loudly():
