@@ -315,6 +315,31 @@ __global__ void kd_keys_kernel(const CullRec* __restrict__ cull, int n, KdBufs k
   for (int a = 0; a < 3; ++a) k.vals[(size_t)a * n + i] = i;
 }
 
+// The three axis orders of the kd build for up to 1024 * ITEMS colliders: one workgroup per axis
+// sorts its (key, id) pairs in LDS (rocprim block radix sort, stable: ties keep id order, as the
+// device-wide radix sorts it replaces for these sizes). One launch instead of three device-wide
+// sorts with their helper launches (round 4: about 54 us of a config-2 rebuild frame).
+template <int ITEMS>
+__global__ __launch_bounds__(1024) void kd_axis_sort_kernel(KdBufs k, int n) {
+  using Sort = hipcub::BlockRadixSort<uint32_t, 1024, ITEMS, int>;
+  __shared__ typename Sort::TempStorage tmp;
+  const int a = blockIdx.x;
+  uint32_t key[ITEMS];
+  int val[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {  // blocked arrangement in id order (padding sorts last: keys of
+    const int i = (int)threadIdx.x * ITEMS + j;  // finite centres stay below 0xff800000)
+    key[j] = i < n ? k.keys[(size_t)a * n + i] : 0xffffffffu;
+    val[j] = i;
+  }
+  Sort(tmp).SortBlockedToStriped(key, val);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = j * 1024 + (int)threadIdx.x;
+    if (i < n) k.p[(size_t)a * n + i] = val[j];
+  }
+}
+
 __device__ __forceinline__ float kd_comp(const float4& c, int a) { return a == 0 ? c.x : (a == 1 ? c.y : c.z); }
 
 // Block-wide exclusive scan of three counters per thread (NT threads, NT / 64 waves).
@@ -793,11 +818,17 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
     hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
-    for (int a = 0; a < 3; ++a) {  // the three axis orders (stable: ties keep id order)
-      size_t bytes = sb.temp_bytes;
-      if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
-                                             n, 0, 32, st) != hipSuccess)
-        return -1;
+    if (n <= 4096) {  // the three axis orders (stable: ties keep id order), one workgroup per axis
+      hipLaunchKernelGGL(kd_axis_sort_kernel<4>, dim3(3), dim3(1024), 0, st, k, n);
+    } else if (n <= kKdMaxColliders) {
+      hipLaunchKernelGGL(kd_axis_sort_kernel<kKdMaxColliders / 1024>, dim3(3), dim3(1024), 0, st, k, n);
+    } else {
+      for (int a = 0; a < 3; ++a) {
+        size_t bytes = sb.temp_bytes;
+        if (hipcub::DeviceRadixSort::SortPairs(sb.temp, bytes, k.keys + (size_t)a * n, sb.keys_s, sb.vals, k.p + (size_t)a * n,
+                                               n, 0, 32, st) != hipSuccess)
+          return -1;
+      }
     }
     if (n <= kKdMaxColliders && kd_wave_enabled()) {
       // one 1024-thread workgroup down to 512-position segments, then one 256-thread workgroup per

@@ -475,8 +475,19 @@ void pack_inputs(const art_frame_desc* d, const Frame& f, uint8_t* h) {
 // An art_launch_device frame still running on the caller's stream reads the scene (records, sorted
 // copies, BVH) and uses the context's shared buffers (accumulators, pairs, side streams): work on
 // dv.stream that rewrites or reuses them waits for it first.
+// The completion event of those frames is recorded only here, when something has to wait for them:
+// an event record between frames costs the launch stream ~5 us of GPU idle per frame (kernel trace,
+// DESIGN.md §4), so back-to-back frames on one stream record none. The caller's stream of the last
+// frame must still exist at the next call that touches the scene (art.h, streams).
+int mark_launch_done(art_ctx* c, Device& dv) {
+  if (!dv.launch_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.launch_done, hipEventDisableTiming));
+  HIP_TRY(c, hipEventRecord(dv.launch_done, dv.launch_stream));
+  return ART_OK;
+}
 int wait_launch(art_ctx* c, Device& dv) {
   if (dv.launch_pending) {
+    int rc = mark_launch_done(c, dv);
+    if (rc) return rc;
     HIP_TRY(c, hipStreamWaitEvent(dv.stream, dv.launch_done, 0));
     dv.launch_pending = false;
   }
@@ -678,9 +689,11 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   fp.muf_curve = reinterpret_cast<const float*>(raw + f.off_muf);
   const int2* slot_batch = reinterpret_cast<const int2*>(raw + f.off_tab);
   const uint8_t* muffle_reset = raw + f.off_reset;
+  const bool fast = (f.stages & ART_STAGE_RAYTRACE) && !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
+  const size_t acc_per_fan = (size_t)f.TC * f.T;
   // muffle accumulators, then (16-B aligned) the visibility pair counters: cleared by the first
   // nearest_first_kernel of each fast-path chunk, by one memset before the reference-order kernel
-  const size_t acc_words = ((size_t)fan_count * f.TC * f.T + 3) & ~(size_t)3;
+  const size_t acc_words = ((size_t)fan_count * acc_per_fan + 3) & ~(size_t)3;
   const size_t acc_bytes = acc_words * sizeof(uint32_t) + 16;  // + 4 pair counters
   if (!dv.acc.reserve(acc_bytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   uint32_t* acc = static_cast<uint32_t*>(dv.acc.p);
@@ -705,7 +718,6 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
 
   // Everything the stages allocate or create comes first: once the permeation job is forked to the
   // side stream, an early error return would leave it writing the caller's block unjoined.
-  const bool fast = (f.stages & ART_STAGE_RAYTRACE) && !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
   // the permeation job over the BVH (art_trace.hip); reference-order and counting frames sweep every
   // collider (art_kernels.hip), an independent implementation the parity tests compare too
   const bool perm_bvh = !count && !(c->flags & ART_CTX_FORCE_REFERENCE_ORDER);
@@ -795,7 +807,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
         FrameParams fpc = fpx;
         fpc.S = std::min(chunk, fan_count - b0);
         launch_raytrace_fast(dv.sc, fpc, f.L, d_origins + 3 * (size_t)b0, d_block + (size_t)b0 * f.L.stride,
-                             acc + (size_t)b0 * f.TC * f.T, order, dv.pairs.p, pair_count, st, echo,
+                             acc + (size_t)b0 * acc_per_fan, order, dv.pairs.p, pair_count, st, echo,
                              marks.cap ? &marks : nullptr);
       }
       for (int k = 0; k < marks.used; ++k)  // pool index base + 2 k
@@ -973,7 +985,7 @@ ART_API void art_destroy(art_ctx* c) {
   for (Device& dv : c->devs) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    if (dv.launch_done) (void)hipEventSynchronize(dv.launch_done);  // a device frame on the caller's stream
+    if (dv.launch_pending) (void)hipDeviceSynchronize();  // a device frame on the caller's stream (which may be gone)
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.exec.release(); dv.pairs.release(); dv.dsp.release(); dv.cones.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
@@ -1247,13 +1259,15 @@ static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, 
   if (f.resident && dv.st_done) HIP_TRY(c, hipStreamWaitEvent(st, dv.st_done, 0));
   // frames share the context's accumulators and pair buffers: a launch on another stream than the
   // previous one waits for it (on the same stream, stream order already does)
-  if (dv.launch_pending && st != dv.launch_stream) HIP_TRY(c, hipStreamWaitEvent(st, dv.launch_done, 0));
+  if (dv.launch_pending && st != dv.launch_stream) {
+    int rc = mark_launch_done(c, dv);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamWaitEvent(st, dv.launch_done, 0));
+  }
   int rc = enqueue_kernels(c, dv, f, d_origins, fan_count, static_cast<uint8_t*>(d_block), st, count);
   if (rc) return rc;
   // the next sync, bind or schedule rewrites the scene or reuses the shared buffers on dv.stream:
-  // after this frame (wait_launch)
-  if (!dv.launch_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.launch_done, hipEventDisableTiming));
-  HIP_TRY(c, hipEventRecord(dv.launch_done, st));
+  // after this frame (wait_launch records the event on this stream then)
   dv.launch_pending = true;
   dv.launch_stream = st;
   if (count) return read_counts(c, dv, st, out, false);

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include <hipcub/hipcub.hpp>
 
@@ -407,11 +408,23 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
                                                                  cells, cb.start, cb.start + 1, 0, 16, st);
     if (e != hipSuccess) return -1;
   }
-  if (env_ll("ART_DEBUG_CELLS", 0)) {  // diagnostics: the built lists' size (synchronizes the stream)
-    uint32_t total = 0;
-    if (hipMemcpyAsync(&total, cb.start + cells, 4, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
-      fprintf(stderr, "[cells] T %d colliders %d: %u entries (capacity %u, %.1f per pair)\n", T, n, total, cb.cap,
-              (double)total / std::max(1ll, pairs));
+  if (env_ll("ART_DEBUG_CELLS", 0)) {  // diagnostics: the built lists' size and length histogram (synchronizes)
+    std::vector<uint32_t> hs((size_t)cells + 1);
+    if (hipMemcpyAsync(hs.data(), cb.start, hs.size() * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        hipStreamSynchronize(st) == hipSuccess) {
+      unsigned long long hist[18] = {};  // lists of length 0, 1, 2-3, 4-7, ... (log2 buckets)
+      uint32_t longest = 0;
+      for (int i = 0; i < cells; ++i) {
+        const uint32_t len = hs[(size_t)i + 1] - hs[i];
+        longest = std::max(longest, len);
+        hist[len == 0 ? 0 : std::min(17, 33 - __builtin_clz(len))]++;
+      }
+      fprintf(stderr, "[cells] T %d colliders %d: %u entries (capacity %u, %.1f per pair), %d lists, longest %u; lengths", T,
+              n, hs[(size_t)cells], cb.cap, (double)hs[(size_t)cells] / std::max(1ll, pairs), cells, longest);
+      for (int b = 0; b < 18; ++b)
+        if (hist[b]) fprintf(stderr, " [%u..%u]:%llu", b == 0 ? 0u : 1u << (b - 1), b == 0 ? 0u : (1u << b) - 1u, hist[b]);
+      fprintf(stderr, "\n");
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

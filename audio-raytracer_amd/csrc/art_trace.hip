@@ -968,58 +968,22 @@ __device__ __forceinline__ bool echo_seg_from_hit(const DevScene& sc, const Echo
   return true;
 }
 
-template <bool OBB, bool HM>
-__device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                              unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
-                                              const uint32_t* ecnt, int bounce, uint8_t* block, const EchoFromHits& eh) {
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
-  const int wq = lane >> 2, slot = w * 16 + wq;                // segment of the block's 64-pair batch
-  if (sc.bvh_levels == 0 && !HM) return;                       // no colliders: nothing blocks
-  bool valid;
-  uint32_t p = 0u, out_at = 0u;
-  uint16_t out_val = 0;
-  Seg s;
-  float maxd = 0.0f;
-  int owner = kNoOwner;
-  s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
-  s.a2 = 0.0f;
-  if (HM) {
-    bool slot_ok;
-    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val, slot_ok);
-    if (eh.no_path) {  // the path kernel's duties for this frame: a miss keeps the reset 0 (:76, :200-207)
-      if (slot_ok && !valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = 0;
-      if (ex) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__ballot(valid) & 0x1111111111111111ull));
-    }
-    if (!__any(valid)) return;
-  } else {
-    if (vp.fixed) {  // bounce `bounce`'s records at fixed slots: 64-slot group blk
-      p = (uint32_t)bounce * vp.fixed + blk * 64u + (uint32_t)slot;
-      valid = vp.out[p].x != kNoRecord;
-      if (!__any(valid)) return;
-      if (valid) load_pair_seg(vp, p, s, maxd, owner);
-    } else {
-      // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
-      uint32_t start = 0u, n;
-      if (bounce < 0) {
-        n = ldc(count, 0);
-      } else {
-        for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
-        n = start + ldc(ecnt, bounce);
-      }
-      const uint32_t base = start + blk * 64u;
-      if (base + (uint32_t)(w * 16) >= n) return;                // this wave's 16 segments are past the emitted pairs
-      valid = base + (uint32_t)slot < n;
-      p = valid ? base + (uint32_t)slot : base;
-      if (valid) load_pair_seg(vp, p, s, maxd, owner);
-    }
-  }
+// Any-hit traversal of the wave's 16 segments, one per quad (lane & 3 = the quad's child / slot;
+// s_wave = the wave's 16 stacks of kBvhStack entries): true in every lane of a quad whose segment
+// no collider blocks (hit and d < maxd, tid != owner: CanRaySeePoint :365-397 / :411-447 with
+// owner = the target). `valid` must be quad-uniform; an invalid segment is reported visible.
+// Work sharing as in the nearest traversal (a blocker of a shared segment ends every traversal of
+// it); nt / nnode accumulate the exact tests and node visits (EX counters).
+template <bool OBB>
+__device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float maxd, int owner, bool valid, int lane,
+                                               uint32_t* s_wave, unsigned* nt, unsigned& nnode) {
+  const int qd = lane & 3, wq = lane >> 2;
+  if (sc.bvh_levels == 0) return true;                         // no colliders: nothing blocks
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
   bool force = force_all(s, om);
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
   const BvhRes br = bvh_res(sc);
-  uint32_t* const s_wave = s_stk + w * 16 * kBvhStack;
   uint32_t* const my = s_wave + wq * kBvhStack;                // entries [bp, sp) pending
-  unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
   uint32_t wblocked = 0u;                                      // wave-uniform: home quads found blocked
   int home = wq;
   int g = valid ? 0 : -1, sp = 0, bp = 0;
@@ -1035,7 +999,6 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     sp = has ? sp - 1 : sp;
     if (sp == bp) sp = bp = 0;
   };
-  constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every quad
   for (;;) {
     const unsigned long long act = __ballot(g >= 0) & kQuad0;
     if (!act) break;
@@ -1103,7 +1066,56 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   if (qd == 0 && valid) diag_add(3, nsteps);
   if (lane == 0) diag_add(1, clock64() - t0);
 #endif
-  const bool visible = !((wblocked >> wq) & 1u);
+  return !((wblocked >> wq) & 1u);
+}
+
+template <bool OBB, bool HM>
+__device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
+                                              unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
+                                              const uint32_t* ecnt, int bounce, uint8_t* block, const EchoFromHits& eh) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
+  const int wq = lane >> 2, slot = w * 16 + wq;                // segment of the block's 64-pair batch
+  if (sc.bvh_levels == 0 && !HM) return;                       // no colliders: nothing blocks
+  bool valid;
+  uint32_t p = 0u, out_at = 0u;
+  uint16_t out_val = 0;
+  Seg s;
+  float maxd = 0.0f;
+  int owner = kNoOwner;
+  s.o = s.d = s.inv = mk3(0.0f, 0.0f, 0.0f);
+  s.a2 = 0.0f;
+  if (HM) {
+    bool slot_ok;
+    valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val, slot_ok);
+    if (eh.no_path) {  // the path kernel's duties for this frame: a miss keeps the reset 0 (:76, :200-207)
+      if (slot_ok && !valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = 0;
+      if (ex) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__ballot(valid) & kQuad0));
+    }
+    if (!__any(valid)) return;
+  } else {
+    if (vp.fixed) {  // bounce `bounce`'s records at fixed slots: 64-slot group blk
+      p = (uint32_t)bounce * vp.fixed + blk * 64u + (uint32_t)slot;
+      valid = vp.out[p].x != kNoRecord;
+      if (!__any(valid)) return;
+      if (valid) load_pair_seg(vp, p, s, maxd, owner);
+    } else {
+      // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
+      uint32_t start = 0u, n;
+      if (bounce < 0) {
+        n = ldc(count, 0);
+      } else {
+        for (int j = 0; j < bounce; ++j) start += ldc(ecnt, j);
+        n = start + ldc(ecnt, bounce);
+      }
+      const uint32_t base = start + blk * 64u;
+      if (base + (uint32_t)(w * 16) >= n) return;                // this wave's 16 segments are past the emitted pairs
+      valid = base + (uint32_t)slot < n;
+      p = valid ? base + (uint32_t)slot : base;
+      if (valid) load_pair_seg(vp, p, s, maxd, owner);
+    }
+  }
+  unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
+  const bool visible = quad_echo_core<OBB>(sc, s, maxd, owner, valid, lane, s_stk + w * 16 * kBvhStack, nt, nnode);
   if (HM) {
     if (valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = visible ? out_val : (uint16_t)0;  // :76, :142-144
   } else if (valid && visible && qd == 0) {  // visible: the echo is stored (:142-144)
@@ -1185,6 +1197,103 @@ __device__ bool muffle_brute(const DevScene& sc, const Seg& s, float maxd, int t
   return false;
 }
 
+// The muffle ray of target t from `off` (the hit point stepped back along the ray, :158), tp the
+// target's position and maxd = distance(off, tp) (:165, the caller checks maxd < MaxMuffleHitDistance
+// :168): true when a collider not owned by t blocks it (CanRaySeeAudioTarget :405-449). The ray
+// walks the three type lists of its direction cell around the target, each by ascending near
+// bound, stopping at the first entry past the segment; a segment longer than the lists' cell_far,
+// a degenerate one or a dropped target tests every collider in reference order. nt / ne / nfb
+// count exact tests, list entries and fallback rays (EX).
+template <bool EX, bool OBB>
+__device__ __forceinline__ bool muffle_blocked(const DevScene& sc, vec3 off, vec3 tp, float maxd, int t, unsigned* nt,
+                                               unsigned& ne, unsigned& nfb) {
+  bool blocked = false;
+  const Seg s = make_seg(off, normalize(tp - off));               // :158-160
+  const vec3 v = off - tp;                                        // the ray seen from the target
+  const bool lists = sc.cell_ok[t] != 0u && maxd <= sc.cell_far[t] && (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f) &&
+                     isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
+  if (lists) {
+    // the cell's Sphere, AABB and OBB lists in turn (a type-uniform test per loop), each by
+    // ascending near bound: a walk stops at the first entry past the segment
+    const uint32_t* st = sc.cell_start + ((size_t)t * kCells + cube_cell(v)) * 3;
+    const float lim = maxd * 1.00001f + 1e-6f;
+    const uint32_t klim = near_key(__float_as_uint(lim));
+    const uint4 se = make_uint4(st[0], st[1], st[2], st[3]);
+    // two entries per step: both records are fetched before either is tested (two dependent
+    // fetch chains in flight per lane instead of one); OBB records (64 B) one at a time, which
+    // keeps the kernel within 64 VGPRs
+    // entry k: in-type index, near key and near bound (4-B entries carry the key, whose float
+    // is a lower bound of the near bound: the per-entry bound check then admits a little more)
+    auto entry = [&](uint32_t k, uint32_t& idx, uint32_t& key, float& nearf) {
+      if (sc.cell_compact) {  // (wave-uniform)
+        const uint32_t v = sc.cell_ent32[k];
+        idx = v & 0xffffu; key = v >> 16; nearf = __uint_as_float(key << 16);
+      } else {
+        const uint2 v = sc.cell_ent[k];
+        idx = v.x & 0x0fffffffu; key = near_key(v.y); nearf = __uint_as_float(v.y);
+      }
+    };
+    auto walk = [&](uint32_t b, uint32_t e, auto load, auto test, auto pair) {
+      uint32_t i0, k0, i1, k1;
+      float n0, n1;
+      if (!decltype(pair)::value) {
+        for (uint32_t k = b; k < e; ++k) {
+          entry(k, i0, k0, n0);
+          if (k0 > klim) break;  // this and every later entry lie beyond the segment
+          if (EX) ++ne;
+          if (!(n0 > lim) && test(load(i0))) { blocked = true; break; }
+        }
+        return;
+      }
+      for (uint32_t k = b; k < e && !blocked; k += 2) {
+        const bool has1 = k + 1 < e;
+        entry(k, i0, k0, n0);
+        entry(has1 ? k + 1 : k, i1, k1, n1);
+        if (k0 > klim) break;             // this and every later entry lie beyond the segment
+        const bool use1 = has1 && k1 <= klim;
+        const auto r0 = load(i0);
+        const auto r1 = load(use1 ? i1 : i0);
+        if (EX) ne += use1 ? 2u : 1u;
+        if (!(n0 > lim) && test(r0)) { blocked = true; break; }
+        if (!use1) break;
+        if (!(n1 > lim) && test(r1)) { blocked = true; break; }
+      }
+    };
+    walk(se.x, se.y,
+         [&](uint32_t idx) {
+           const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
+           SphereRec r;
+           r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
+           return r;
+         },
+         [&](const SphereRec& r) {
+           ++nt[0];
+           float d;
+           return sphere_hit_dist(s, r, d) && d < maxd;
+         },
+         std::true_type{});
+    walk(se.y, se.z, [&](uint32_t idx) { return sc.aabb[idx]; },
+         [&](const AabbRec& r) {
+           ++nt[1];
+           float d;
+           return aabb_test<false>(s, r, d) && d < maxd;
+         },
+         std::true_type{});
+    if (OBB)
+      walk(se.z, se.w, [&](uint32_t idx) { return sc.obb + idx; },
+           [&](const ObbRec* r) {
+             ++nt[2];
+             float d;
+             return obb_test_staged(s, r, d) && d < maxd;
+           },
+           std::false_type{});
+  } else {
+    if (EX) ++nfb;
+    blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
+  }
+  return blocked;
+}
+
 // HM: one-hit frames with one batch slot whose path kernel does not run: lane i is ray slot i
 // (64-ray group i / 64) and its muffle rays start from the nearest hit as the path kernel computes
 // it (hit_from_pre); the accumulator base is fan * T (TC == 1: batch slot 0).
@@ -1219,89 +1328,7 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
     const bool act = valid && maxd < fp.max_muffle;                   // :168
     bool blocked = false;
     if (act) {
-      const Seg s = make_seg(off, normalize(tp - off));               // :158-160
-      const vec3 v = off - tp;                                        // the ray seen from the target
-      const bool lists = sc.cell_ok[t] != 0u && maxd <= sc.cell_far[t] && (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f) &&
-                         isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
-      if (lists) {
-        // the cell's Sphere, AABB and OBB lists in turn (a type-uniform test per loop), each by
-        // ascending near bound: a walk stops at the first entry past the segment
-        const uint32_t* st = sc.cell_start + ((size_t)t * kCells + cube_cell(v)) * 3;
-        const float lim = maxd * 1.00001f + 1e-6f;
-        const uint32_t klim = near_key(__float_as_uint(lim));
-        const uint4 se = make_uint4(st[0], st[1], st[2], st[3]);
-        // two entries per step: both records are fetched before either is tested (two dependent
-        // fetch chains in flight per lane instead of one); OBB records (64 B) one at a time, which
-        // keeps the kernel within 64 VGPRs
-        // entry k: in-type index, near key and near bound (4-B entries carry the key, whose float
-        // is a lower bound of the near bound: the per-entry bound check then admits a little more)
-        auto entry = [&](uint32_t k, uint32_t& idx, uint32_t& key, float& nearf) {
-          if (sc.cell_compact) {  // (wave-uniform)
-            const uint32_t v = sc.cell_ent32[k];
-            idx = v & 0xffffu; key = v >> 16; nearf = __uint_as_float(key << 16);
-          } else {
-            const uint2 v = sc.cell_ent[k];
-            idx = v.x & 0x0fffffffu; key = near_key(v.y); nearf = __uint_as_float(v.y);
-          }
-        };
-        auto walk = [&](uint32_t b, uint32_t e, auto load, auto test, auto pair) {
-          uint32_t i0, k0, i1, k1;
-          float n0, n1;
-          if (!decltype(pair)::value) {
-            for (uint32_t k = b; k < e; ++k) {
-              entry(k, i0, k0, n0);
-              if (k0 > klim) break;  // this and every later entry lie beyond the segment
-              if (EX) ++ne;
-              if (!(n0 > lim) && test(load(i0))) { blocked = true; break; }
-            }
-            return;
-          }
-          for (uint32_t k = b; k < e && !blocked; k += 2) {
-            const bool has1 = k + 1 < e;
-            entry(k, i0, k0, n0);
-            entry(has1 ? k + 1 : k, i1, k1, n1);
-            if (k0 > klim) break;             // this and every later entry lie beyond the segment
-            const bool use1 = has1 && k1 <= klim;
-            const auto r0 = load(i0);
-            const auto r1 = load(use1 ? i1 : i0);
-            if (EX) ne += use1 ? 2u : 1u;
-            if (!(n0 > lim) && test(r0)) { blocked = true; break; }
-            if (!use1) break;
-            if (!(n1 > lim) && test(r1)) { blocked = true; break; }
-          }
-        };
-        walk(se.x, se.y,
-             [&](uint32_t idx) {
-               const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
-               SphereRec r;
-               r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
-               return r;
-             },
-             [&](const SphereRec& r) {
-               ++nt[0];
-               float d;
-               return sphere_hit_dist(s, r, d) && d < maxd;
-             },
-             std::true_type{});
-        walk(se.y, se.z, [&](uint32_t idx) { return sc.aabb[idx]; },
-             [&](const AabbRec& r) {
-               ++nt[1];
-               float d;
-               return aabb_test<false>(s, r, d) && d < maxd;
-             },
-             std::true_type{});
-        if (OBB)
-          walk(se.z, se.w, [&](uint32_t idx) { return sc.obb + idx; },
-               [&](const ObbRec* r) {
-                 ++nt[2];
-                 float d;
-                 return obb_test_staged(s, r, d) && d < maxd;
-               },
-               std::false_type{});
-      } else {
-        if (EX) ++nfb;
-        blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
-      }
+      blocked = muffle_blocked<EX, OBB>(sc, off, tp, maxd, t, nt, ne, nfb);
     }
     const bool vis = act && !blocked;                                 // :171
     unsigned long long mv = __ballot(vis);
@@ -1371,6 +1398,7 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
   muffle_block(blockIdx.x - groups, mblocks, mt, rb, t);  // (groups is a multiple of 8 in the bench shapes)
   muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, rb * 256u + threadIdx.x, t, mt);
 }
+
 
 // ------------------------------------------------------------------------------------------
 // Permeation job (AudioPermeationJobBatched.Execute :34-91) over the BVH. One wave per (batch slot,
@@ -1656,11 +1684,11 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
                           uint8_t* block, uint32_t* muffle_acc, const int* ray_order, void* pair_buf, uint32_t* pair_count,
                           hipStream_t st, const SideStream& echo, KernelMarks* marks) {
   if (fp.S == 0) return;
-  PairBufs pb = pair_bufs(pair_buf, fp);
   const unsigned groups = (unsigned)((size_t)fp.S * ((fp.R + 63) / 64));
+  const bool obb = sc.no > 0;  // OBB-free scenes run instantiations without the OBB tests
+  PairBufs pb = pair_bufs(pair_buf, fp);
   const unsigned path_blocks = (groups + kPathWaves - 1) / kPathWaves;
   const bool multi = fp.H > 1;
-  const bool obb = sc.no > 0;  // OBB-free scenes run instantiations without the OBB tests
   const uint32_t nacc = (uint32_t)((size_t)fp.S * fp.TC * fp.T);  // this chunk's muffle accumulators
   const uint32_t eb = pb.vp.echo_cap / 64;                         // echo batches (one workgroup each)
   const size_t hcap = (size_t)fp.S * fp.R * fp.H;

@@ -74,7 +74,9 @@ ART_API int art_scene_bind(art_ctx* ctx, const art_frame_desc* desc);
 /* Enqueue one frame on the context's first device: d_origins = float3[fan_count] (device),
  * d_block = fan_count * stride bytes (device, in/out), stream = the hipStream_t to enqueue on
  * (NULL = the HIP default stream, e.g. torch's default stream). Kernels only; returns without
- * synchronizing. */
+ * synchronizing and records no event (back-to-back frames run without gaps). The stream must stay
+ * valid until the context's next call that touches the scene or its buffers (a bind, sync,
+ * schedule, or a launch on another stream), which orders itself after the frame. */
 ART_API int art_launch_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
                               uint32_t out_flags, void* stream);
 
