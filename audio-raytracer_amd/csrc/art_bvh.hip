@@ -319,6 +319,18 @@ __global__ void kd_keys_kernel(const CullRec* __restrict__ cull, int n, KdBufs k
 // sorts its (key, id) pairs in LDS (rocprim block radix sort, stable: ties keep id order, as the
 // device-wide radix sorts it replaces for these sizes). One launch instead of three device-wide
 // sorts with their helper launches (round 4: about 54 us of a config-2 rebuild frame).
+// The centre of collider i on axis a (non-finite -> FLT_MAX, sorting last) and its radix-sortable key.
+__device__ __forceinline__ float kd_centre(const CullRec& c, int a) {
+  const float v = a == 0 ? 0.5f * (c.lox + c.hix) : (a == 1 ? 0.5f * (c.loy + c.hiy) : 0.5f * (c.loz + c.hiz));
+  return isfinite(v) ? v : FLT_MAX;
+}
+__device__ __forceinline__ uint32_t kd_key(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// (the centres and keys are computed here from the bounds, workgroup 0 storing the centres: no
+// separate kd_keys_kernel launch for these sizes)
 template <int ITEMS>
 __global__ __launch_bounds__(1024) void kd_axis_sort_kernel(KdBufs k, int n) {
   using Sort = hipcub::BlockRadixSort<uint32_t, 1024, ITEMS, int>;
@@ -329,7 +341,12 @@ __global__ __launch_bounds__(1024) void kd_axis_sort_kernel(KdBufs k, int n) {
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {  // blocked arrangement in id order (padding sorts last: keys of
     const int i = (int)threadIdx.x * ITEMS + j;  // finite centres stay below 0xff800000)
-    key[j] = i < n ? k.keys[(size_t)a * n + i] : 0xffffffffu;
+    key[j] = 0xffffffffu;
+    if (i < n) {
+      const CullRec c = k.cull[i];
+      key[j] = kd_key(kd_centre(c, a));
+      if (a == 0) k.cen[i] = make_float4(kd_centre(c, 0), kd_centre(c, 1), kd_centre(c, 2), 0.0f);
+    }
     val[j] = i;
   }
   Sort(tmp).SortBlockedToStriped(key, val);
@@ -817,7 +834,7 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   if (sb.kd) {  // kd leaf order
     KdBufs k = kd_bufs(sb.kd, n);
     k.cull = sc.cull;
-    hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
+    if (n > kKdMaxColliders) hipLaunchKernelGGL(kd_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc.cull, n, k, sb.vals);
     if (n <= 4096) {  // the three axis orders (stable: ties keep id order), one workgroup per axis
       hipLaunchKernelGGL(kd_axis_sort_kernel<4>, dim3(3), dim3(1024), 0, st, k, n);
     } else if (n <= kKdMaxColliders) {

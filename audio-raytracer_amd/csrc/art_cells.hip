@@ -26,8 +26,6 @@
 #include <cstdlib>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
-
 #include "art_device_fns.hpp"
 
 namespace art {
@@ -212,7 +210,7 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int
 // us at config 2). FILL = false counts per cell; FILL = true reserves each (cell, type)'s range
 // once, counting the cell's counter down from its count (ranges start + [new, old) are disjoint and
 // fill the cell exactly), and writes the entries of the targets whose lists fit
-// (cells_drop_kernel). (Round 4 also measured one workgroup per (target, face): 128 + 256 us with
+// (cells_block_scan_kernel). (Round 4 also measured one workgroup per (target, face): 128 + 256 us with
 // per-item load balancing over each wave — 32x fewer waves left every step's latency exposed.)
 template <bool FILL>
 __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ geo, int T, CellBufs cb, int n) {
@@ -283,63 +281,164 @@ __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ ge
   }
 }
 
-// Entries per target (64-bit sums of its cells' counts) for the capacity check: one workgroup per
-// 256 counters (kCells * 3 = 72 of them per target), one atomic per workgroup. (Round 4: one
-// workgroup per target took 19 us at config 2; per-entry atomics on T counters serialized the count
-// pass, 90 -> 264 us.)
-__global__ __launch_bounds__(256) void cells_total_kernel(CellBufs cb) {
-  static_assert((kCells * 3) % 256 == 0, "a workgroup covers one target's counters");
-  __shared__ unsigned long long s[256];
-  s[threadIdx.x] = cb.count[(size_t)blockIdx.x * 256 + threadIdx.x];
-  __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if ((int)threadIdx.x < st) s[threadIdx.x] += s[threadIdx.x + st];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0 && s[0]) atomicAdd(cb.tcount + blockIdx.x / ((kCells * 3) / 256), s[0]);
+// Each (target, cell, type) list by ascending near key (muffle_kernel stops at the first entry past
+// its segment), one wave per list, every entry ranked among its list's (the keys below it, equal
+// keys by fill position) and scattered into the sorted array: a list of at most 64 entries holds one
+// entry per lane and broadcasts the keys by readlane; up to kCellSortReg entries, each lane holds
+// several; a longer list reads the keys from memory (O(n^2 / 64) per wave; no list of configs 2-5
+// comes near: config 2's longest has 29 entries, config 4's fewer than 128, ART_DEBUG_CELLS
+// histograms in DESIGN.md §4). (Round 4 sorted every list with a segmented radix sort: 51 us of a
+// config-2 rebuild frame.)
+constexpr int kCellSortReg = 256;
+template <bool COMPACT>
+__device__ __forceinline__ void cells_scatter(const CellBufs& cb, uint32_t from, uint32_t to) {
+  if (COMPACT) reinterpret_cast<uint32_t*>(cb.ent_s)[to] = reinterpret_cast<const uint32_t*>(cb.ent)[from];
+  else cb.ent_s[to] = cb.ent[from];
 }
-
-// Capacity check between the count and the fill, one work-item per (target, cell, type) counter:
-// targets in order keep their lists while the running total of entries fits the capacity; a
-// target that does not fit (or whose far bound is non-finite) is dropped — ok = 0, its counters
-// cleared, its muffle rays test every collider. Each workgroup's first work-item replays the
-// running total up to its target (kCells * 3 is a multiple of 256: a workgroup covers one target).
-// Another workgroup may clear ok[t'] of an earlier target while this one reads it: that happens
-// only for a target the replay leaves out either way. The kept targets' total is at most the
-// capacity (< 2^32), so the u32 scan of the counts cannot wrap and every start is <= cap.
-__global__ __launch_bounds__(256) void cells_drop_kernel(CellBufs cb, int T, uint32_t cells) {
-  static_assert((kCells * 3) % 256 == 0, "a workgroup covers one target's counters");
-  __shared__ uint32_t s_keep;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int t = min((int)(blockIdx.x * blockDim.x / (kCells * 3)), T - 1);
-  if (threadIdx.x == 0) {
-    unsigned long long run = 0;
-    bool keep = false;
-    for (int u = 0; u <= t; ++u) {
-      const unsigned long long c = cb.tcount[u];
-      keep = cb.ok[u] && run + c <= (unsigned long long)cb.cap;
-      if (keep) run += c;
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void cells_sort_kernel(CellBufs cb, int cells) {
+  constexpr int kR = kCellSortReg / 64;
+  const int lane = threadIdx.x & 63;
+  const int i = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (i >= cells) return;  // (wave-uniform)
+  const uint32_t b = cb.start[i], e = cb.start[i + 1], n = e - b;
+  if (n <= 1u) {
+    if (n == 1u && lane == 0) cells_scatter<COMPACT>(cb, b, b);
+    return;
+  }
+  if (n <= 64u) {  // one entry per lane
+    const bool in = (uint32_t)lane < n;
+    const uint32_t key = in ? cb.keys[b + lane] : 0xffffffffu;
+    uint32_t rank = 0u;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)j);
+      rank += (kj < key || (kj == key && j < (uint32_t)lane)) ? 1u : 0u;
     }
-    s_keep = keep ? 1u : 0u;
-    if (!keep && blockIdx.x * blockDim.x == (uint32_t)t * (kCells * 3)) cb.ok[t] = 0u;
+    if (in) cells_scatter<COMPACT>(cb, b + lane, b + rank);
+    return;
   }
-  __syncthreads();
-  if (i < cells && !s_keep) cb.count[i] = 0u;
+  if (n <= (uint32_t)kCellSortReg) {  // kR entries per lane (lane l: l, l + 64, ...)
+    const uint32_t nr = (n + 63u) >> 6;
+    uint32_t key[kR], rank[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t p = (uint32_t)(r * 64 + lane);
+      key[r] = p < n ? cb.keys[b + p] : 0xffffffffu;
+      rank[r] = 0u;
+    }
+#pragma unroll
+    for (int r2 = 0; r2 < kR; ++r2) {
+      if ((uint32_t)r2 >= nr) break;
+      const uint32_t m = min(64u, n - (uint32_t)r2 * 64u);
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key[r2], (int)j), pj = (uint32_t)r2 * 64u + j;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) rank[r] += (kj < key[r] || (kj == key[r] && pj < (uint32_t)(r * 64 + lane))) ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t p = (uint32_t)(r * 64 + lane);
+      if (p < n) cells_scatter<COMPACT>(cb, b + p, b + rank[r]);
+    }
+    return;
+  }
+  for (uint32_t p = (uint32_t)lane; p < n; p += 64u) {  // long list: the other keys from memory
+    const uint32_t key = cb.keys[b + p];
+    uint32_t rank = 0u;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t kj = cb.keys[b + j];
+      rank += (kj < key || (kj == key && j < p)) ? 1u : 0u;
+    }
+    cells_scatter<COMPACT>(cb, b + p, b + rank);
+  }
 }
 
-size_t cells_scan_temp_bytes(int T, uint32_t cap) {
-  size_t scan = 0, sort = 0;
-  const int n = T * kCells * 3 + 1;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, n);
-  size_t sort32 = 0;
-  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, sort, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                                    (int)cap, n - 1, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
-                                                    0, 16);
-  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, sort32, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, n - 1,
-                                                    (const uint32_t*)nullptr, (const uint32_t*)nullptr, 0, 16);
-  return std::max(scan, std::max(sort, sort32));
+// The list starts (round 4: a per-target total kernel, a drop kernel and hipCUB's two-launch scan;
+// a one-workgroup version of all three measured 72 us, its waves walking their groups serially):
+//   cells_block_sum_kernel   one workgroup per 256 counters (a block lies in one target: kCells * 3
+//                            is a multiple of 256): the block's sum, and one 64-bit atomic into its
+//                            target's entry total;
+//   cells_block_scan_kernel  one workgroup: the capacity check in target order (a target keeps its
+//                            lists while the running total fits the capacity, else ok = 0 and its
+//                            muffle rays test every collider), then the exclusive scan of the block
+//                            sums with a dropped target's blocks taken as 0 (its lists stay empty; the
+//                            fill pass skips it);
+//   cells_start_kernel       one workgroup per block: its starts, the block's offset plus the
+//                            exclusive scan of its counts.
+// The block sums and offsets sit in the cursor array, the targets' totals in `tot` (T x u64).
+__global__ __launch_bounds__(256) void cells_block_sum_kernel(CellBufs cb, unsigned long long* __restrict__ tot) {
+  static_assert((kCells * 3) % 256 == 0, "a block lies in one target");
+  __shared__ uint32_t s[4];
+  uint32_t v = cb.count[(size_t)blockIdx.x * 256 + threadIdx.x];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t sum = s[0] + s[1] + s[2] + s[3];
+    cb.cursor[blockIdx.x] = sum;
+    if (sum) atomicAdd(tot + blockIdx.x / ((kCells * 3) / 256), (unsigned long long)sum);
+  }
+}
+__global__ __launch_bounds__(1024) void cells_block_scan_kernel(CellBufs cb, int T, uint32_t blocks,
+                                                                unsigned long long* __restrict__ tot) {
+  __shared__ uint32_t s_keep[kMaxTargets];
+  __shared__ uint32_t s_w[16];
+  constexpr uint32_t kPerT = (kCells * 3) / 256;  // blocks per target
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) {
+    unsigned long long run = 0ull;
+    for (int t = 0; t < T; ++t) {
+      const unsigned long long c = tot[t];
+      const bool keep = cb.ok[t] && run + c <= (unsigned long long)cb.cap;
+      if (keep) run += c;
+      else cb.ok[t] = 0u;
+      s_keep[t] = keep ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  // thread i scans blocks [i * per, (i + 1) * per) (the kept total is at most cap < 2^32)
+  const uint32_t per = (blocks + 1023u) / 1024u, b0 = min(blocks, (uint32_t)tid * per), b1 = min(blocks, b0 + per);
+  uint32_t sum = 0u;
+  for (uint32_t b = b0; b < b1; ++b) sum += s_keep[b / kPerT] ? cb.cursor[b] : 0u;
+  uint32_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (int k = 0; k < w; ++k) run += s_w[k];
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t v = s_keep[b / kPerT] ? cb.cursor[b] : 0u;
+    cb.cursor[b] = run;  // the block's offset
+    run += v;
+  }
+  if (b1 == blocks && b0 < b1) cb.start[(size_t)blocks * 256] = run;  // the sentinel: every kept entry
+  if (blocks == 0 && tid == 0) cb.start[0] = 0u;
+}
+__global__ __launch_bounds__(256) void cells_start_kernel(CellBufs cb) {
+  __shared__ uint32_t s[4];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t v = cb.ok[blockIdx.x / ((kCells * 3) / 256)] ? cb.count[i] : 0u;
+  uint32_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s[w] = inc;
+  __syncthreads();
+  uint32_t base = cb.cursor[blockIdx.x];
+  for (int k = 0; k < w; ++k) base += s[k];
+  cb.start[i] = base + inc - v;
+}
+
+size_t cells_scan_temp_bytes(int T, uint32_t cap) {  // (no library scratch since round 5: cells_block_scan_kernel)
+  (void)T;
+  (void)cap;
+  return 0;
 }
 
 // Entry capacity: 128 cells per (target, collider) on average (a collider near its target spans
@@ -387,27 +486,22 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   if (pairs > 0) {
     hipLaunchKernelGGL(cells_row_kernel<false>, dim3(row_grid(T, n)), dim3(256), 0, st, geo, T, cb, n);
   }
-  if (T > 0) hipLaunchKernelGGL(cells_total_kernel, dim3((unsigned)cells / 256), dim3(256), 0, st, cb);
-  if (T > 0) hipLaunchKernelGGL(cells_drop_kernel, dim3((cells + 255) / 256), dim3(256), 0, st, cb, T, (uint32_t)cells);
-  size_t bytes = cb.temp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(cb.temp, bytes, cb.count, cb.start, cells + 1, st) != hipSuccess) return -1;
+  // per-target totals, the capacity check and the list starts (three launches)
+  {
+    const uint32_t blocks = (uint32_t)cells / 256u;
+    unsigned long long* tot = cb.tcount;  // (zeroed by cells_geo_kernel)
+    if (blocks) hipLaunchKernelGGL(cells_block_sum_kernel, dim3(blocks), dim3(256), 0, st, cb, tot);
+    hipLaunchKernelGGL(cells_block_scan_kernel, dim3(1), dim3(1024), 0, st, cb, T, blocks, tot);
+    if (blocks) hipLaunchKernelGGL(cells_start_kernel, dim3(blocks), dim3(256), 0, st, cb);
+  }
   if (pairs > 0)
     hipLaunchKernelGGL(cells_row_kernel<true>, dim3(row_grid(T, n)), dim3(256), 0, st, geo, T, cb, n);
   // each cell's entries by ascending near bound: muffle_kernel stops at the first one past its
-  // segment (the segments are the starts themselves: every start is <= cap after the drop pass)
-  {
-    size_t sbytes = cb.temp_bytes;
-    const hipError_t e =
-        cb.compact ? hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
-                                                                 reinterpret_cast<const uint32_t*>(cb.ent),
-                                                                 reinterpret_cast<uint32_t*>(cb.ent_s), (int)cb.cap, cells,
-                                                                 cb.start, cb.start + 1, 0, 16, st)
-                   : hipcub::DeviceSegmentedRadixSort::SortPairs(cb.temp, sbytes, cb.keys, cb.keys + cb.cap,
-                                                                 reinterpret_cast<const unsigned long long*>(cb.ent),
-                                                                 reinterpret_cast<unsigned long long*>(cb.ent_s), (int)cb.cap,
-                                                                 cells, cb.start, cb.start + 1, 0, 16, st);
-    if (e != hipSuccess) return -1;
-  }
+  // segment (every start is <= cap after the drop pass)
+  if (cb.compact)
+    hipLaunchKernelGGL(cells_sort_kernel<true>, dim3((unsigned)((cells + 3) / 4)), dim3(256), 0, st, cb, cells);
+  else
+    hipLaunchKernelGGL(cells_sort_kernel<false>, dim3((unsigned)((cells + 3) / 4)), dim3(256), 0, st, cb, cells);
   if (env_ll("ART_DEBUG_CELLS", 0)) {  // diagnostics: the built lists' size and length histogram (synchronizes)
     std::vector<uint32_t> hs((size_t)cells + 1);
     if (hipMemcpyAsync(hs.data(), cb.start, hs.size() * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&

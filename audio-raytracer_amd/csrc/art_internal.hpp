@@ -161,16 +161,16 @@ struct CellBufs {
   float alpha_max;                // largest cone half-angle (with slack)
   uint32_t* count;                // [T * kCells * 3 + 1] entries per (cell, collider type)
   uint32_t* start;                // [T * kCells * 3 + 1] exclusive scan of count (DevScene::cell_start)
-  uint32_t* cursor;               // [T * kCells * 3 + 1] fill positions, then the sort's segment offsets
+  uint32_t* cursor;               // [T * kCells * 3 + 1] scratch: the 256-counter block sums, then their offsets
   uint2* ent;                     // [cap] in fill order
   uint2* ent_s;                   // [cap] each cell's entries by ascending near bound (DevScene::cell_ent)
   uint32_t compact;               // 4-B entries in the same storage (DevScene::cell_compact)
   uint32_t* keys;                 // [2 * cap] sort keys (near_key) and their sorted copy
   float* far;                     // [T]: distance bound of t's segments
   uint32_t* ok;                   // [T]
-  unsigned long long* tcount;     // [T] entries per target (count pass), for the capacity check
+  unsigned long long* tcount;     // [T] entries per target (cells_block_sum_kernel), for the capacity check
   uint32_t cap;                   // entry capacity; 0: no lists (cells_enabled false), every muffle ray tests every collider
-  void* temp; size_t temp_bytes;  // hipcub scan / segmented sort storage
+  void* temp; size_t temp_bytes;  // (unused since round 5: no library scan or sort)
   void* geo;                      // [T * C] per-(target, collider) geometry (cells_geo_bytes)
 };
 size_t cells_scan_temp_bytes(int T, uint32_t cap);

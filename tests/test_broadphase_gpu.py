@@ -385,3 +385,31 @@ def test_kd_wave_pass_builds_the_same_tree(monkeypatch, cfg_index, C_scale):
     for key in ("00",):
         assert np.array_equal(orders[key], orders["10"]), (key, int((orders[key] != orders["10"]).sum()))
         assert all(outs[key].equal(outs["10"]).values()), key
+
+
+@pytest.mark.parametrize("H,hits", [(1, False), (2, True)])
+def test_cell_lists_long_and_mid(ctx, monkeypatch, capfd, H, hits):
+    """Muffle direction-cell lists longer than the cells sort's register paths (art_cells.hip
+    cells_sort_kernel: <= 64 entries one per lane, <= 256 several per lane, longer ones from memory):
+    a cluster of 700 small spheres and one of 160 small boxes, each seen from the targets through a
+    few cells, so those cells list hundreds of colliders; the muffle rays crossing them must still
+    equal the brute-force oracle (CanRaySeeAudioTarget :405-449), through the bench's plan (H = 1, no
+    hit outputs: echo_muffle_kernel) and the multi-hit plan with hit outputs."""
+    monkeypatch.setenv("ART_DEBUG_CELLS", "1")
+    rng = np.random.default_rng(2024)
+    R = 256
+    dirs = fib_dirs(R)
+    sph = spheres(np.array([12.0, 0.0, 0.0]) + rng.uniform(-1.2, 1.2, (700, 3)), rng.uniform(0.05, 0.15, 700), rng)
+    box = aabbs(np.array([0.0, 14.0, 0.0]) + rng.uniform(-1.0, 1.0, (160, 3)), rng.uniform(0.05, 0.2, (160, 3)), rng)
+    walls = aabbs(np.array([[30.0, 0, 0], [-30.0, 0, 0], [0, 30.0, 0], [0, -30.0, 0], [0, 0, 30.0], [0, 0, -30.0]]),
+                  np.array([[1.0, 40, 40], [1.0, 40, 40], [40, 1.0, 40], [40, 1.0, 40], [40, 40, 1.0], [40, 40, 1.0]]), rng)
+    targets = np.array([[-2.0, 0.5, 0.3], [0.5, -3.0, 0.2], [1.0, 1.0, -2.0]], np.float32)
+    org = np.array([[20.0, 2.0, 1.0], [3.0, 22.0, -1.0], [18.0, 10.0, 5.0], [-10.0, -10.0, 8.0]], np.float32)
+    scene = art.Scene(dirs=dirs, targets=targets, spheres=sph, aabbs=np.concatenate([box, walls]))
+    params = art.FrameParams(max_hits_per_ray=H, max_ray_life=1e4, max_muffle_hit_distance=1e5,
+                             stages=abi.ART_STAGE_RAYTRACE | abi.ART_STAGE_REDUCE)
+    out, _ = gpu_vs_oracle(ctx, scene, params, org, hits=hits, counts=False)
+    assert (out.muffle != 0).any()
+    err = capfd.readouterr().err
+    longest = max(int(l.split("longest ")[1].split(";")[0]) for l in err.splitlines() if "[cells]" in l)
+    assert longest > 256, err[-2000:]
