@@ -1301,15 +1301,10 @@ __device__ __forceinline__ bool muffle_blocked(const DevScene& sc, vec3 off, vec
 template <bool EX, bool OBB, bool HM>
 __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParams& fp, const VisPairs& vp,
                                             const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
-                                            const EchoFromHits& eh, uint32_t i, int by, int gy, uint32_t rec0 = 0u,
-                                            uint32_t nrec = 0u) {
+                                            const EchoFromHits& eh, uint32_t i, int by, int gy) {
   const int lane = threadIdx.x & 63;
-  // (fixed slots: every bounce's records, kNoRecord marking the slots with no hit; nrec > 0: the
-  // records [rec0, rec0 + nrec) only, one bounce's fixed slots)
-  i += rec0;
-  const uint32_t n = nrec ? rec0 + nrec
-                          : (HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u
-                                : (vp.fixed ? vp.fixed * (uint32_t)fp.H : ldc(count, 1)));
+  // (fixed slots: every bounce's records, kNoRecord marking the slots with no hit)
+  const uint32_t n = HM ? (uint32_t)fp.S * (uint32_t)((fp.R + 63) >> 6) * 64u : (vp.fixed ? vp.fixed * (uint32_t)fp.H : ldc(count, 1));
   if (__builtin_amdgcn_readfirstlane(i - (uint32_t)lane) >= n) return;
   bool valid = i < n;
   vec3 off = mk3(0.0f, 0.0f, 0.0f);
@@ -1379,9 +1374,8 @@ __device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uin
 template <bool EX, bool OBB, bool HM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EX && OBB ? 7 : 8))) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
                                                      const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
-                                                     EchoFromHits eh, uint32_t rec0, uint32_t nrec) {
-  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x * 256u + threadIdx.x, (int)blockIdx.y, (int)gridDim.y, rec0,
-                           nrec);
+                                                     EchoFromHits eh) {
+  muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x * 256u + threadIdx.x, (int)blockIdx.y, (int)gridDim.y);
 }
 
 // One-hit frames with one batch slot and no path kernel (HM2): the echo traversal and the muffle
@@ -1736,11 +1730,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   const unsigned mblocks = hm2 ? (groups + 3) / 4
                                : (unsigned)(((fold ? (size_t)groups * 64 * fp.H : hcap) + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over the grid (the rest looped)
-  unsigned mb_ = mblocks;                                      // muffle launch: blocks, first record, records (0: all)
-  uint32_t rec0_ = 0u, nrec_ = 0u;
 #define ART_MUFFLE(S_, EX_, OBB_, HM_)                                                                                  \
-  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), dim3(mb_, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, \
-                     muffle_acc, eh, rec0_, nrec_)
+  hipLaunchKernelGGL((muffle_kernel<EX_, OBB_, HM_>), dim3(mblocks, mt), dim3(256), 0, S_, sc, fp, pb.vp, pair_count, \
+                     muffle_acc, eh)
 #define ART_MUFFLE_ANY(S_)                                                                                             \
   do {                                                                                                                 \
     if (hm2) {                                                                                                         \
@@ -1759,13 +1751,6 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // echo traversal on st, the muffle kernel on the side stream (the longer kernel stays on st: a
   // fork costs ~10 us before the side stream starts). Without a side stream everything runs on st.
   const bool per_bounce = split && multi && ecnt;
-  // folded frames: each bounce's muffle rays on the side stream after its echo traversal (beside the
-  // next bounces' nearest traversals) instead of one muffle launch after the last bounce
-  static const bool muffle_each = [] {
-    const char* e = getenv("ART_MUFFLE_PER_BOUNCE");
-    return e && e[0] == '1';
-  }();
-  const bool muffle_per_bounce = per_bounce && fold && muffle_each;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
 #define ART_NEAREST(EX_, OBB_, F_)                                                                                  \
   hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order,      \
@@ -1797,16 +1782,9 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
       (void)hipEventRecord(echo.fork, st);
       (void)hipStreamWaitEvent(echo.st, echo.fork, 0);
       marked(marks, kMarkEcho, echo.st, [&] { ART_VIS_ANY(echo.st, groups, k, false); });
-      if (muffle_per_bounce) {  // this bounce's fixed slots: groups * 64 records from k * fixed
-        mb_ = (groups * 64u + 255u) / 256u;
-        rec0_ = (uint32_t)k * pb.vp.fixed;
-        nrec_ = pb.vp.fixed;
-        marked(marks, kMarkMuffle, echo.st, [&] { ART_MUFFLE_ANY(echo.st); });
-      }
     }
   }
-  if (muffle_per_bounce) {
-  } else if (per_bounce) {
+  if (per_bounce) {
     marked(marks, kMarkMuffle, st, [&] { ART_MUFFLE_ANY(st); });  // the bounces' echoes are already on the side stream
   } else if (fused) {
 #define ART_ECHO_MUFFLE(EX_, OBB_)                                                                                    \
