@@ -27,6 +27,9 @@
 namespace art {
 
 constexpr int kNoHit = 0x7fffffff;
+#ifndef ART_MEASURE_PARTS
+#define ART_MEASURE_PARTS 0  // (measurement builds only, wrong outputs: 1 = no muffle rays in echo_muffle_kernel, 2 = no echo rays)
+#endif
 constexpr int kNoOwner = 0x7fffffff;  // echo rays skip no collider (AudioTargetId is 16-bit)
 
 // Sphere test split so the common miss costs no branch: the square root and the two IEEE
@@ -1390,6 +1393,7 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
                         uint32_t groups, uint32_t mblocks, int mt) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
   if (blockIdx.x < groups) {
+    if (ART_MEASURE_PARTS == 2) return;
     vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, nullptr, -1, block, eh);
     return;
   }
@@ -1727,7 +1731,7 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // ... and the two as one launch on st (echo_muffle_kernel)
   const bool fused = hm2;
   eh.no_path = hm2 ? 1 : 0;
-  const unsigned mblocks = hm2 ? (groups + 3) / 4
+  const unsigned mblocks = (ART_MEASURE_PARTS == 1 && hm2) ? 0u : hm2 ? (groups + 3) / 4
                                : (unsigned)(((fold ? (size_t)groups * 64 * fp.H : hcap) + 255) / 256);  // ray slots / hit records
   const unsigned mt = (unsigned)std::min(fp.T, 64);           // targets over the grid (the rest looped)
 #define ART_MUFFLE(S_, EX_, OBB_, HM_)                                                                                  \
