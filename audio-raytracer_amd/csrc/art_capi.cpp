@@ -973,9 +973,15 @@ ART_API int art_create_on(const int32_t* device_ids, int32_t count, art_ctx** ou
 #ifdef ART_DIAG
 void art_diag_dump_impl();
 #endif
+#ifdef ART_WAVE_TIMES
+extern "C" void art_wave_times_dump_impl();
+#endif
 ART_API void art_destroy(art_ctx* c) {
 #ifdef ART_DIAG
   if (c && !c->devs.empty()) art_diag_dump_impl();
+#endif
+#ifdef ART_WAVE_TIMES
+  if (c && !c->devs.empty()) art_wave_times_dump_impl();
 #endif
   if (!c) return;
   if (c->cpu) {

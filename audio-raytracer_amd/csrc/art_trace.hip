@@ -72,6 +72,36 @@ __device__ __forceinline__ void diag_add(int k, unsigned long long v) {
 #define ART_DIAG_STEP(x) ((void)0)
 #endif
 
+#ifdef ART_WAVE_TIMES
+// Diagnostic build only (tools/build_variant.sh wt -DART_WAVE_TIMES): every wave of the nearest and
+// echo+muffle launches appends (start | kind << 60, end) in wall-clock ticks (100 MHz) and its
+// (block, HW_ID, XCC_ID) to a ring that art_destroy writes to $ART_WAVE_TIMES_OUT
+// (tools/wave_times.py reads it): the launches' wave timelines, per-XCD tails included.
+constexpr unsigned kWtCap = 1u << 16;
+__device__ unsigned long long g_wt[kWtCap][2];
+__device__ uint32_t g_wt_id[kWtCap][3];
+__device__ unsigned g_wt_n;
+struct WaveTimer {
+  unsigned long long t0;
+  unsigned kind;
+  __device__ explicit WaveTimer(unsigned k) : t0(wall_clock64()), kind(k) {}
+  __device__ ~WaveTimer() {
+    const unsigned long long t1 = wall_clock64();
+    if ((threadIdx.x & 63) == 0) {
+      const unsigned i = atomicAdd(&g_wt_n, 1u) % kWtCap;
+      g_wt[i][0] = t0 | ((unsigned long long)kind << 60);
+      g_wt[i][1] = t1;
+      g_wt_id[i][0] = blockIdx.x | (threadIdx.x >> 6) << 24;
+      g_wt_id[i][1] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_ID
+      g_wt_id[i][2] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // XCC_ID
+    }
+  }
+};
+#define ART_WAVE_TIMER(k) WaveTimer art_wave_timer_(k)
+#else
+#define ART_WAVE_TIMER(k) ((void)0)
+#endif
+
 // A ray whose direction or origin is non-finite, or whose direction is zero, makes every box test
 // inconclusive: its traversals visit every node (the exact tests alone decide).
 __device__ __forceinline__ bool force_all(const Seg& s, float om) {
@@ -573,6 +603,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   __shared__ uint32_t s_stk[kBvhStack * 64];
   __shared__ int s_bound[64];
   __shared__ unsigned long long s_key[64];
+  ART_WAVE_TIMER(0);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
   const int ngroups = fp.S * nrb;
@@ -1392,6 +1423,7 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
                         unsigned long long* ex, uint8_t* __restrict__ block, EchoFromHits eh, uint32_t* __restrict__ acc,
                         uint32_t groups, uint32_t mblocks, int mt) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
+  ART_WAVE_TIMER(blockIdx.x < groups ? 1u : 2u);
   if (blockIdx.x < groups) {
     if (ART_MEASURE_PARTS == 2) return;
     vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, nullptr, -1, block, eh);
@@ -1836,6 +1868,27 @@ extern "C" void art_diag_dump_impl() {
       if (h[k][b]) fprintf(stderr, " %d:%llu", b, h[k][b]);
     fprintf(stderr, "\n");
   }
+}
+#endif
+#ifdef ART_WAVE_TIMES
+extern "C" void art_wave_times_dump_impl() {
+  const char* path = getenv("ART_WAVE_TIMES_OUT");
+  if (!path || hipDeviceSynchronize() != hipSuccess) return;
+  static unsigned long long t[kWtCap][2];
+  static uint32_t id[kWtCap][3];
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wt), sizeof t) != hipSuccess ||
+      hipMemcpyFromSymbol(id, HIP_SYMBOL(g_wt_id), sizeof id) != hipSuccess ||
+      hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_wt_n), sizeof n) != hipSuccess)
+    return;
+  FILE* f = fopen(path, "wb");
+  if (!f) return;
+  const unsigned cap = kWtCap;
+  fwrite(&n, sizeof n, 1, f);
+  fwrite(&cap, sizeof cap, 1, f);
+  fwrite(t, sizeof t, 1, f);
+  fwrite(id, sizeof id, 1, f);
+  fclose(f);
 }
 #endif
 }  // namespace art
