@@ -74,13 +74,13 @@ __device__ __forceinline__ void diag_add(int k, unsigned long long v) {
 
 #ifdef ART_WAVE_TIMES
 // Diagnostic build only (tools/build_variant.sh wt -DART_WAVE_TIMES): every wave of the nearest and
-// echo+muffle launches appends (start | kind << 60, end) in wall-clock ticks (100 MHz) and its
-// (block, HW_ID, XCC_ID) to a ring that art_destroy writes to $ART_WAVE_TIMES_OUT
-// (tools/wave_times.py reads it): the launches' wave timelines, per-XCD tails included.
-constexpr unsigned kWtCap = 1u << 16;
+// echo+muffle launches writes (start | kind << 60, end) in wall-clock ticks and its (block, HW_ID,
+// XCC_ID) to its own slot (nearest waves in the first half, echo+muffle waves in the second; no
+// atomics, each frame overwrites the previous one's), which art_destroy writes to
+// $ART_WAVE_TIMES_OUT (tools/wave_times.py reads it): the launches' wave timelines of the last frame.
+constexpr unsigned kWtCap = 1u << 18;
 __device__ unsigned long long g_wt[kWtCap][2];
 __device__ uint32_t g_wt_id[kWtCap][3];
-__device__ unsigned g_wt_n;
 struct WaveTimer {
   unsigned long long t0;
   unsigned kind;
@@ -88,7 +88,7 @@ struct WaveTimer {
   __device__ ~WaveTimer() {
     const unsigned long long t1 = wall_clock64();
     if ((threadIdx.x & 63) == 0) {
-      const unsigned i = atomicAdd(&g_wt_n, 1u) % kWtCap;
+      const unsigned i = (kind ? kWtCap / 2 : 0u) + (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % (kWtCap / 2);
       g_wt[i][0] = t0 | ((unsigned long long)kind << 60);
       g_wt[i][1] = t1;
       g_wt_id[i][0] = blockIdx.x | (threadIdx.x >> 6) << 24;
@@ -1876,16 +1876,18 @@ extern "C" void art_wave_times_dump_impl() {
   if (!path || hipDeviceSynchronize() != hipSuccess) return;
   static unsigned long long t[kWtCap][2];
   static uint32_t id[kWtCap][3];
-  unsigned n = 0;
+  const unsigned n = 0;  // (header word kept for the reader)
   if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wt), sizeof t) != hipSuccess ||
-      hipMemcpyFromSymbol(id, HIP_SYMBOL(g_wt_id), sizeof id) != hipSuccess ||
-      hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_wt_n), sizeof n) != hipSuccess)
+      hipMemcpyFromSymbol(id, HIP_SYMBOL(g_wt_id), sizeof id) != hipSuccess)
     return;
   FILE* f = fopen(path, "wb");
   if (!f) return;
   const unsigned cap = kWtCap;
+  int dev = 0, khz = 0;  // wall-clock rate
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) khz = 0;
   fwrite(&n, sizeof n, 1, f);
   fwrite(&cap, sizeof cap, 1, f);
+  fwrite(&khz, sizeof khz, 1, f);
   fwrite(t, sizeof t, 1, f);
   fwrite(id, sizeof id, 1, f);
   fclose(f);
