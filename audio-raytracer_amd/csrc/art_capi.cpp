@@ -57,6 +57,11 @@ constexpr uint32_t kAbiVersion = (3u << 16) | 0u;
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
 
+#ifndef ART_CELLS_BESIDE_BVH
+#define ART_CELLS_BESIDE_BVH 1
+#endif
+constexpr bool kCellsBesideBvh = ART_CELLS_BESIDE_BVH != 0;
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -105,7 +110,7 @@ struct Frame {
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
   size_t soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0, soa_kd = 0;
   // muffle candidate lists (art_cells.hip)
-  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, soa_ctot = 0, cells_temp = 0,
+  size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, soa_ctot = 0, soa_cbox = 0, cells_temp = 0,
          soa_cgeo = 0;
   uint32_t cells_cap = 0;
 };
@@ -450,6 +455,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_cfar = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_cok = s; s = align_up(s + (size_t)f.T * 4, 256);
     f.soa_ctot = s; s = align_up(s + (size_t)f.T * 8, 256);
+    f.soa_cbox = s; s = align_up(s + sizeof(CullRec), 256);
     f.soa_ctemp = s; s = align_up(s + f.cells_temp, 256);
     f.soa_cent = s; s = align_up(s + (size_t)f.cells_cap * 8, 256);
     f.soa_cgeo = s; s = align_up(s + cells_geo_bytes(f.T, f.ns + f.na + f.no), 256);
@@ -574,27 +580,29 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sb.kd = kd_scratch_bytes(f.ns + f.na + f.no) ? soa + f.soa_kd : nullptr;
   sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
   dv.sb = sb;
+  // The cell lists need only the decoded colliders and the targets (cells_box_kernel gives their
+  // distance bound), the BVH only the colliders: with a rebuilt BVH the lists build on the side
+  // stream beside it (its surface-area passes occupy a few CUs for ~70 us), joined before the frame.
+  hipStream_t cells_st = dv.stream;
   {
-    const bool reuse = f.resident && dv.sorted_gen != ~0ull && dv.sorted_soa == dv.soa.p && dv.sorted_n[0] == f.ns &&
-                       dv.sorted_n[1] == f.na && dv.sorted_n[2] == f.no;
-    if (reuse) {  // same resident colliders (or only moved ones): keep the orders, refit if needed
-      const DevScene& o = dv.sorted_sc;
-      sc.bvh = o.bvh; sc.bvh_ref = o.bvh_ref; sc.bvh_leaf = o.bvh_leaf;
-      sc.bvh_levels = o.bvh_levels; sc.bvh_leaf0 = o.bvh_leaf0;
-      if (dv.sorted_gen != c->sync_gen && launch_refit_scene(sc, sb, dv.stream) != 0)
-        return fail(c, ART_E_DEVICE, "collider refit failed");
-    } else if (launch_sort_scene(sc, sb, dv.stream) != 0) {
-      return fail(c, ART_E_DEVICE, "collider sort failed");
-    }
-    dv.sorted_gen = f.resident ? c->sync_gen : ~0ull;
-    dv.sorted_soa = dv.soa.p;
-    dv.sorted_n[0] = f.ns; dv.sorted_n[1] = f.na; dv.sorted_n[2] = f.no;
-  }
-  {  // muffle candidate lists for these colliders and targets
     if (!dv.cones.p) {
       if (!dv.cones.reserve(sizeof(CellCone) * kCells)) return fail(c, ART_E_NOMEM, "device allocation failed");
       HIP_TRY(c, hipMemcpyAsync(dv.cones.p, cone_table().cone, sizeof(CellCone) * kCells, hipMemcpyHostToDevice, dv.stream));
     }
+    const bool rebuild = !(f.resident && dv.sorted_gen != ~0ull && dv.sorted_soa == dv.soa.p && dv.sorted_n[0] == f.ns &&
+                           dv.sorted_n[1] == f.na && dv.sorted_n[2] == f.no);
+    if (rebuild && kCellsBesideBvh && f.cells_cap > 0) {
+      if (!dv.side) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&dv.fork, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&dv.join, hipEventDisableTiming));
+      }
+      HIP_TRY(c, hipEventRecord(dv.fork, dv.stream));
+      HIP_TRY(c, hipStreamWaitEvent(dv.side, dv.fork, 0));
+      cells_st = dv.side;
+    }
+  }
+  auto build_cells = [&]() -> int {
     CellBufs& cb = dv.cb;
     cb.cones = static_cast<const CellCone*>(dv.cones.p);
     cb.alpha_max = cone_table().alpha_max;
@@ -614,7 +622,37 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
 #endif
     cb.compact = (ART_CELLS_COMPACT && f.ns < (1 << 16) && f.na < (1 << 16) && f.no < (1 << 16)) ? 1u : 0u;  // 4-B entries
     cb.geo = soa + f.soa_cgeo;
-    if (launch_build_cells(sc, cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
+    cb.box = reinterpret_cast<CullRec*>(soa + f.soa_cbox);
+    if (launch_build_cells(sc, cb, cells_st) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
+    return 0;
+  };
+  auto build_bvh = [&]() -> int {
+    const bool reuse = f.resident && dv.sorted_gen != ~0ull && dv.sorted_soa == dv.soa.p && dv.sorted_n[0] == f.ns &&
+                       dv.sorted_n[1] == f.na && dv.sorted_n[2] == f.no;
+    if (reuse) {  // same resident colliders (or only moved ones): keep the orders, refit if needed
+      const DevScene& o = dv.sorted_sc;
+      sc.bvh = o.bvh; sc.bvh_ref = o.bvh_ref; sc.bvh_leaf = o.bvh_leaf;
+      sc.bvh_levels = o.bvh_levels; sc.bvh_leaf0 = o.bvh_leaf0;
+      if (dv.sorted_gen != c->sync_gen && launch_refit_scene(sc, sb, dv.stream) != 0)
+        return fail(c, ART_E_DEVICE, "collider refit failed");
+    } else if (launch_sort_scene(sc, sb, dv.stream) != 0) {
+      return fail(c, ART_E_DEVICE, "collider sort failed");
+    }
+    dv.sorted_gen = f.resident ? c->sync_gen : ~0ull;
+    dv.sorted_soa = dv.soa.p;
+    dv.sorted_n[0] = f.ns; dv.sorted_n[1] = f.na; dv.sorted_n[2] = f.no;
+    return 0;
+  };
+  {  // the BVH's launches first: its first kernels reach the CUs before the lists' wide passes fill them
+    int rc = build_bvh();
+    if (rc == 0) rc = build_cells();
+    if (rc) return rc;
+  }
+  if (cells_st != dv.stream) {  // the frame's kernels wait for the lists
+    HIP_TRY(c, hipEventRecord(dv.join, cells_st));
+    HIP_TRY(c, hipStreamWaitEvent(dv.stream, dv.join, 0));
+  }
+  {
     dv.sorted_sc = sc;
     if (f.resident) snapshot_cell_base(c);  // the store's synced records (clean unless edited since)
     else c->cell_base_ok = false;

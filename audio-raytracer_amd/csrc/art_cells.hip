@@ -51,10 +51,48 @@ __device__ __forceinline__ float cells_far_of(const CullRec& root, vec3 tg) {
   return sqrtf(dx * dx + dy * dy + dz * dz) * 1.001f + 1e-3f;
 }
 
-// far_t of target t, or INFINITY (no BVH or non-finite colliders: every muffle ray of t tests
-// every collider)
-__device__ __forceinline__ float cells_far_t(const DevScene& sc, int t) {
-  return sc.bvh_levels > 0 ? cells_far_of(sc.bvh[0], load3(sc.targets, t)) : INFINITY;
+// far_t of target t from the colliders' bounds box (cells_box_kernel: the box the BVH root holds),
+// or INFINITY (no colliders or non-finite ones: every muffle ray of t tests every collider)
+__device__ __forceinline__ float cells_far_t(const DevScene& sc, const CellBufs& cb, int t) {
+  const CullRec& b = cb.box[0];
+  return (b.lox == INFINITY && b.hix == INFINITY) ? INFINITY : cells_far_of(b, load3(sc.targets, t));
+}
+
+// The union of every collider's cull bounds (fminf / fmaxf, as the BVH's nodes; no colliders: the
+// empty box at +infinity, as cull_stored), so the lists need no BVH and build beside it. One
+// workgroup.
+__global__ __launch_bounds__(1024) void cells_box_kernel(const CullRec* __restrict__ cull, int n, CullRec* __restrict__ box) {
+  __shared__ float s[6][16];
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const CullRec c = cull[i];
+    v[0] = fminf(v[0], c.lox); v[1] = fminf(v[1], c.loy); v[2] = fminf(v[2], c.loz);
+    v[3] = fmaxf(v[3], c.hix); v[4] = fmaxf(v[4], c.hiy); v[5] = fmaxf(v[5], c.hiz);
+  }
+  for (int q = 0; q < 6; ++q)
+    for (int m = 32; m >= 1; m >>= 1) {
+      const float o = __shfl_xor(v[q], m, 64);
+      v[q] = q < 3 ? fminf(v[q], o) : fmaxf(v[q], o);
+    }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int q = 0; q < 6; ++q) s[q][w] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (int)(blockDim.x >> 6);
+    for (int q = 0; q < 6; ++q) {
+      v[q] = s[q][0];
+      for (int k = 1; k < nw; ++k) v[q] = q < 3 ? fminf(v[q], s[q][k]) : fmaxf(v[q], s[q][k]);
+    }
+    CullRec r;
+    r.fscale = 0.0f; r.factor = 0.0f;
+    if (!(v[0] > v[3])) {
+      r.lox = v[0]; r.loy = v[1]; r.loz = v[2]; r.hix = v[3]; r.hiy = v[4]; r.hiz = v[5];
+    } else {
+      r.lox = r.loy = r.loz = r.hix = r.hiy = r.hiz = INFINITY;
+    }
+    box[0] = r;
+  }
 }
 
 // Global collider g (spheres, AABBs, OBBs): its order code and AudioTargetId.
@@ -119,7 +157,7 @@ __global__ __launch_bounds__(256) void cells_geo_kernel(DevScene sc, CellBufs cb
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < items; k += (long long)gridDim.x * blockDim.x) {
     if (k < counters) cb.count[k] = 0u;
     if (k < T) {
-      const float v = cells_far_t(sc, (int)k);
+      const float v = cells_far_t(sc, cb, (int)k);
       cb.far[k] = v;
       cb.ok[k] = isfinite(v) ? 1u : 0u;
       cb.tcount[k] = 0ull;
@@ -139,7 +177,7 @@ __device__ void cells_geo_one(const DevScene& sc, const CellBufs& cb, int n, int
   G.all = 0u;
   G.ux = G.uy = G.uz = G.sb = G.cb = G.near = 0.0f;
   // owned by the target (its muffle rays skip it, :413, :426, :439) or no lists: no cells
-  const float far = cells_far_t(sc, t);  // (cb.far[t], written by another work-item of this launch)
+  const float far = cells_far_t(sc, cb, t);  // (cb.far[t], written by another work-item of this launch)
   if (!isfinite(far) || tid == t) { geo[k] = G; cell_rects_write(geo, T, n, t, g, G); return; }
   // The collider's bounding sphere and its error margin. Every test's rounding is relative to the
   // segment-start-to-collider vector (the operands o and the record are exact floats): a reported
@@ -481,6 +519,7 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
   }
   const long long pairs = (long long)n * T;
   CellGeo* geo = reinterpret_cast<CellGeo*>(cb.geo);
+  hipLaunchKernelGGL(cells_box_kernel, dim3(1), dim3(1024), 0, st, sc.cull, n, cb.box);
   hipLaunchKernelGGL(cells_geo_kernel, dim3(stride_grid(std::max(pairs, (long long)cells + 1))), dim3(256), 0, st, sc, cb, T,
                      geo, (uint32_t)cells + 1);
   if (pairs > 0) {

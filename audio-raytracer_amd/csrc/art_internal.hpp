@@ -172,6 +172,7 @@ struct CellBufs {
   uint32_t cap;                   // entry capacity; 0: no lists (cells_enabled false), every muffle ray tests every collider
   void* temp; size_t temp_bytes;  // (unused since round 5: no library scan or sort)
   void* geo;                      // [T * C] per-(target, collider) geometry (cells_geo_bytes)
+  CullRec* box;                   // [1] the union of the colliders' bounds (cells_box_kernel: the BVH root's box)
 };
 size_t cells_scan_temp_bytes(int T, uint32_t cap);
 size_t cells_geo_bytes(int T, int C);
