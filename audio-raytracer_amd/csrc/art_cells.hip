@@ -324,8 +324,8 @@ __global__ __launch_bounds__(256) void cells_row_kernel(CellGeo* __restrict__ ge
 // keys by fill position) and scattered into the sorted array: a list of at most 64 entries holds one
 // entry per lane and broadcasts the keys by readlane; up to kCellSortReg entries, each lane holds
 // several; a longer list reads the keys from memory (O(n^2 / 64) per wave; no list of configs 2-5
-// comes near: config 2's longest has 29 entries, config 4's fewer than 128, ART_DEBUG_CELLS
-// histograms in DESIGN.md §4). (Round 4 sorted every list with a segmented radix sort: 51 us of a
+// comes near: the longest lists have 29 / 64 / 48 / 26 entries at configs 2 / 3 / 4 / 5,
+// ART_DEBUG_CELLS histograms in profiles/r05_cell_lists.txt). (Round 4 sorted every list with a segmented radix sort: 51 us of a
 // config-2 rebuild frame.)
 constexpr int kCellSortReg = 256;
 template <bool COMPACT>
@@ -550,7 +550,7 @@ int launch_build_cells(DevScene& sc, const CellBufs& cb, hipStream_t st) {
       for (int i = 0; i < cells; ++i) {
         const uint32_t len = hs[(size_t)i + 1] - hs[i];
         longest = std::max(longest, len);
-        hist[len == 0 ? 0 : std::min(17, 33 - __builtin_clz(len))]++;
+        hist[len == 0 ? 0 : std::min(17, 32 - __builtin_clz(len))]++;
       }
       fprintf(stderr, "[cells] T %d colliders %d: %u entries (capacity %u, %.1f per pair), %d lists, longest %u; lengths", T,
               n, hs[(size_t)cells], cb.cap, (double)hs[(size_t)cells] / std::max(1ll, pairs), cells, longest);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One rebuild frame's GPU timeline (kernels and copies, per stream) from tools/rebuild_trace.sh.
 
-    python3 tools/rebuild_timeline.py gpurun_out/rebuild/trace [frame_from_end]"""
+    python3 tools/rebuild_timeline.py gpurun_out/rebuild/trace [frame_from_end] [first_kernel]"""
 import csv
 import os
 import sys
@@ -19,7 +19,8 @@ def main():
         for r in csv.DictReader(open(p)):
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id", ""), "copy " + r.get("Direction", "")))
     ev.sort()
-    starts = [i for i, e in enumerate(ev) if e[3].startswith("prep_kernel")]
+    first = sys.argv[3] if len(sys.argv) > 3 else "prep_kernel"  # (static frames: nearest_first_kernel)
+    starts = [i for i, e in enumerate(ev) if e[3].startswith(first)]
     a, b = starts[-back], starts[-back + 1]
     while a > 0 and ev[a - 1][3].startswith("copy") and "HOST_TO_DEVICE" in ev[a - 1][3]:
         a -= 1
