@@ -294,15 +294,15 @@ constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
 #ifndef ART_ECHO_MUFFLE_OBB_WAVES
 #define ART_ECHO_MUFFLE_OBB_WAVES 8
 #endif
-// k-th (0-based) set bit of m, k < popcount(m).
-__device__ __forceinline__ int select_bit(unsigned long long m, int k) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const int c = __popcll((m >> pos) & ((1ull << w) - 1ull));
-    if (k >= c) { k -= c; pos += w; }
-  }
-  return pos;
+// Work sharing's pairing: the quad base lane (l4) of the donor whose rank among the donors equals
+// this thief's rank ir. Two cross-lane moves instead of a select-bit search: lane 0 of each robbed
+// donor (rank dr) forwards its l4 to lane 4 dr + 1 (ds_permute; every other lane writes into a
+// 4k + 2 lane nobody reads), then each lane reads lane 4 ir + 1 (ds_bpermute). Both run in every
+// lane of the wave; the caller uses the result in its thieves only.
+__device__ __forceinline__ int rank_match(int l4, int qd, bool robbed, int dr, int ir) {
+  const int dst = (robbed && qd == 0) ? 4 * dr + 1 : l4 + 2;
+  const int tab = __builtin_amdgcn_ds_permute(dst << 2, l4);
+  return __builtin_amdgcn_ds_bpermute(((4 * ir + 1) & 63) << 2, tab);
 }
 
 // (distance, order) as one ordered 64-bit key; distances are >= 0 or -0, the two zeros equal
@@ -409,7 +409,8 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
         const int ir = __popcll(idle & below), dr = __popcll(donors & below);
         const bool thief = (act >> l4 & 1ull) == 0ull && ir < __popcll(donors);
         const bool robbed = sp > bp && dr < __popcll(idle);
-        const int src = (thief ? select_bit(donors, ir) : l4) + qd;
+        const int match = rank_match(l4, qd, robbed, dr, ir);  // (every lane takes part)
+        const int src = (thief ? match : l4) + qd;
         const int dbp = __shfl(bp, src), dhome = __shfl(home, src);
         const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
         const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
@@ -1044,7 +1045,8 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       const int ir = __popcll(idle & below), dr = __popcll(donors & below);
       const bool thief = g < 0 && ir < __popcll(donors);
       const bool robbed = g >= 0 && sp > bp && dr < __popcll(idle);
-      const int src = (thief ? select_bit(donors, ir) : l4) + qd;
+      const int match = rank_match(l4, qd, robbed, dr, ir);  // (every lane takes part)
+      const int src = (thief ? match : l4) + qd;
       const int dbp = __shfl(bp, src), dhome = __shfl(home, src), downer = __shfl(owner, src);
       const float ox = __shfl(s.o.x, src), oy = __shfl(s.o.y, src), oz = __shfl(s.o.z, src);
       const float dx = __shfl(s.d.x, src), dy = __shfl(s.d.y, src), dz = __shfl(s.d.z, src);
