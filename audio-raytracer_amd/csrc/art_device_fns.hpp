@@ -79,6 +79,24 @@ ART_HD bool obb_test(const Seg& s, const ObbRec& b, quat q, float& dist) {
 
 ART_HD quat stored_q(const ObbRec& b) { quat q; q.x = b.qx; q.y = b.qy; q.z = b.qz; q.w = b.qw; return q; }
 
+// 1.0f / x bit for bit: where x's exponent field lies in [3, 251] the hardware reciprocal plus one
+// Newton step (3 instructions) equals the IEEE division for every float (checked exhaustively on
+// the GPU, tools/rcp_check.hip); the other lanes (tiny, huge, zero, inf, NaN) divide. Device only.
+#ifndef ART_FAST_RCP
+#define ART_FAST_RCP 1
+#endif
+__device__ __forceinline__ float recip_exact(float x) {
+  if (!ART_FAST_RCP) return 1.0f / x;
+  float r;
+  if (((__float_as_uint(x) >> 23) & 0xffu) - 3u <= 248u) {
+    const float a = __builtin_amdgcn_rcpf(x);
+    r = __builtin_fmaf(__builtin_fmaf(-x, a, 1.0f), a, a);
+  } else {
+    r = 1.0f / x;
+  }
+  return r;
+}
+
 // obb_test<false> with the stored rotation on the record at p, fetched in the order that keeps the
 // fewest values live (the kernels' register budget): the rotation and the rotated direction's
 // reciprocals, then the centre and the rotated origin, then the local bounds. Same operations.
@@ -88,7 +106,7 @@ __device__ __forceinline__ bool obb_test_staged(const Seg& s, const ObbRec* p, f
   quat q;
   q.x = qa.x; q.y = qa.y; q.z = qa.z; q.w = qa.w;
   const vec3 ld = qmul(q, s.d);
-  const float ix = 1.0f / ld.x, iy = 1.0f / ld.y, iz = 1.0f / ld.z;
+  const float ix = recip_exact(ld.x), iy = recip_exact(ld.y), iz = recip_exact(ld.z);
   const float4 c = v[0];
   const vec3 lo = qmul(q, s.o - mk3(c.x, c.y, c.z));
   __builtin_amdgcn_sched_barrier(0);

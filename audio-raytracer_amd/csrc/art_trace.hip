@@ -245,7 +245,7 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
     q.x = qa.w; q.y = qb.x; q.z = qb.y; q.w = qb.z;
   }
   const vec3 ld3 = qmul(q, s.d);
-  const float ix = 1.0f / ld3.x, iy = 1.0f / ld3.y, iz = 1.0f / ld3.z;
+  const float ix = recip_exact(ld3.x), iy = recip_exact(ld3.y), iz = recip_exact(ld3.z);
   const vec3 lo = qmul(q, s.o - mk3(qa.x, qa.y, qa.z));
   __builtin_amdgcn_sched_barrier(0);
   const float4 qc = ld(2), qe = ld(3);
@@ -1519,7 +1519,7 @@ __device__ __forceinline__ float leaf_loss_term(const DevScene& sc, const Seg& s
   quat q;
   q.x = qa.w; q.y = qb.x; q.z = qb.y; q.w = qb.z;
   const vec3 ld3 = qmul(q, s.d);
-  const float ix = 1.0f / ld3.x, iy = 1.0f / ld3.y, iz = 1.0f / ld3.z;
+  const float ix = recip_exact(ld3.x), iy = recip_exact(ld3.y), iz = recip_exact(ld3.z);
   const vec3 lo = qmul(q, s.o - mk3(qa.x, qa.y, qa.z));
   const float4 qc = ld(2), qe = ld(3);
   if (__float_as_int(qe.z) == t) return 0.0f;
