@@ -1107,9 +1107,9 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
 
 template <bool OBB, bool HM>
 __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs& vp, const uint32_t* count,
-                                              unsigned long long* ex, uint32_t blk, uint32_t* s_stk,
+                                              unsigned long long* ex, uint32_t blk, int w, uint32_t* s_wave,
                                               const uint32_t* ecnt, int bounce, uint8_t* block, const EchoFromHits& eh) {
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qd = lane & 3;
+  const int lane = threadIdx.x & 63, qd = lane & 3;
   const int wq = lane >> 2, slot = w * 16 + wq;                // segment of the block's 64-pair batch
   if (sc.bvh_levels == 0 && !HM) return;                       // no colliders: nothing blocks
   bool valid;
@@ -1151,7 +1151,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     }
   }
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
-  const bool visible = quad_echo_core<OBB>(sc, s, maxd, owner, valid, lane, s_stk + w * 16 * kBvhStack, nt, nnode);
+  const bool visible = quad_echo_core<OBB>(sc, s, maxd, owner, valid, lane, s_wave, nt, nnode);
   if (HM) {
     if (valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = visible ? out_val : (uint16_t)0;  // :76, :142-144
   } else if (valid && visible && qd == 0) {  // visible: the echo is stored (:142-144)
@@ -1173,7 +1173,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEchoWaves<
 void vis_kernel(DevScene sc, VisPairs vp, const uint32_t* __restrict__ count, unsigned long long* ex,
                 const uint32_t* __restrict__ ecnt, int bounce, uint8_t* __restrict__ block, EchoFromHits eh) {
   __shared__ uint32_t s_stk[64 * kBvhStack];
-  vis_quad_body<OBB, HM>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, ecnt, bounce, block, eh);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  vis_quad_body<OBB, HM>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, w, s_stk + w * 16 * kBvhStack, ecnt, bounce, block, eh);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1385,9 +1386,10 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
   }
 }
 
-// Muffle workgroup b of M ray blocks x mt targets in echo_muffle_kernel. Consecutive workgroups are
+// Muffle block b of M ray blocks x mt targets in echo_muffle_kernel (its 4 one-wave workgroups on the
+// XCD of block b, as below). Consecutive blocks are
 // dispatched to the chip's 8 XCDs in turn (each with its own L2), so when mt divides 8 the XCD of
-// workgroup b serves one target, b % 8 % mt: each L2 then holds that target's direction-cell lists
+// block b serves one target, b % 8 % mt: each L2 then holds that target's direction-cell lists
 // only, not all targets' (config 2: echo_muffle traffic 12.9 -> 10.8 MB per frame with the 4-B
 // entries). The muffle blocks there fill the echo traversal's tails; in the standalone muffle_kernel
 // the uneven work per target left XCDs idle (config 5: 171 -> 193 us), so it keeps the plain order.
@@ -1415,26 +1417,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EX && OBB ?
 }
 
 // One-hit frames with one batch slot and no path kernel (HM2): the echo traversal and the muffle
-// rays, both from the nearest hits, as one launch on the launch stream: workgroups [0, groups) are
-// the echo batches (dispatched first, one round of waves), the rest the muffle blocks (mblocks x
+// rays, both from the nearest hits, as one launch on the launch stream: workgroups [0, 4 groups) are
+// the echo batches (one wave each) (dispatched first, one round of waves), the rest the muffle blocks (mblocks x
 // mt, filling the echo traversal's tails). No side stream, so no fork / join on the frame's path.
 // With OBB tests the joint kernel runs at 6 waves per SIMD (5 counting), where it needs no spills.
+// One-wave workgroups (4 per 64-ray echo group / 256-ray muffle block), so a muffle wave can start in
+// any single wave slot an echo wave frees (with 4-wave workgroups a CU waited for 4 free slots:
+// config 3 0.1686 -> 0.1660 ms/step, config 4 1.164 -> 1.149, config 2 even); the 4 waves of a
+// group or block stay on one XCD (workgroup b runs on XCD b % 8).
 template <bool EX, bool OBB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OBB ? (EX ? 5 : ART_ECHO_MUFFLE_OBB_WAVES) : kEchoWaves<EX, OBB>)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OBB ? (EX ? 5 : ART_ECHO_MUFFLE_OBB_WAVES) : kEchoWaves<EX, OBB>)))
 void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t* __restrict__ count,
                         unsigned long long* ex, uint8_t* __restrict__ block, EchoFromHits eh, uint32_t* __restrict__ acc,
                         uint32_t groups, uint32_t mblocks, int mt) {
-  __shared__ uint32_t s_stk[64 * kBvhStack];
-  ART_WAVE_TIMER(blockIdx.x < groups ? 1u : 2u);
-  if (blockIdx.x < groups) {
+  __shared__ uint32_t s_stk[16 * kBvhStack];
+  const uint32_t b = blockIdx.x;
+  const uint32_t ne = 4u * groups;  // echo workgroups
+  ART_WAVE_TIMER(b < ne ? 1u : 2u);
+  // (group or muffle block, wave): a group's 4 waves on one XCD when the counts are multiples of 8,
+  // else consecutive
+  auto split = [](uint32_t x, uint32_t n, uint32_t& u, int& wv) {
+    if (n % 8u == 0u) {
+      const uint32_t j = x >> 3;
+      u = (j >> 2) * 8u + (x & 7u);
+      wv = (int)(j & 3u);
+    } else {
+      u = x >> 2;
+      wv = (int)(x & 3u);
+    }
+  };
+  if (b < ne) {
     if (ART_MEASURE_PARTS == 2) return;
-    vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, blockIdx.x, s_stk, nullptr, -1, block, eh);
+    uint32_t g;
+    int w;
+    split(b, groups, g, w);
+    vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, g, w, s_stk, nullptr, -1, block, eh);
     return;
   }
-  uint32_t rb;
-  int t;
-  muffle_block(blockIdx.x - groups, mblocks, mt, rb, t);  // (groups is a multiple of 8 in the bench shapes)
-  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, rb * 256u + threadIdx.x, t, mt);
+  uint32_t mb, rb;
+  int sub, t;
+  split(b - ne, mblocks * (uint32_t)mt, mb, sub);
+  muffle_block(mb, mblocks, mt, rb, t);  // (groups is a multiple of 8 in the bench shapes)
+  muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, rb * 256u + (uint32_t)sub * 64u + threadIdx.x, t, mt);
 }
 
 
@@ -1826,7 +1850,8 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
     marked(marks, kMarkMuffle, st, [&] { ART_MUFFLE_ANY(st); });  // the bounces' echoes are already on the side stream
   } else if (fused) {
 #define ART_ECHO_MUFFLE(EX_, OBB_)                                                                                    \
-  hipLaunchKernelGGL((echo_muffle_kernel<EX_, OBB_>), dim3(groups + mblocks * mt), dim3(256), 0, st, sc, fp, pb.vp,   \
+  hipLaunchKernelGGL((echo_muffle_kernel<EX_, OBB_>), dim3(4 * (groups + mblocks * mt)), dim3(64), 0, \
+                     st, sc, fp, pb.vp,   \
                      pair_count, EX_ ? fp.exec : nullptr, block, eh, muffle_acc, groups, mblocks, (int)mt)
     marked(marks, kMarkEchoMuffle, st, [&] {
       if (fp.exec) { if (obb) ART_ECHO_MUFFLE(true, true); else ART_ECHO_MUFFLE(true, false); }
