@@ -51,6 +51,7 @@ ART_CTX_FORCE_REFERENCE_ORDER = 0x4
 ART_CTX_COUNT_EXECUTED = 0x10
 ART_CTX_RESIDENT_COLLIDERS = 0x20  # art_colliders.h
 ART_CTX_TIME_EACH_KERNEL = 0x200
+ART_CTX_EVENT_EACH_LAUNCH = 0x400  # art_launch_device records its completion event (the caller may drop its stream)
 ART_KIND_SPHERE, ART_KIND_AABB, ART_KIND_OBB = 0, 1, 2
 ART_OUT_HIT_RESULTS = 0x1
 # art_fan.ray_hit_ids: ColliderType (Enums/ColliderType.cs) << 30 | index in that type's array
@@ -231,6 +232,7 @@ SIGNATURES = {
     "art_f16tof32": (C.c_float, [C.c_uint16]),
     "art_f32tof16_range": (None, [U32, U32, VP]),
     "art_f32tof16_device": (I32, [VP, U32, U32, VP, VP]),
+    "art_recip_exact_device": (I32, [VP, U32, U32, VP, VP]),
 }
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

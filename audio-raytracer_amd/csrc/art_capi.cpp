@@ -28,6 +28,7 @@
 #include "art_internal.hpp"
 #include "unity_math.hpp"
 
+#include <chrono>
 #include <cmath>
 #include <csignal>
 #include <cstdlib>
@@ -52,7 +53,7 @@ namespace {
 // art_debug_leaf_order, ART_CTX_GRAPH removed — a growth 2.3 should have made a major bump; 3.0:
 // art_kernel_times per kernel family (kernel_ms / kernel_launches / kernel_marks_dropped, 80 B),
 // ART_CTX_TIME_EACH_KERNEL.
-constexpr uint32_t kAbiVersion = (3u << 16) | 0u;
+constexpr uint32_t kAbiVersion = (3u << 16) | 1u;  // 3.1: ART_CTX_EVENT_EACH_LAUNCH, art_recip_exact_device
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 float art_f16tof32_host(uint16_t h) { return art::f16tof32(h); }
@@ -103,6 +104,7 @@ struct Frame {
   std::vector<int2> slot_batch;        // permeation: [TC] ray range of the last batch writing slot s
   std::vector<uint8_t> muffle_reset;   // raytrace: [TC] 1 if some batch resets slot s
   std::vector<int> ray_order;          // lane slot -> ray index (direction-coherent at TC == 1)
+  std::vector<uint8_t> order_dirs;     // the half3 directions ray_order was computed from
   // input staging layout (bytes)
   size_t off_sph = 0, off_aabb = 0, off_obb = 0, off_tgt = 0, off_dirs = 0, off_vol = 0, off_muf = 0, off_tab = 0,
          off_reset = 0, off_order = 0, raw_bytes = 0;
@@ -135,8 +137,10 @@ struct Device {
   hipEvent_t launch_done = nullptr;  // after the last art_launch_device frame (caller's stream)
   bool launch_pending = false;       // work on dv.stream waits for it before reusing the scene / buffers
   hipStream_t launch_stream = nullptr;  // the caller's stream of that frame
+  bool launch_recorded = false;         // launch_done already recorded after that frame
   uint64_t exec_launches = 0;
   int fan_begin = 0, fan_count = 0;
+  size_t in_off = 0;  // art_schedule: this shard's [origins | permeation slots] in the input staging
   DevScene sc{};
   SortBufs sb{};  // buffers of the spatially sorted scene copy (art_bvh.hip), set by upload_scene
   // resident scenes: the sorted copies / BVH in dv.soa were built for store generation sorted_gen
@@ -204,7 +208,31 @@ struct art_ctx {
   std::vector<int> tid_hist[3];
   art_collider_sync_stats last_sync{};
   HostBuf h_upd;
+  // Host phases of the Unity-facing frame (ART_HOST_TIMES=1 in the environment at art_create:
+  // steady_clock marks in art_schedule / art_complete, means printed by art_destroy to stderr).
+  struct HostPhases {
+    bool on = false;
+    uint64_t frames = 0;
+    double us[8] = {};
+  } hp;
 };
+
+namespace {
+// phase names of art_ctx::HostPhases (in the order the frame runs them)
+const char* const kHostPhase[8] = {"validate_frame", "pack_inputs", "stage_fans", "upload_scene", "enqueue_copies_kernels",
+                                   "complete_wait", "unpack_outputs", "complete_other"};
+struct PhaseClock {
+  art_ctx::HostPhases* hp;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseClock(art_ctx::HostPhases* h) : hp(h && h->on ? h : nullptr) { if (hp) t = std::chrono::steady_clock::now(); }
+  void mark(int phase) {
+    if (!hp) return;
+    const auto n = std::chrono::steady_clock::now();
+    hp->us[phase] += std::chrono::duration<double, std::micro>(n - t).count();
+    t = n;
+  }
+};
+}  // namespace
 
 namespace {
 
@@ -363,6 +391,12 @@ const ConeTable& cone_table() {
 
 // Frame scalars + batch tables (Audio/AudioRayTracer.cs:161, Jobs/*:63-64, :36-37).
 void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int* resident_counts = nullptr) {
+  // the direction-coherent order of the last frame is kept while its directions stay the same
+  // (they are set once at init, AudioRayTracer.cs:72-86): a 3-KB compare instead of the sort
+  std::vector<int> last_order;
+  std::vector<uint8_t> last_dirs;
+  last_order.swap(f.ray_order);
+  last_dirs.swap(f.order_dirs);
   f = Frame();
   f.R = d->ray_count; f.H = d->max_hits_per_ray; f.T = d->audio_target_count;
   f.TC = d->batch_slots; f.bs = d->batch_size; f.nb = (f.R + f.bs - 1) / f.bs;
@@ -388,7 +422,15 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.slot_batch[pid] = make_int2(start, start + cnt);  // later batches overwrite earlier ones
   }
   if (f.TC == 1) {
-    coherent_order(d->ray_directions, f.R, f.ray_order);
+    const size_t nb = (size_t)f.R * sizeof(art_half3);
+    if (last_order.size() == (size_t)f.R && last_dirs.size() == nb && memcmp(last_dirs.data(), d->ray_directions, nb) == 0) {
+      f.ray_order.swap(last_order);
+      f.order_dirs.swap(last_dirs);
+    } else {
+      coherent_order(d->ray_directions, f.R, f.ray_order);
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(d->ray_directions);
+      f.order_dirs.assign(b, b + nb);
+    }
   } else {  // per-batch muffle slots: keep rays in index order
     f.ray_order.resize((size_t)f.R);
     for (int i = 0; i < f.R; ++i) f.ray_order[(size_t)i] = i;
@@ -485,9 +527,13 @@ void pack_inputs(const art_frame_desc* d, const Frame& f, uint8_t* h) {
 // an event record between frames costs the launch stream ~5 us of GPU idle per frame (kernel trace,
 // DESIGN.md §4), so back-to-back frames on one stream record none. The caller's stream of the last
 // frame must still exist at the next call that touches the scene (art.h, streams).
+// With ART_CTX_EVENT_EACH_LAUNCH the event is recorded by art_launch_device itself (launch_recorded),
+// so the caller may destroy or recycle its stream right after the call.
 int mark_launch_done(art_ctx* c, Device& dv) {
+  if (dv.launch_recorded) return ART_OK;
   if (!dv.launch_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.launch_done, hipEventDisableTiming));
   HIP_TRY(c, hipEventRecord(dv.launch_done, dv.launch_stream));
+  dv.launch_recorded = true;
   return ART_OK;
 }
 int wait_launch(art_ctx* c, Device& dv) {
@@ -646,7 +692,11 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   {  // the BVH's launches first: its first kernels reach the CUs before the lists' wide passes fill them
     int rc = build_bvh();
     if (rc == 0) rc = build_cells();
-    if (rc) return rc;
+    if (rc) {  // kernels may already be queued on the side stream: later work on dv.stream waits for them
+      if (cells_st != dv.stream && hipEventRecord(dv.join, cells_st) == hipSuccess)
+        (void)hipStreamWaitEvent(dv.stream, dv.join, 0);
+      return rc;
+    }
   }
   if (cells_st != dv.stream) {  // the frame's kernels wait for the lists
     HIP_TRY(c, hipEventRecord(dv.join, cells_st));
@@ -717,7 +767,7 @@ hipEvent_t pool_event(Device& dv, size_t i) {
 
 // Enqueue the kernels of one frame for fan_count fans on stream st.
 int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origins, int fan_count, uint8_t* d_block,
-                    hipStream_t st, bool count) {
+                    hipStream_t st, bool count, const float* perm_in = nullptr, uint8_t* host_out = nullptr) {
   if (fan_count == 0) return ART_OK;
   const bool timing = (c->flags & ART_CTX_TIME_KERNELS) && !count;
   FrameParams fp = f.fp;
@@ -871,7 +921,7 @@ int enqueue_kernels(art_ctx* c, Device& dv, const Frame& f, const float* d_origi
   }
   if (f.stages & (ART_STAGE_RAYTRACE | ART_STAGE_REDUCE)) {
     size_t ti = timing ? tstart(kEvReduce, st) : 0;
-    launch_reduce(dv.sc, fp, f.L, d_block, acc, muffle_reset, st);
+    launch_reduce(dv.sc, fp, f.L, d_block, acc, muffle_reset, st, perm_in, (f.stages & ART_STAGE_REDUCE) ? host_out : nullptr);
     if (timing) tstop(ti, st);
     HIP_TRY(c, hipGetLastError());
   }
@@ -904,12 +954,37 @@ bool fan_wants_hits(const art_fan* fans, int n) {
   return false;
 }
 
+// JobHandle.Complete (AudioRayTracer.cs:97): the frame's completion event, polled for up to 4 ms
+// (a frame takes ~0.1-2 ms: polling wakes the caller within a microsecond or two of the event,
+// where a blocking wait adds the runtime's wake-up latency), then waited for. ART_COMPLETE_SPIN=0
+// in the environment: always the blocking wait.
+hipError_t wait_done(hipEvent_t ev) {
+  static const bool spin = [] { const char* e = getenv("ART_COMPLETE_SPIN"); return !(e && e[0] == '0'); }();
+  if (spin) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e != hipErrorNotReady) return e;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(4)) break;
+    }
+  }
+  return hipEventSynchronize(ev);
+}
+
+// Host-API frames whose slot arrays need no upload (art_schedule): one batch slot (every muffle
+// slot is reset by the raytrace stage, the permeation stage rewrites its slot), the raytrace stage
+// on, no echo upload, no hit outputs.
+bool compact_slots(const Frame& f, bool need_echo) {
+  return f.TC == 1 && (f.stages & ART_STAGE_RAYTRACE) && !need_echo && !f.L.has_hits;
+}
+
 // One device's share of an art_schedule frame: scene upload, origins and in/out slot arrays H2D,
 // kernels, result blocks D2H, completion event (all async on dv.stream).
-int enqueue_device_frame(art_ctx* c, Device& dv, const Frame& f, const uint8_t* hin, const float* horg, uint8_t* hb,
-                         bool need_echo, bool count, bool inject_failure = false) {
+int enqueue_device_frame(art_ctx* c, Device& dv, const Frame& f, const uint8_t* hin, uint8_t* hb, bool need_echo, bool count,
+                         bool inject_failure = false, PhaseClock* pc = nullptr) {
   const FanLayout& L = f.L;
   int rc = upload_scene(c, dv, f, hin);
+  if (pc) pc->mark(3);
   if (rc) return rc;
   if (inject_failure) {
     dv.raw_valid = false;  // the scene upload may not have completed: never reuse it
@@ -917,21 +992,34 @@ int enqueue_device_frame(art_ctx* c, Device& dv, const Frame& f, const uint8_t* 
   }
   if (dv.fan_count == 0) { HIP_TRY(c, hipEventRecord(dv.done, dv.stream)); return ART_OK; }
   const size_t bbytes = (size_t)dv.fan_count * L.stride;
-  if (!dv.origins.reserve((size_t)dv.fan_count * 12) || !dv.block.reserve(bbytes))
-    return fail(c, ART_E_NOMEM, "device allocation failed");
-  HIP_TRY(c, hipMemcpyAsync(dv.origins.p, horg + 3 * dv.fan_begin, (size_t)dv.fan_count * 12, hipMemcpyHostToDevice, dv.stream));
+  const size_t tcT = (size_t)f.TC * f.T;
+  const bool compact = compact_slots(f, need_echo);
+  // compact frames: the origins and (without the permeation stage) the caller's permeation slots in
+  // one copy; the block's slot sections are written by the kernels (muffle) or not used (permeation)
+  const size_t perm_in_off = align_up((size_t)dv.fan_count * 12, 16);
+  const bool perm_in = compact && !(f.stages & ART_STAGE_PERMEATE);
+  const size_t in_bytes = perm_in ? perm_in_off + (size_t)dv.fan_count * tcT * 4 : (size_t)dv.fan_count * 12;
+  if (!dv.origins.reserve(in_bytes) || !dv.block.reserve(bbytes)) return fail(c, ART_E_NOMEM, "device allocation failed");
   uint8_t* hbs = hb + (size_t)dv.fan_begin * L.stride;
+  // the shard's origins (and permeation slots), contiguous in the staging (art_schedule)
+  HIP_TRY(c, hipMemcpyAsync(dv.origins.p, hin + dv.in_off, in_bytes, hipMemcpyHostToDevice, dv.stream));
   if (need_echo || L.has_hits) {
     HIP_TRY(c, hipMemcpyAsync(dv.block.p, hbs, bbytes, hipMemcpyHostToDevice, dv.stream));
-  } else {  // only the muffle + permeation slot arrays (adjacent in the record)
+  } else if (!compact) {  // only the muffle + permeation slot arrays (adjacent in the record)
     HIP_TRY(c, hipMemcpy2DAsync(static_cast<uint8_t*>(dv.block.p) + L.muffle_off, L.stride, hbs + L.muffle_off, L.stride,
                                 L.echo_off - L.muffle_off, dv.fan_count, hipMemcpyHostToDevice, dv.stream));
   }
+  // the reduce kernel stores each fan's record into the pinned staging itself (no D2H copy) when it
+  // runs the reduce stage
+  const bool direct = (f.stages & ART_STAGE_REDUCE) && !count;
   rc = enqueue_kernels(c, dv, f, static_cast<const float*>(dv.origins.p), dv.fan_count, static_cast<uint8_t*>(dv.block.p),
-                       dv.stream, count);
+                       dv.stream, count,
+                       perm_in ? reinterpret_cast<const float*>(static_cast<uint8_t*>(dv.origins.p) + perm_in_off) : nullptr,
+                       direct ? hbs : nullptr);
   if (rc) return rc;
-  HIP_TRY(c, hipMemcpyAsync(hbs, dv.block.p, bbytes, hipMemcpyDeviceToHost, dv.stream));
+  if (!direct) HIP_TRY(c, hipMemcpyAsync(hbs, dv.block.p, bbytes, hipMemcpyDeviceToHost, dv.stream));
   HIP_TRY(c, hipEventRecord(dv.done, dv.stream));
+  if (pc) pc->mark(4);
   return ART_OK;
 }
 
@@ -970,6 +1058,7 @@ static int create_on(const int32_t* ids, int32_t count, art_ctx** out) {
   if (count <= 0 || count > 64 || !ids) return ART_E_INVALID;
   art_ctx* c = new (std::nothrow) art_ctx();
   if (!c) return ART_E_NOMEM;
+  if (const char* e = getenv("ART_HOST_TIMES")) c->hp.on = e[0] == '1';
   for (int32_t k = 0; k < count; ++k) {
     const int i = ids[k];
     Device dv;
@@ -1022,6 +1111,11 @@ ART_API void art_destroy(art_ctx* c) {
   if (c && !c->devs.empty()) art_wave_times_dump_impl();
 #endif
   if (!c) return;
+  if (c->hp.on && c->hp.frames) {
+    fprintf(stderr, "{\"art_host_phases_us\": {");
+    for (int k = 0; k < 8; ++k) fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", kHostPhase[k], c->hp.us[k] / (double)c->hp.frames);
+    fprintf(stderr, "}, \"frames\": %llu}\n", (unsigned long long)c->hp.frames);
+  }
   if (c->cpu) {
     if (c->inflight) art::cpu_complete(c->cpu, nullptr);
     art::cpu_destroy(c->cpu);
@@ -1029,7 +1123,11 @@ ART_API void art_destroy(art_ctx* c) {
   for (Device& dv : c->devs) {
     (void)hipSetDevice(dv.id);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    if (dv.launch_pending) (void)hipDeviceSynchronize();  // a device frame on the caller's stream (which may be gone)
+    if (dv.launch_pending) {  // a device frame on the caller's stream: wait for it alone (the stream is valid
+                              // until this call, art_device.h); the device-wide wait only if that fails
+      if (mark_launch_done(c, dv) != ART_OK || hipEventSynchronize(dv.launch_done) != hipSuccess) (void)hipDeviceSynchronize();
+      dv.launch_pending = false;
+    }
     dv.raw.release(); dv.soa.release(); dv.origins.release(); dv.block.release(); dv.acc.release(); dv.counts.release();
     dv.exec.release(); dv.pairs.release(); dv.dsp.release(); dv.cones.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
@@ -1121,6 +1219,7 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
     *out = c->handle;
     return ART_OK;
   }
+  PhaseClock pc(&c->hp);
   Frame& f = c->fr;
   make_frame(d, hits ? ART_OUT_HIT_RESULTS : 0u, f, (c->flags & ART_CTX_RESIDENT_COLLIDERS) ? c->synced : nullptr);
   const FanLayout& L = f.L;
@@ -1128,20 +1227,47 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
   const size_t origins_off = align_up(f.raw_bytes, 16);
   if (!c->h_in.reserve(origins_off + (size_t)fan_count * 12)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
   if (!c->h_block.reserve((size_t)fan_count * L.stride)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
-  uint8_t* hin = static_cast<uint8_t*>(c->h_in.p);
-  uint8_t* hb = static_cast<uint8_t*>(c->h_block.p);
-  pack_inputs(d, f, hin);
-  float* horg = reinterpret_cast<float*>(hin + origins_off);
+  // shard fans over devices
+  const int nd = (int)c->devs.size();
+  for (int k = 0; k < nd; ++k) {
+    Device& dv = c->devs[k];
+    dv.fan_begin = (int)((long long)fan_count * k / nd);
+    dv.fan_count = (int)((long long)fan_count * (k + 1) / nd) - dv.fan_begin;
+  }
   // In/out arrays (the reference's persistent NativeArrays): slots no batch resets keep their
-  // contents, so their current values travel to the device with the frame.
+  // contents, so their current values travel to the device with the frame. Compact frames (one
+  // batch slot, raytrace stage, no echo upload or hit outputs: every muffle slot is reset) upload
+  // no slots, except the permeation slots when the permeation stage does not rewrite them, and
+  // those beside the origins (one H2D copy per shard: [origins | permeation slots]).
   const size_t RH = (size_t)f.R * f.H;
   const bool need_echo = f.TC > 1 || !(f.stages & ART_STAGE_RAYTRACE);
-  for (int i = 0; i < fan_count; ++i) {
+  const bool compact = compact_slots(f, need_echo);
+  const bool perm_in = compact && !(f.stages & ART_STAGE_PERMEATE);
+  const size_t tcT = (size_t)f.TC * f.T;
+  size_t in_end = origins_off;
+  for (Device& dv : c->devs) {
+    dv.in_off = in_end;
+    in_end += align_up(align_up((size_t)dv.fan_count * 12, 16) + (perm_in ? (size_t)dv.fan_count * tcT * 4 : 0), 16);
+  }
+  if (!c->h_in.reserve(in_end)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  uint8_t* hin = static_cast<uint8_t*>(c->h_in.p);
+  uint8_t* hb = static_cast<uint8_t*>(c->h_block.p);
+  pc.mark(0);
+  pack_inputs(d, f, hin);
+  pc.mark(1);
+  for (int i = 0, k = 0; i < fan_count; ++i) {
     const art_fan& fn = fans[i];
-    memcpy(horg + 3 * i, fn.origin, 12);
+    while (i >= c->devs[k].fan_begin + c->devs[k].fan_count) ++k;
+    const Device& dv = c->devs[k];
+    uint8_t* seg = hin + dv.in_off;
+    const size_t j = (size_t)(i - dv.fan_begin);
+    memcpy(seg + 12 * j, fn.origin, 12);
+    if (perm_in) memcpy(seg + align_up((size_t)dv.fan_count * 12, 16) + j * tcT * 4, fn.permeation_power_remains, tcT * 4);
     uint8_t* rec = hb + (size_t)i * L.stride;
-    memcpy(rec + L.muffle_off, fn.muffle_ray_hits, (size_t)f.TC * f.T * 2);
-    memcpy(rec + L.perm_off, fn.permeation_power_remains, (size_t)f.TC * f.T * 4);
+    if (!compact) {
+      memcpy(rec + L.muffle_off, fn.muffle_ray_hits, tcT * 2);
+      memcpy(rec + L.perm_off, fn.permeation_power_remains, tcT * 4);
+    }
     if (need_echo) {
       memcpy(rec + L.echo_off, fn.echo_ray_distances, RH * 2);
       if (L.has_hits) {
@@ -1158,13 +1284,7 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
   }
   const bool count = (c->flags & ART_CTX_COUNT_TESTS) != 0;
   if (count) count_nonowned(c, d);
-  // shard fans over devices
-  const int nd = (int)c->devs.size();
-  for (int k = 0; k < nd; ++k) {
-    Device& dv = c->devs[k];
-    dv.fan_begin = (int)((long long)fan_count * k / nd);
-    dv.fan_count = (int)((long long)fan_count * (k + 1) / nd) - dv.fan_begin;
-  }
+  pc.mark(2);
   // Enqueue per device. An error on device k leaves devices [0, k) (and k itself, partly) with
   // async copies that still read or write the pinned staging: drain every stream before returning,
   // so the next art_schedule can repack h_in / h_block safely.
@@ -1173,7 +1293,7 @@ ART_API int art_schedule(art_ctx* c, const art_frame_desc* d, const art_fan* fan
   const int fail_shard = fail_env ? atoi(fail_env) : -1;
   for (size_t k = 0; k < c->devs.size(); ++k) {
     Device& dv = c->devs[k];
-    rc = enqueue_device_frame(c, dv, f, hin, horg, hb, need_echo, count, (int)k == fail_shard);
+    rc = enqueue_device_frame(c, dv, f, hin, hb, need_echo, count, (int)k == fail_shard, &pc);
     if (rc) {
       for (Device& e : c->devs) {
         (void)hipSetDevice(e.id);
@@ -1217,14 +1337,18 @@ ART_API int art_complete(art_ctx* c, art_handle h) {
     if (c->counted) c->has_counts = true;
     return ART_OK;
   }
+  PhaseClock pc(&c->hp);
   for (Device& dv : c->devs) {
     HIP_TRY(c, hipSetDevice(dv.id));
-    HIP_TRY(c, hipEventSynchronize(dv.done));
+    HIP_TRY(c, wait_done(dv.done));
   }
+  pc.mark(5);
   const Frame& f = c->fr;
   const FanLayout& L = f.L;
   const size_t RH = (size_t)f.R * f.H;
   const uint8_t* hb = static_cast<const uint8_t*>(c->h_block.p);
+  // compact frames without the permeation stage leave the caller's permeation slots as they are
+  const bool perm_back = !(compact_slots(f, f.TC > 1 || !(f.stages & ART_STAGE_RAYTRACE)) && !(f.stages & ART_STAGE_PERMEATE));
   for (size_t i = 0; i < c->fans.size(); ++i) {
     const art_fan& fn = c->fans[i];
     const uint8_t* rec = hb + i * L.stride;
@@ -1232,12 +1356,13 @@ ART_API int art_complete(art_ctx* c, art_handle h) {
       memcpy(fn.settings, rec + L.settings_off, (size_t)f.T * sizeof(art_target_settings));
     if (L.has_dsp && fn.dsp_params) memcpy(fn.dsp_params, rec + L.dsp_off, (size_t)f.T * sizeof(art_dsp_params));
     memcpy(fn.muffle_ray_hits, rec + L.muffle_off, (size_t)f.TC * f.T * 2);
-    memcpy(fn.permeation_power_remains, rec + L.perm_off, (size_t)f.TC * f.T * 4);
+    if (perm_back) memcpy(fn.permeation_power_remains, rec + L.perm_off, (size_t)f.TC * f.T * 4);
     memcpy(fn.echo_ray_distances, rec + L.echo_off, RH * 2);
     if (L.has_hits && fn.ray_hit_points) memcpy(fn.ray_hit_points, rec + L.hit_points_off, RH * sizeof(art_half3));
     if (L.has_hits && fn.ray_hit_counts) memcpy(fn.ray_hit_counts, rec + L.hit_counts_off, (size_t)f.R);
     if (L.has_hits && fn.ray_hit_ids) memcpy(fn.ray_hit_ids, rec + L.hit_ids_off, RH * sizeof(uint32_t));
   }
+  pc.mark(6);
   if (c->counted) {
     memset(&c->last_counts, 0, sizeof c->last_counts);
     for (Device& dv : c->devs) {
@@ -1248,6 +1373,8 @@ ART_API int art_complete(art_ctx* c, art_handle h) {
     }
     c->has_counts = true;
   }
+  pc.mark(7);
+  if (c->hp.on) c->hp.frames++;
   return ART_OK;
 }
 
@@ -1314,6 +1441,11 @@ static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, 
   // after this frame (wait_launch records the event on this stream then)
   dv.launch_pending = true;
   dv.launch_stream = st;
+  dv.launch_recorded = false;
+  if (c->flags & ART_CTX_EVENT_EACH_LAUNCH) {  // opt-in: the caller may drop its stream after this call
+    int rc2 = mark_launch_done(c, dv);
+    if (rc2) return rc2;
+  }
   if (count) return read_counts(c, dv, st, out, false);
   return ART_OK;
 }
@@ -1346,6 +1478,16 @@ ART_API int art_f32tof16_device(art_ctx* c, uint32_t first_bits, uint32_t count,
   if (count > 0 && !d_out) return fail(c, ART_E_INVALID, "art_f32tof16_device: d_out is NULL");
   HIP_TRY(c, hipSetDevice(c->devs[0].id));
   launch_half_range(first_bits, count, d_out, static_cast<hipStream_t>(stream));
+  HIP_TRY(c, hipGetLastError());
+  return ART_OK;
+}
+
+ART_API int art_recip_exact_device(art_ctx* c, uint32_t first_bits, uint32_t count, uint32_t* d_out, void* stream) {
+  if (!c) return ART_E_INVALID;
+  if (c->cpu) return fail(c, ART_E_UNSUPPORTED, "%s: the CPU backend (device_mask 0) has the host entry points only", __func__);
+  if (count > 0 && !d_out) return fail(c, ART_E_INVALID, "art_recip_exact_device: d_out is NULL");
+  HIP_TRY(c, hipSetDevice(c->devs[0].id));
+  launch_recip_range(first_bits, count, d_out, static_cast<hipStream_t>(stream));
   HIP_TRY(c, hipGetLastError());
   return ART_OK;
 }

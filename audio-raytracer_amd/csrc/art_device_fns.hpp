@@ -81,7 +81,8 @@ ART_HD quat stored_q(const ObbRec& b) { quat q; q.x = b.qx; q.y = b.qy; q.z = b.
 
 // 1.0f / x bit for bit: where x's exponent field lies in [3, 251] the hardware reciprocal plus one
 // Newton step (3 instructions) equals the IEEE division for every float (checked exhaustively on
-// the GPU, tools/rcp_check.hip); the other lanes (tiny, huge, zero, inf, NaN) divide. Device only.
+// the GPU on this function itself through art_recip_exact_device, tests/test_recip_exhaustive.py);
+// the other lanes (tiny, huge, zero, inf, NaN) divide. Device only.
 #ifndef ART_FAST_RCP
 #define ART_FAST_RCP 1
 #endif

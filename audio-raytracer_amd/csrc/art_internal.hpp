@@ -217,6 +217,7 @@ void launch_prep(const art_sphere* sph, int ns, const art_aabb* aabb, int na, co
                  CullRec* cull, hipStream_t st);
 void launch_fibonacci(int count, art_half3* out, hipStream_t st);
 void launch_half_range(uint32_t first, uint32_t count, uint16_t* out, hipStream_t st);
+void launch_recip_range(uint32_t first, uint32_t count, uint32_t* out, hipStream_t st);
 void launch_scatter_prep(const int* idx_s, const art_sphere* rec_s, int ds, const int* idx_a, const art_aabb* rec_a,
                          int da, const int* idx_o, const art_obb* rec_o, int dob, art_sphere* sph, art_aabb* aabb,
                          art_obb* obb, int ns, int na, SphereRec* osph, SphereCold* osphc, AabbRec* oaabb,
@@ -256,6 +257,7 @@ void launch_permeate_sweep(const DevScene& sc, const FrameParams& fp, const FanL
 void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* origins, DevCounts* counts,
                        unsigned long long* nhit, hipStream_t st);
 void launch_reduce(const DevScene& sc, const FrameParams& fp, const FanLayout& L, uint8_t* block,
-                   const uint32_t* muffle_acc, const uint8_t* muffle_reset, hipStream_t st);
+                   const uint32_t* muffle_acc, const uint8_t* muffle_reset, hipStream_t st, const float* perm_in = nullptr,
+                   uint8_t* host_out = nullptr);
 
 }  // namespace art

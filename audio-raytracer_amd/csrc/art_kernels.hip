@@ -390,9 +390,14 @@ __global__ __launch_bounds__(kPermBlock) void perm_count_kernel(DevScene sc, Fra
 // One wave per fan. The echo sum is sequential in index order (App. A.4): non-zero halves are
 // added one by one in order; zeros are counted as "returned" (Q4).
 // ------------------------------------------------------------------------------------------
+// perm_in (host-API frames at TC == 1 without the permeation stage): the caller's permeation
+// slots, uploaded with the origins, in place of the block's (which then stay unwritten and are not
+// copied back). host_out (host-API frames): the fan's whole result record is also stored into the
+// pinned host staging (the frame's D2H copy, done by the kernel that finishes the frame).
 __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp, FanLayout L, uint8_t* __restrict__ block,
                                                     const uint32_t* __restrict__ muffle_acc,
-                                                    const uint8_t* __restrict__ muffle_reset) {
+                                                    const uint8_t* __restrict__ muffle_reset, const float* __restrict__ perm_in,
+                                                    uint8_t* __restrict__ host_out) {
   const int fan = blockIdx.x, lane = threadIdx.x;
   uint8_t* fb = block + (size_t)fan * L.stride;
   const int T = fp.T, TC = fp.TC;
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
   const float reverbStrength = avg / fp.max_reverb;
   const float reverbVolume = returned / (float)n;
 
-  const float* ppr = reinterpret_cast<const float*>(fb + L.perm_off);
+  const float* ppr = perm_in ? perm_in + (size_t)fan * TC * T : reinterpret_cast<const float*>(fb + L.perm_off);
   art_target_settings* st = reinterpret_cast<art_target_settings*>(fb + L.settings_off);
   art_dsp_params* dp = reinterpret_cast<art_dsp_params*>(fb + L.dsp_off);
   for (int t = lane; t < T; t += 64) {
@@ -494,6 +499,12 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
       }
       dp[t] = p;
     }
+  }
+  if (host_out) {  // the fan's record into the pinned host staging (16-B aligned sections and stride)
+    __syncthreads();  // (this wave's settings, DSP and muffle stores above come first)
+    const uint4* src = reinterpret_cast<const uint4*>(fb);
+    uint4* dst = reinterpret_cast<uint4*>(host_out + (size_t)fan * L.stride);
+    for (uint32_t i = (uint32_t)lane; i < L.stride / 16u; i += 64u) dst[i] = src[i];
   }
 }
 
@@ -540,6 +551,21 @@ void launch_half_range(uint32_t first, uint32_t count, uint16_t* out, hipStream_
   if (count == 0) return;
   const unsigned blocks = (unsigned)(((unsigned long long)count + 255ull) / 256ull);  // no 32-bit wrap near 2^32
   hipLaunchKernelGGL(half_range_kernel, dim3(blocks), dim3(256), 0, st, first, count, out);
+}
+
+// The OBB slab's reciprocal (art_device_fns.hpp recip_exact, the product function itself) over a
+// range of float bit patterns, for the exhaustive check against IEEE 1.0f / x
+// (tests/test_recip_exhaustive.py).
+__global__ void recip_range_kernel(uint32_t first, uint32_t count, uint32_t* __restrict__ out) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  out[i] = __float_as_uint(recip_exact(asfloat(first + (uint32_t)i)));  // wraps past 0xFFFFFFFF
+}
+
+void launch_recip_range(uint32_t first, uint32_t count, uint32_t* out, hipStream_t st) {
+  if (count == 0) return;
+  const unsigned blocks = (unsigned)(((unsigned long long)count + 255ull) / 256ull);
+  hipLaunchKernelGGL(recip_range_kernel, dim3(blocks), dim3(256), 0, st, first, count, out);
 }
 
 void launch_fibonacci(int count, art_half3* out, hipStream_t st) {
@@ -589,9 +615,9 @@ void launch_perm_count(const DevScene& sc, const FrameParams& fp, const float* o
 }
 
 void launch_reduce(const DevScene& sc, const FrameParams& fp, const FanLayout& L, uint8_t* block, const uint32_t* muffle_acc,
-                   const uint8_t* muffle_reset, hipStream_t st) {
+                   const uint8_t* muffle_reset, hipStream_t st, const float* perm_in, uint8_t* host_out) {
   if (fp.S == 0) return;
-  hipLaunchKernelGGL(reduce_kernel, dim3(fp.S), dim3(64), 0, st, sc, fp, L, block, muffle_acc, muffle_reset);
+  hipLaunchKernelGGL(reduce_kernel, dim3(fp.S), dim3(64), 0, st, sc, fp, L, block, muffle_acc, muffle_reset, perm_in, host_out);
 }
 
 }  // namespace art

@@ -175,6 +175,41 @@ __device__ __forceinline__ CullRec load_node(const BvhRes& b, int i) {
   return r;
 }
 
+// Shared-origin node table (TAB kernels): every ray of a workgroup starts at the fan origin O, so a
+// node's widened box relative to O, (lo - m) - O and (hi + m) - O with m = factor * (scale + |O|_1),
+// is the same for all of them. Built once per workgroup in LDS (node_table_build), the node test is
+// then the slab's multiplies and min / max on the very operands node_entry computes (bit-identical:
+// the same operations in the same order, DESIGN.md §5 item 8 unchanged). Up to kTabNodes nodes
+// (the BVH of <= 4096 colliders: 1365 nodes, 32 KB).
+constexpr int kTabNodes = 1365;
+#ifndef ART_TAB_USE
+#define ART_TAB_USE 1  // (measurement builds: 0 = the table is built but the node tests load the nodes; -1 = not built either)
+#endif
+struct NodeTab {
+  float4 a[kTabNodes];  // (lo.x, lo.y, lo.z, hi.x) relative to O, widened
+  float2 b[kTabNodes];  // (hi.y, hi.z)
+};
+__device__ __forceinline__ void node_table_build(const DevScene& sc, vec3 O, NodeTab* tab) {
+  const BvhRes br = bvh_res(sc);
+  const int nn = sc.bvh_leaf0 + 3 * sc.bvh_leaf0 + 1;
+  const float om = fabsf(O.x) + fabsf(O.y) + fabsf(O.z);  // quad_nearest_core's om of every ray at O
+  for (int i = (int)threadIdx.x; i < nn; i += (int)blockDim.x) {
+    const CullRec r = load_node(br, i);
+    const float m = __builtin_fmaf(r.factor, om, r.fscale);  // node_entry's margin
+    tab->a[i] = make_float4((r.lox - m) - O.x, (r.loy - m) - O.y, (r.loz - m) - O.z, (r.hix + m) - O.x);
+    tab->b[i] = make_float2((r.hiy + m) - O.y, (r.hiz + m) - O.z);
+  }
+}
+__device__ __forceinline__ bool node_entry_tab(const Seg& s, const NodeTab* tab, int i, float& tn) {
+  const float4 a = tab->a[i];
+  const float2 b = tab->b[i];
+  const float t0x = a.x * s.inv.x, t0y = a.y * s.inv.y, t0z = a.z * s.inv.z;  // slab<false>'s (mn - o) * inv
+  const float t1x = a.w * s.inv.x, t1y = b.x * s.inv.y, t1z = b.y * s.inv.z;
+  tn = fmax_ieee(fmax_ieee(fmin_ieee(t0x, t1x), fmin_ieee(t0y, t1y)), fmin_ieee(t0z, t1z));
+  const float tf = fmin_ieee(fmin_ieee(fmax_ieee(t0x, t1x), fmax_ieee(t0y, t1y)), fmax_ieee(t0z, t1z));
+  return !(tn > tf || tf < 0.0f);
+}
+
 // One inner step of a quad traversal (lane qd holds child c0 + qd; `enter` / entry `en` its
 // verdict): descend into the nearest entered child and push the other entered children far first
 // onto the ray's stack, or pop when none is entered. Near-first order by rank: each lane's key is
@@ -280,9 +315,9 @@ constexpr unsigned long long kQuad0 = 0x1111111111111111ull;  // lane 0 of every
 
 // Waves per SIMD of the traversal kernels: 8 (64 VGPRs). Register spills inside the divergent
 // traversal loops hung a fused kernel once, so the counting instantiations and
-// the echo traversal's OBB one run at the occupancy that holds them without spills; the nearest
-// traversal's OBB instantiation keeps 8 waves and 5 spilled VGPRs (at 7 waves config 3's nearest
-// kernel took 300 instead of 243 us), covered by the full-size OBB parity tests.
+// the echo traversal's OBB one run at the occupancy that holds them without spills. Every
+// instantiation in this file compiles without scratch, the OBB nearest one at 8 waves included
+// (its round-3 spills went with the round-4 leaf layout; profiles/r06_spill_check.txt).
 #ifndef ART_NEAREST_OBB_WAVES
 #define ART_NEAREST_OBB_WAVES 8
 #endif
@@ -320,10 +355,13 @@ __device__ __forceinline__ unsigned long long nearest_key(float d, int code) {
 // re-evaluates a zero distance).
 // PERM: the permeation job's first-hit cast (ShootRayCast :101-141: INFINITY sentinel, inverse OBB
 // rotation); otherwise the raytracer's (:225-280: float.MaxValue sentinel).
-template <bool EX, bool OBB, bool PERM = false>
+// TAB: every ray of the workgroup starts at one origin (a fan's bounce-0 casts), and `tab` holds
+// each BVH node's widened box relative to it (node_table): a node test is 6 multiplies and the
+// min / max, with the same operands as node_entry's.
+template <bool EX, bool OBB, bool PERM = false, bool TAB = false>
 __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, bool alive, int lane, uint32_t* my,
                                                   int* s_bound, unsigned long long* s_key, float& best, int& code,
-                                                  unsigned long long* ex) {
+                                                  unsigned long long* ex, const NodeTab* tab = nullptr) {
   const int qd = lane & 3, wq = lane >> 2;
   uint32_t* const s_wave = my - wq * kBvhStack;
   best = FLT_MAX;
@@ -356,9 +394,14 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     const int c0 = 4 * g + 1;
     if (EX && qd == 0) ++nnode;
     ART_DIAG_STEP(nsteps);
-    const CullRec r = load_node(br, c0 + qd);
     float tn;
-    const bool h = node_entry(s, r, om, tn);
+    bool h;
+    if (TAB && ART_TAB_USE > 0) {
+      h = node_entry_tab(s, tab, c0 + qd, tn);
+    } else {
+      const CullRec r = load_node(br, c0 + qd);
+      h = node_entry(s, r, om, tn);
+    }
     const float en = fmaxf(tn, 0.0f);
     const bool enter = force | (h & (en <= lim));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
     quad_descend(enter, en, force, qd, c0, my, g, sp);
@@ -481,8 +524,11 @@ __device__ __forceinline__ uint32_t* echo_counts(float4* state, int ngroups) {
 
 // Visibility work (struct of arrays, below): echo segments and outputs, hit records. `fixed`
 // (multi-hit frames with one batch slot and no hit outputs, nearest_first_kernel<..., FOLD>): the
-// records sit at fixed positions bounce * fixed + ray slot, an output index of kNoRecord / a hit
-// record destination of kNoRecord marking a slot with no echo / no muffle rays that bounce.
+// records sit at fixed positions bounce * fixed + ray slot and are compact (round 6): no echo
+// segment, out = (echo distance bits, echo half) with out.y = kNoRecord marking a slot with no hit
+// that bounce (then nothing else is written for it), hrec = (off.xyz, muffle destination); the
+// echo traversal rebuilds the segment from off and the fan origin, and the echo's index from the
+// slot (fold_path).
 constexpr uint32_t kNoRecord = 0xffffffffu;
 struct VisPairs {
   float4* seg;
@@ -569,25 +615,20 @@ __device__ __forceinline__ void fold_path(const DevScene& sc, const FrameParams&
   uint16_t* echo = reinterpret_cast<uint16_t*>(block + (size_t)fan * L.stride + L.echo_off);
   const size_t rec = (size_t)step * vp.fixed + sidx;
   if (lead) {  // this bounce's echo ray (:124-145) and the muffle rays' hit record (:150-173), or none
-    if (hit) {
+    if (hit) {   // (the echo's index is ray * H + hits - 1 = ray * H + step: every earlier bounce hit)
       const vec3 off = o - d * kEps;                 // :124, :158
       const float dist0 = distance(O, o);            // :130 (un-offset hit point)
-      const vec3 qdir = normalize(O - off);
-      vp.seg[2 * rec] = make_float4(off.x, off.y, off.z, dist0);
-      vp.seg[2 * rec + 1] = make_float4(qdir.x, qdir.y, qdir.z, __int_as_float(kNoOwner));
-      vp.out[rec] = make_uint2((uint32_t)(((size_t)fan * L.stride + L.echo_off) / 2) + (uint32_t)(ray * H + hits - 1),
-                               f32tof16(dist0 * echo_of(sc, type, idx)));  // :142-144
+      vp.out[rec] = make_uint2(__float_as_uint(dist0), f32tof16(dist0 * echo_of(sc, type, idx)));  // :142-144
       vp.hrec[rec] = make_float4(off.x, off.y, off.z, __uint_as_float((uint32_t)fan * (uint32_t)fp.T));  // batch slot 0
       echo[ray * H + hits - 1] = 0;  // a blocked echo keeps the reset value (:76); the echo traversal stores the rest
     } else {
-      vp.out[rec] = make_uint2(kNoRecord, 0u);
-      vp.hrec[rec] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kNoRecord));
+      vp.out[rec] = make_uint2(0u, kNoRecord);
     }
   }
   // termination / reflection (:179-193, ReflectRay :456-532)
   bool next = hit;  // a miss ends the ray (:200-207)
   if (hit) next = (hits >= H || life <= 0.0f) ? false : reflect_at_hit(sc, fp, type, idx, o, d, life);
-  if (lead && slot_ok) {
+  if (lead && slot_ok && alive) {  // (an ended ray's state already says so: later bounces leave it)
     state[2 * (size_t)sidx] = make_float4(o.x, o.y, o.z, life);
     state[2 * (size_t)sidx + 1] = make_float4(d.x, d.y, d.z, __int_as_float(hits | (next ? 256 : 0)));
     if (alive && !next)  // the ray stops here: slots past its last hit keep the reset value 0 (:72-80)
@@ -596,21 +637,33 @@ __device__ __forceinline__ void fold_path(const DevScene& sc, const FrameParams&
 }
 
 // EX: count the executed tests (fp.exec); OBB: the scene has OBBs; FOLD: fold_path above.
-template <bool EX, bool OBB, bool FOLD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWaves<EX, OBB>))) void nearest_first_kernel(
+// TAB (bounce 0 only, 64-ray groups per fan a multiple of 4, <= kTabNodes BVH nodes): workgroups of
+// 1024 lanes, the 4 consecutive 64-ray groups of one fan, all rays at the fan origin, traverse with
+// the shared-origin node table in LDS (node_table_build; 2 workgroups and 8 waves per SIMD per CU,
+// 70 KB of LDS each).
+template <bool EX, bool OBB, bool FOLD, bool TAB = false>
+__global__ __launch_bounds__(TAB ? 1024 : 256) __attribute__((amdgpu_waves_per_eu(kNearestWaves<EX, OBB>))) void nearest_first_kernel(
     DevScene sc, FrameParams fp, const float* __restrict__ origins, const int* __restrict__ ray_order,
     int2* __restrict__ hits, float4* __restrict__ state, int step, uint32_t* __restrict__ zero, uint32_t nzero,
     uint32_t* __restrict__ counters, FanLayout L, uint8_t* __restrict__ block, VisPairs vp) {
-  __shared__ uint32_t s_stk[kBvhStack * 64];
-  __shared__ int s_bound[64];
-  __shared__ unsigned long long s_key[64];
+  constexpr int kGroupsPerWg = TAB ? 4 : 1;
+  __shared__ uint32_t s_stk[kBvhStack * 64 * kGroupsPerWg];
+  __shared__ int s_bound[64 * kGroupsPerWg];
+  __shared__ unsigned long long s_key[64 * kGroupsPerWg];
+  __shared__ std::conditional_t<TAB, NodeTab, int> s_tab;
   ART_WAVE_TIMER(0);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nrb = (fp.R + 63) >> 6;
   const int ngroups = fp.S * nrb;
-  const int g = blockIdx.x;
-  const int rr = 16 * w + (lane >> 2);
-  uint32_t* my = s_stk + rr * kBvhStack;
+  const int g = (int)blockIdx.x * kGroupsPerWg + (w >> 2);  // TAB: 4 groups of one fan per workgroup
+  const int rr = 16 * (w & 3) + (lane >> 2);
+  uint32_t* my = s_stk + (16 * w + (lane >> 2)) * kBvhStack;
+  if constexpr (TAB) {  // the fan origin's node table (every ray of the workgroup starts there)
+    if (ART_TAB_USE >= 0) {
+      node_table_build(sc, load3(origins, g / nrb), &s_tab);
+      __syncthreads();
+    }
+  }
   unsigned long long* ex = EX ? fp.exec : nullptr;
   float best;
   int code;
@@ -622,7 +675,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
   bool slot_ok = true;
   if (FOLD) {  // every ray in its slot for every bounce
     if (step == 0) {
-      for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
+      for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0u;
       if (counters && blockIdx.x == 0 && threadIdx.x < 4) counters[threadIdx.x] = 0u;
     }
     fan = g / nrb;
@@ -662,7 +715,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
       live_list(state, ngroups)[(size_t)ngroups * 64 + threadIdx.x] = 0u;
     // the frame's muffle accumulators and pair counters, consumed only by later launches (no
     // memset dispatch between frames)
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0u;
     if (counters && blockIdx.x == 0 && threadIdx.x < 4) counters[threadIdx.x] = 0u;
     const int fan = g / nrb;
     const int slot = (g - fan * nrb) * 64 + rr;
@@ -678,13 +731,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kNearestWav
 #ifdef ART_DIAG
   const unsigned long long t0 = clock64();
 #endif
-  quad_nearest_core<EX, OBB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code, ex);
+  quad_nearest_core<EX, OBB, false, TAB>(sc, make_seg(o, d), alive, lane, my, s_bound + 16 * w, s_key + 16 * w, best, code,
+                                         ex, TAB ? reinterpret_cast<const NodeTab*>(&s_tab) : nullptr);
   if (FOLD) {
     // The ray's state is fetched again rather than kept live across the traversal (a memory
     // clobber: the compiler may not reuse the values loaded before it): 64 VGPRs, no spills.
     asm volatile("" ::: "memory");
     {
-      const int rr2 = 16 * w + (lane >> 2);
+      const int rr2 = 16 * (w & 3) + (lane >> 2);
       fan = g / nrb;
       const int sl = (g - fan * nrb) * 64 + rr2;
       slot_ok = sl < fp.R;
@@ -1129,11 +1183,24 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     }
     if (!__any(valid)) return;
   } else {
-    if (vp.fixed) {  // bounce `bounce`'s records at fixed slots: 64-slot group blk
+    if (vp.fixed) {  // bounce `bounce`'s compact records at fixed slots: 64-slot group blk (fold_path)
       p = (uint32_t)bounce * vp.fixed + blk * 64u + (uint32_t)slot;
-      valid = vp.out[p].x != kNoRecord;
+      const uint2 ov = vp.out[p];
+      valid = ov.y != kNoRecord;
       if (!__any(valid)) return;
-      if (valid) load_pair_seg(vp, p, s, maxd, owner);
+      if (valid) {  // the segment as fold_path's reference expressions give it: off -> fan origin (:124-130)
+        const FrameParams& fp = eh.fp;
+        const int nrb = (fp.R + 63) >> 6;
+        const int fan = (int)(blk / (uint32_t)nrb);
+        const int ray = eh.ray_order[(int)(blk - (uint32_t)fan * nrb) * 64 + slot];
+        const float4 hr = vp.hrec[p];
+        const vec3 off = mk3(hr.x, hr.y, hr.z), O = load3(eh.origins, fan);
+        s = make_seg(off, normalize(O - off));
+        maxd = __uint_as_float(ov.x);
+        owner = kNoOwner;
+        out_at = (uint32_t)(((size_t)fan * eh.L.stride + eh.L.echo_off) / 2) + (uint32_t)(ray * fp.H + bounce);
+        out_val = (uint16_t)(ov.y & 0xffffu);
+      }
     } else {
       // all echo pairs, or (bounce >= 0) those bounce `bounce` emitted: they follow the earlier bounces'
       uint32_t start = 0u, n;
@@ -1154,6 +1221,8 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
   const bool visible = quad_echo_core<OBB>(sc, s, maxd, owner, valid, lane, s_wave, nt, nnode);
   if (HM) {
     if (valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = visible ? out_val : (uint16_t)0;  // :76, :142-144
+  } else if (vp.fixed) {
+    if (valid && visible && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = out_val;  // :142-144
   } else if (valid && visible && qd == 0) {  // visible: the echo is stored (:142-144)
     const uint2 o = vp.out[p];
     reinterpret_cast<uint16_t*>(block)[o.x] = (uint16_t)(o.y & 0xffffu);
@@ -1353,6 +1422,7 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
     valid = valid && hit_from_pre(sc, eh, i >> 6, (int)(i & 63u), slot_ok, fan, ray, O, o, off, type, idx);
     dbase = (uint32_t)fan * (uint32_t)fp.T;
   } else {
+    if (vp.fixed) valid = valid && vp.out[i].y != kNoRecord;  // (compact records: fold_path)
     const float4 r = vp.hrec[valid ? i : 0u];
     off = mk3(r.x, r.y, r.z);
     dbase = __float_as_uint(r.w);
@@ -1813,10 +1883,26 @@ void launch_raytrace_fast(const DevScene& sc, const FrameParams& fp, const FanLa
   // echo traversal on st, the muffle kernel on the side stream (the longer kernel stays on st: a
   // fork costs ~10 us before the side stream starts). Without a side stream everything runs on st.
   const bool per_bounce = split && multi && ecnt;
+  // bounce 0 with the shared-origin node table (nearest_first_kernel<..., TAB>) when a fan's 64-ray
+  // groups come in fours, the BVH fits the table and the scene has OBBs. Measured (round 6, A/B of
+  // per-kernel HIP-event times): config 3 (4096 OBBs) nearest 68.4 -> 63.3 us, config 5 even; in
+  // OBB-free scenes the 1024-lane workgroups and the table build cost more than the table saves
+  // (config 2 nearest 50.8 -> 53.6 us), so they keep the 256-lane kernel.
+#ifndef ART_NEAREST_TAB
+#define ART_NEAREST_TAB 1  // (2: every scene, for A/B runs)
+#endif
+  const bool tab = ART_NEAREST_TAB && (ART_NEAREST_TAB == 2 || sc.no > 0) && ((fp.R + 63) / 64) % 4 == 0 &&
+                   sc.bvh_levels > 0 && (long long)sc.bvh_leaf0 * 4 + 1 <= kTabNodes;
   for (int k = 0; k < (multi ? fp.H : 1); ++k) {
 #define ART_NEAREST(EX_, OBB_, F_)                                                                                  \
-  hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order,      \
-                     pb.pre, pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr, L, block, pb.vp)
+  do {                                                                                                              \
+    if (tab && k == 0)                                                                                              \
+      hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_, true>), dim3(groups / 4), dim3(1024), 0, st, sc, fp, origins, \
+                         ray_order, pb.pre, pb.state, k, muffle_acc, nacc, pair_count, L, block, pb.vp);           \
+    else                                                                                                            \
+      hipLaunchKernelGGL((nearest_first_kernel<EX_, OBB_, F_>), dim3(groups), dim3(256), 0, st, sc, fp, origins, ray_order,  \
+                         pb.pre, pb.state, k, muffle_acc, k == 0 ? nacc : 0u, k == 0 ? pair_count : nullptr, L, block, pb.vp); \
+  } while (0)
     marked(marks, kMarkNearest, st, [&] {
       if (fold) {
         if (fp.exec) { if (obb) ART_NEAREST(true, true, true); else ART_NEAREST(true, false, true); }

@@ -108,11 +108,12 @@ def host_cpu_info():
 def cpu_leg(cfg, scene, params, org, threads, min_seconds):
     """The oracle (C restatement of the reference jobs, oracle/art_oracle.c) timed on `threads`
     host threads, one fan per task (TC = 1, as the shipped scene): batches of whole fans of this
-    config until at least `min_seconds` of wall time (a bounded sample; fans wrap around)."""
+    config until at least `min_seconds` of wall time (a bounded sample; fans wrap around). The
+    oracle is rebuilt -march=native for this host when gcc is present (oracle.load_native)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle  # CPU baseline leg only
 
-    oracle.load()
+    lib, label = oracle.load_native()
     S = org.shape[0]
     tests, fans, dt, nxt, batch = 0, 0, 0.0, 0, max(1, min(threads, S))
     while dt < min_seconds:
@@ -120,14 +121,14 @@ def cpu_leg(cfg, scene, params, org, threads, min_seconds):
         nxt = (nxt + batch) % S
         out = art.FanOutputs(batch, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None)
         t0 = time.perf_counter()
-        _, counts = oracle.run(scene, params, np.ascontiguousarray(org[idx]), out, threads=threads)
+        _, counts = oracle.run(scene, params, np.ascontiguousarray(org[idx]), out, threads=threads, lib=lib)
         dt += time.perf_counter() - t0
         tests += sum(counts.values())
         fans += batch
         per_fan = dt / fans
         want = int((min_seconds - dt) / per_fan) + 1
         batch = max(1, min(S, -(-want // threads) * threads))
-    return {"value": tests / dt, "seconds": dt, "tests": tests, "fans": fans}
+    return {"value": tests / dt, "seconds": dt, "tests": tests, "fans": fans, "build": label}
 
 
 def cpu_baseline(cfg, scene, params, org, min_seconds):
@@ -138,8 +139,8 @@ def cpu_baseline(cfg, scene, params, org, min_seconds):
     return {"value": many["value"], "unit": "ray-collider tests/s", "cores": n, "kind": "port",
             "label": "reference algorithm (C restatement of the Burst jobs, oracle/art_oracle.c; Burst cannot run here)",
             "sample": f"{many['fans']} fans of config {cfg.index} ({many['tests']} reference tests, {many['seconds']:.1f} s) "
-                      f"on {n} threads, one fan per task; gcc -O3 -march=x86-64-v3 -ffp-contract=off (x86-64-v3, "
-                      "not -march=native: the oracle library is built in the container and runs on the GPU box's host)",
+                      f"on {n} threads, one fan per task; oracle built with {many['build']}",
+            "build": many["build"],
             "one_thread": {"value": one["value"], "unit": "ray-collider tests/s",
                            "sample": f"{one['fans']} fans ({one['tests']} tests, {one['seconds']:.1f} s) on 1 thread"},
             "host": host}
@@ -525,6 +526,55 @@ def main_cpu(a):
         "threads_n": res["n"], "threads_1": res["one"], "host": host}))
 
 
+def verify_allgather(ctx, dist, backend, world, rank, org_all, S_total, d_org, S, d_blk, stride, dev, sp):
+    """N > 1, outside the timed region: the process group has the expected size, every rank sits on
+    its own device under RCCL (ranks may share one only over gloo, the CPU tests' setup), and the
+    all-gathered result blocks equal, byte for byte, rank 0's own launch of a sample of every rank's
+    fans (first, middle and last of each shard; fans are independent, Audio/AudioRayTracer.cs:161-237).
+    Raises on any failure, so a scaling run never reports a number without its correctness check."""
+    import torch.distributed as tdist
+    if tdist.get_world_size() != world:
+        raise RuntimeError(f"process group size {tdist.get_world_size()} != WORLD_SIZE {world}")
+    props = torch.cuda.get_device_properties(dev)
+    ident = (socket_host(), str(getattr(props, "uuid", "")), int(getattr(props, "pci_bus_id", -1)),
+             int(getattr(props, "pci_domain_id", -1)), dev.index)
+    idents = [None] * world
+    tdist.all_gather_object(idents, ident)
+    distinct = len({i[:4] if i[1] or i[2] >= 0 else i for i in idents}) == world
+    if backend == "nccl" and not distinct:
+        raise RuntimeError(f"RCCL ranks share a device: {idents}")
+    ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+    full = art.dist.all_gather_fan_blocks(d_blk[: S * stride], S_total, stride, world)
+    torch.cuda.synchronize()
+    sample = []
+    for r in range(world):
+        b, e = art.dist.shard_range(S_total, world, r)
+        if e > b:
+            sample += sorted({b, (b + e) // 2, e - 1})
+    ok = True
+    if rank == 0:
+        d_s = torch.from_numpy(np.ascontiguousarray(org_all[sample])).to(dev)
+        d_ref = torch.zeros(len(sample) * stride, dtype=torch.uint8, device=dev)
+        ctx.launch_device(d_s.data_ptr(), len(sample), d_ref.data_ptr(), 0, sp)
+        torch.cuda.synchronize()
+        got = torch.stack([full[i * stride:(i + 1) * stride] for i in sample])
+        ok = bool(torch.equal(got.reshape(-1), d_ref))
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+    tdist.broadcast(flag, 0)
+    if not flag.item():
+        raise RuntimeError("all-gathered fan blocks differ from rank 0's own launch of the sampled fans")
+    return {"verified": True, "world_size": tdist.get_world_size(), "backend": backend, "distinct_devices": distinct,
+            "devices": [{"host": i[0], "uuid": i[1], "pci_bus_id": i[2], "local_index": i[4]} for i in idents],
+            "sampled_fans": sample, "bytes_compared": len(sample) * stride,
+            "note": "untimed, after the timed region: the all-gather's output for the sampled fans equals rank 0's own "
+                    "art_launch_device of the same fans byte for byte"}
+
+
+def socket_host():
+    import socket
+    return socket.gethostname()
+
+
 def main():
     a = parse()
     if a.config is None:
@@ -615,6 +665,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    verify = verify_allgather(ctx, dist, a.dist_backend, world, rank, org_all, S_total, d_org, S, d_blk, lay["stride"], dev,
+                              sp) if world > 1 else None
 
     # Kernel durations: untimed passes of the same launches after the timed region, HIP events on
     # the streams the kernels run on. Pass 1: the frame's stages only (raytrace stage, permeation
@@ -631,6 +683,8 @@ def main():
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
     keach = ctx.kernel_timing()
     ctx.set_flags(0)
+    if keach["kernel_marks_dropped"]:  # a family's time would be missing launches: never report it silently
+        raise RuntimeError(f"per-kernel timing dropped {keach['kernel_marks_dropped']} launch marks")
     # the all-gather alone: HIP events on the launch stream around the collective of n_pass frames
     allgather_ms = None
     if world > 1:
@@ -753,6 +807,8 @@ def main():
                    "parallelism": f"fan-sharded x{world}" + (f" + all-gather ({'RCCL' if a.dist_backend == 'nccl' else 'gloo'})"
                                                               if world > 1 else "")},
         "allgather_ms": allgather_ms,
+        "allgather_verified": verify["verified"] if verify else None,
+        "allgather_verify": verify,
         "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
         "allgather_note": f"HIP events on the launch stream around the all-gather of {n_pass} untimed frames after the "
                           "timed region, max over ranks; the step time includes it" if world > 1 else None,
@@ -802,7 +858,8 @@ def main():
                                      "(2 x FETCH_SIZE + WRITE_SIZE, same build) / stage time"}},
         "kernel_ms": {"raytrace": rt_ms, "permeate": ktimes["permeate_ms"] / n_rt, "reduce": ktimes["reduce_ms"] / n_rt,
                       **{k: v["ms_per_frame"] for k, v in kernels.items()},
-                      "frames_timed": n_rt, "note": f"pass 1 (stage events only, {n_pass} untimed frames after the timed "
+                      "frames_timed": n_rt, "kernel_marks_dropped": keach["kernel_marks_dropped"],
+                      "note": f"pass 1 (stage events only, {n_pass} untimed frames after the timed "
                                                     "region); per kernel family: pass 2 (ART_CTX_TIME_EACH_KERNEL)"},
         "lib_sha256": lib_sha256(),
         "cpu_baseline": cpu,

@@ -59,6 +59,11 @@ typedef struct {
 /* Frame outputs from the reference-order raytrace kernel (one ray per lane, every collider in
  * reference order; the kernel the test counts come from) instead of the throughput stage. */
 #define ART_CTX_FORCE_REFERENCE_ORDER 0x4u
+/* art_launch_device records the frame's completion event on the caller's stream before it returns
+ * (ABI 3.1), so the caller may destroy or recycle that stream right after the call. Off by default:
+ * the record costs the stream ~5 us of GPU idle per frame, and without it the event is recorded
+ * lazily, on that stream, by the next call that has to wait for the frame. */
+#define ART_CTX_EVENT_EACH_LAUNCH 0x400u
 /* (0x8, 0x40 and 0x80 selected round-1 alternative raytrace implementations; they are gone and
  * the bits are reserved.) */
 
@@ -76,7 +81,9 @@ ART_API int art_scene_bind(art_ctx* ctx, const art_frame_desc* desc);
  * (NULL = the HIP default stream, e.g. torch's default stream). Kernels only; returns without
  * synchronizing and records no event (back-to-back frames run without gaps). The stream must stay
  * valid until the context's next call that touches the scene or its buffers (a bind, sync,
- * schedule, or a launch on another stream), which orders itself after the frame. */
+ * schedule, a launch on another stream, or art_destroy), which orders itself after the frame by
+ * recording an event on it then; a caller that cannot keep its stream alive that long sets
+ * ART_CTX_EVENT_EACH_LAUNCH. */
 ART_API int art_launch_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,
                               uint32_t out_flags, void* stream);
 
@@ -90,6 +97,14 @@ ART_API int art_fibonacci_directions_device(art_ctx* ctx, int32_t count, art_hal
  * u16[count]) on `stream`: the device conversion every echo, hit point and direction goes through,
  * exposed so it can be checked against the host and the oracle over all 2^32 inputs. */
 ART_API int art_f32tof16_device(art_ctx* ctx, uint32_t first_bits, uint32_t count, uint16_t* d_out, void* stream);
+
+/* The OBB slab's reciprocal as the kernels compute it (recip_exact: v_rcp_f32 + one Newton step
+ * where the exponent field lies in [3, 251], the IEEE division elsewhere), the bits of 1/x for
+ * x = first_bits .. first_bits + count - 1 (wrapping) into d_out (HBM, u32[count]) on `stream`:
+ * exposed so the claim that it equals 1.0f / x (RayIntersectsAABB's `1.0f / rayDir`,
+ * Jobs/AudioRaytracerJobBatched.cs:289, reached from RayIntersectsOBB :314-320) is checked
+ * over all 2^32 inputs. */
+ART_API int art_recip_exact_device(art_ctx* ctx, uint32_t first_bits, uint32_t count, uint32_t* d_out, void* stream);
 
 /* Same frame with the test-counting kernels (for the tests/s metric); synchronizes. */
 ART_API int art_count_device(art_ctx* ctx, const float* d_origins, int32_t fan_count, void* d_block,

@@ -23,6 +23,35 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "libart_oracle.so")
 
 _lib = None
+_native = None
+
+
+def load_native():
+    """bench.py's CPU-baseline leg only: the oracle rebuilt with -march=native for the host it runs
+    on (SURVEY.md 8(d)'s recipe), into a scratch directory, when gcc is present; otherwise the shipped
+    x86-64-v3 library. Returns (library, label of the build that ran). The checker (load()) stays
+    the portable build, so parity never depends on the host's instruction set."""
+    global _native
+    if _native is not None:
+        return _native
+    import shutil
+    import tempfile
+    label = "gcc -O3 -march=x86-64-v3 -ffp-contract=off (the shipped portable build: no compiler on this host)"
+    path = None
+    if shutil.which("gcc"):
+        d = tempfile.mkdtemp(prefix="art_oracle_native_")
+        path = os.path.join(d, "libart_oracle_native.so")
+        cmd = ["gcc", "-O3", "-march=native", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-pthread",
+               "-shared", "-o", path, os.path.join(ORACLE_DIR, "art_oracle.c"), "-lm"]
+        try:
+            subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+            label = "gcc -O3 -march=native -ffp-contract=off, built on this host at run time"
+        except Exception as e:  # noqa: BLE001 - fall back to the portable build, and say so
+            path = None
+            label += f" (native build failed: {type(e).__name__})"
+    lib = _bind(C.CDLL(path)) if path else load()
+    _native = (lib, label)
+    return _native
 
 
 def load():
@@ -31,7 +60,11 @@ def load():
         return _lib
     if not os.path.exists(ORACLE_LIB):
         subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
-    lib = C.CDLL(ORACLE_LIB)
+    _lib = _bind(C.CDLL(ORACLE_LIB))
+    return _lib
+
+
+def _bind(lib):
     lib.or_f32tof16.restype = C.c_uint16
     lib.or_f32tof16.argtypes = [C.c_float]
     lib.or_f32tof16_range.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p]
@@ -55,13 +88,12 @@ def load():
     lib.or_half_quaternion_value.argtypes = [C.c_uint16, C.c_uint16, C.c_uint16, f4]
     lib.or_quat_inverse.argtypes = [f4, f4]
     lib.or_quat_mul_vec.argtypes = [f4, f3, f3]
-    _lib = lib
     return lib
 
 
-def run_frame(frame: Frame, threads: int = 1):
+def run_frame(frame: Frame, threads: int = 1, lib=None):
     """Run the oracle on `frame` (writes into frame.out); returns the per-kind test counts."""
-    lib = load()
+    lib = lib or load()
     cnt = abi.art_test_counts()
     rc = lib.or_run_frame(C.byref(frame.desc), frame.fans, frame.S, threads, C.byref(cnt))
     if rc:
@@ -69,9 +101,9 @@ def run_frame(frame: Frame, threads: int = 1):
     return cnt.as_dict()
 
 
-def run(scene, params, origins, out: FanOutputs, threads: int = 1):
+def run(scene, params, origins, out: FanOutputs, threads: int = 1, lib=None):
     fr = Frame(scene, params, origins, out)
-    counts = run_frame(fr, threads)
+    counts = run_frame(fr, threads, lib)
     return out, counts
 
 

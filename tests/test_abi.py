@@ -77,7 +77,9 @@ def test_header_struct_sizes_match_bindings(tmp_path):
 
 def test_version():
     v = art.load_library().art_version()
-    assert v >> 16 == 3 and v & 0xffff >= 0  # 3.0: art_kernel_times per kernel family (a grown struct: major bump)
+    # 3.0: art_kernel_times per kernel family (a grown struct: major bump); 3.1: ART_CTX_EVENT_EACH_LAUNCH,
+    # art_recip_exact_device
+    assert v >> 16 == 3 and v & 0xffff >= 1
 
 
 def test_no_gpu_fails_loudly():

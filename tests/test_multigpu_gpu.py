@@ -192,3 +192,10 @@ def test_bench_two_ranks_gloo_strong_shards():
     assert two["config"]["reference_tests_per_frame_rank0"] < one["config"]["reference_tests_per_frame_rank0"]
     assert two["allgather_ms"] is not None and two["allgather_ms"] > 0
     assert two["allgather_bytes"] > 0 and one["allgather_ms"] is None
+    # the N > 1 self-check (outside the timed region): group size, device identities, and the gathered
+    # blocks of first / middle / last fans of both shards byte-equal to rank 0's own launch of them
+    v = two["allgather_verify"]
+    assert two["allgather_verified"] is True and v["world_size"] == 2 and v["backend"] == "gloo"
+    assert v["sampled_fans"] == [0, 256, 511, 512, 768, 1023] and v["bytes_compared"] > 0
+    assert v["distinct_devices"] is False  # both gloo ranks share device 0 here; under nccl this must be True
+    assert one["allgather_verified"] is None

@@ -463,3 +463,95 @@ def test_launch_device_then_schedule_and_bind_without_sync(ctx):
         assert all(got.equal(ref_a).values()), (rnd, got.equal(ref_a))
 
 
+def _hip_runtime():
+    """The HIP runtime already loaded in this process (libart's and torch's), without loading another."""
+    import ctypes
+    for name in ("libamdhip64.so.7", "libamdhip64.so"):
+        try:
+            return ctypes.CDLL(name, mode=os.RTLD_NOLOAD)
+        except OSError:
+            continue
+    pytest.skip("no loaded HIP runtime found")
+
+
+def test_launch_streams_short_lived_and_busy():
+    """The lazy completion event: art_launch_device records no event, the next call
+    that reuses the scene records one on the launch stream. (1) A frame launched on a side stream
+    that then gets more unrelated work, followed by a bind of a changed scene, a launch of it on
+    another stream and art_destroy: both frames equal the oracle. (2) With ART_CTX_EVENT_EACH_LAUNCH
+    the frame's event is recorded by the launch itself, so the caller may destroy its stream at once:
+    a raw HIP stream is destroyed right after the launch, a changed scene is bound and launched, and
+    the context destroyed, with every result equal to the oracle."""
+    import ctypes
+    torch = pytest.importorskip("torch")
+    cfg = art.CONFIGS[5]
+    sa, org, params = art.synth(cfg, S=16, R=128, C_scale=0.25)
+    sb, _, _ = art.synth(art.CONFIGS[2], S=16, R=128, C_scale=0.25)
+    sb = art.Scene(dirs=sa.dirs, targets=sa.targets, spheres=sb.spheres, aabbs=sb.aabbs)
+    refs = {}
+    for k, sc in (("a", sa), ("b", sb)):
+        refs[k] = art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True)
+        oracle.run_frame(art.Frame(sc, params, org, refs[k]), threads=16)
+    fa = art.Frame(sa, params, org, art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True))
+    fb = art.Frame(sb, params, org, art.FanOutputs(16, 128, cfg.H, cfg.T, 1, dsp=True))
+    lay = art.fan_layout(fa)
+    d_org = torch.from_numpy(org.copy()).cuda()
+    hip = _hip_runtime()
+    for mode in ("busy side stream", "destroyed stream"):
+        c = art.Context(1)
+        d_a = torch.zeros(16 * lay["stride"], dtype=torch.uint8, device="cuda")
+        d_b = torch.zeros_like(d_a)
+        c.set_flags(abi.ART_CTX_EVENT_EACH_LAUNCH if mode == "destroyed stream" else 0)
+        c.bind(fa)
+        if mode == "busy side stream":
+            side = torch.cuda.Stream()
+            c.launch_device(d_org.data_ptr(), 16, d_a.data_ptr(), 0, side.cuda_stream)
+            with torch.cuda.stream(side):  # unrelated work queued behind the frame
+                x = torch.randn(1 << 22, device="cuda")
+                for _ in range(8):
+                    x = torch.sin(x) * 1.0001
+        else:
+            raw = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+            c.launch_device(d_org.data_ptr(), 16, d_a.data_ptr(), 0, raw.value)
+            assert hip.hipStreamDestroy(raw) == 0  # the caller drops its stream right after the launch
+        c.bind(fb)
+        st = torch.cuda.current_stream()
+        c.launch_device(d_org.data_ptr(), 16, d_b.data_ptr(), 0, st.cuda_stream)
+        c.close()
+        torch.cuda.synchronize()
+        for k, d in (("a", d_a), ("b", d_b)):
+            got = art.unpack_block(d.cpu().numpy(), lay, 16, 128, cfg.H, cfg.T, 1, dsp=True)
+            assert all(got.equal(refs[k]).values()), (mode, k, got.equal(refs[k]))
+
+
+@pytest.mark.parametrize("ci", [2, 5])
+def test_kernel_timing_launch_counts(ctx, ci):
+    """ART_CTX_TIME_EACH_KERNEL (bench.py's per-kernel roofline times): the launches counted per
+    kernel family follow the frame's plan — a one-hit frame (config 2) is one nearest_first_kernel and
+    one echo_muffle_kernel launch; a folded multi-hit frame (config 5, H = 5) is H nearest launches,
+    H echo vis_kernel launches and one muffle_kernel launch — no mark is dropped, and every family
+    that ran has a positive time."""
+    torch = pytest.importorskip("torch")
+    cfg = art.CONFIGS[ci]
+    scene, org, params = art.synth(cfg, S=32, R=cfg.R, C_scale=0.25)
+    fr = art.Frame(scene, params, org, art.FanOutputs(32, cfg.R, cfg.H, cfg.T, 1, dsp=params.dsp is not None))
+    lay = art.fan_layout(fr)
+    ctx.set_flags(0)
+    ctx.bind(fr)
+    d_org = torch.from_numpy(np.ascontiguousarray(org)).cuda()
+    d_blk = torch.zeros(32 * lay["stride"], dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    n = 6
+    ctx.set_flags(abi.ART_CTX_TIME_KERNELS | abi.ART_CTX_TIME_EACH_KERNEL)
+    ctx.kernel_timing()  # reset
+    for _ in range(n):
+        ctx.launch_device(d_org.data_ptr(), 32, d_blk.data_ptr(), 0, st.cuda_stream)
+    t = ctx.kernel_timing()
+    ctx.set_flags(0)
+    want = ({"nearest_first_kernel": 1, "echo_muffle_kernel": 1, "vis_kernel": 0, "muffle_kernel": 0} if cfg.H == 1 else
+            {"nearest_first_kernel": cfg.H, "echo_muffle_kernel": 0, "vis_kernel": cfg.H, "muffle_kernel": 1})
+    assert t["launches"] == n and t["kernel_marks_dropped"] == 0
+    assert {k: v // n for k, v in t["kernel_launches"].items()} == want
+    assert all(t["kernel_launches"][k] == n * w for k, w in want.items())
+    assert all((t["kernel_ms"][k] > 0) == (w > 0) for k, w in want.items())
