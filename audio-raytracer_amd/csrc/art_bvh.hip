@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "art_device_fns.hpp"
+#include "art_frame_math.hpp"
 
 namespace art {
 
@@ -148,60 +149,77 @@ __device__ __forceinline__ void cull_union_stored(CullRec& a, const CullRec& b) 
 // Leaf j = sorted colliders [kBvhLeaf j, kBvhLeaf (j + 1)) (empty past the last); writes the
 // leaf references.
 // REFIT: the leaf order is kept (ref holds it) and only bounds and slots are recomputed.
+// Leaf slot k holding collider g (global order; g < 0: an empty slot past the last collider).
+__device__ __forceinline__ void bvh_write_slot(int k, int g, int ns, int na, int n, const SphereRec* __restrict__ sph,
+                                               const AabbRec* __restrict__ aabb, const ObbRec* __restrict__ obb,
+                                               float4* __restrict__ slots) {
+  const int per = n - ns - na > 0 ? 4 : 2;  // float4s per slot (bvh_slot_bytes)
+  float4* sl = slots + per * (size_t)k;
+  float4 a = make_float4(0, 0, 0, 0), b = a, c = a, d = a;
+  int code = -1;
+  if (g >= 0) {
+    if (g < ns) {
+      const SphereRec r = sph[g];
+      a = make_float4(r.cx, r.cy, r.cz, r.r2);
+      b.z = __int_as_float(r.tid);
+      code = g;
+    } else if (g < ns + na) {
+      const AabbRec r = aabb[g - ns];
+      a = make_float4(r.mnx, r.mny, r.mnz, r.mxx);
+      b = make_float4(r.mxy, r.mxz, __int_as_float(r.tid), 0.0f);
+      code = (1 << 28) | (g - ns);
+    } else {
+      const ObbRec r = obb[g - ns - na];
+      a = make_float4(r.cx, r.cy, r.cz, r.qx);
+      b = make_float4(r.qy, r.qz, r.qw, 0.0f);
+      c = make_float4(r.lmnx, r.lmny, r.lmnz, r.lmxx);
+      d = make_float4(r.lmxy, r.lmxz, __int_as_float(r.tid), 0.0f);
+      code = (2 << 28) | (g - ns - na);
+    }
+  }
+  b.w = __int_as_float(code);
+  sl[0] = a; sl[1] = b;
+  if (per == 4) { sl[2] = c; sl[3] = d; }
+}
+// the global index of the collider in leaf position k (bvh_ref: type << 30 | in-type index)
+__device__ __forceinline__ int bvh_ref_global(uint32_t r, int ns, int na) {
+  const uint32_t t = r >> 30, i = r & 0x3fffffffu;
+  return (int)i + (t == 0 ? 0 : (t == 1 ? ns : ns + na));
+}
+
 template <bool REFIT>
-__global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __restrict__ perm, int ns, int na, int n,
-                                const SphereRec* __restrict__ sph, const AabbRec* __restrict__ aabb,
-                                const ObbRec* __restrict__ obb, CullRec* __restrict__ leaves, int nleaf,
-                                uint32_t* __restrict__ ref, float4* __restrict__ slots) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nleaf) return;
+__device__ __forceinline__ void bvh_leaf_one(int j, const CullRec* __restrict__ cull, const int* __restrict__ perm, int ns,
+                                             int na, int n, const SphereRec* __restrict__ sph, const AabbRec* __restrict__ aabb,
+                                             const ObbRec* __restrict__ obb, CullRec* __restrict__ leaves,
+                                             uint32_t* __restrict__ ref, float4* __restrict__ slots,
+                                             uint32_t* __restrict__ pos = nullptr) {
   CullRec u = cull_empty();
   // slot (64 B; 32 B in scenes without OBBs, so a leaf is one 128-B line): a = first 16 B,
   // b = next 16 B (b.w = code), c, d = an OBB's local bounds
   //   sphere: a = (cx, cy, cz, r2), b.z = AudioTargetId
   //   AABB:   a = (mn.xyz, mx.x), b.xy = mx.yz, b.z = AudioTargetId
   //   OBB:    a = (c.xyz, q.x), b.xyz = q.yzw, c = (lmn.xyz, lmx.x), d.xy = lmx.yz, d.z = AudioTargetId
-  const int per = n - ns - na > 0 ? 4 : 2;  // float4s per slot (bvh_slot_bytes)
   for (int k = j * kBvhLeaf; k < (j + 1) * kBvhLeaf; ++k) {
-    float4* sl = slots + per * (size_t)k;
-    float4 a = make_float4(0, 0, 0, 0), b = a, c = a, d = a;
-    int code = -1;
+    int g = -1;
     if (k < n) {
-      int g;
-      if (REFIT) {
-        const uint32_t r = ref[k], t = r >> 30, i = r & 0x3fffffffu;
-        g = (int)i + (t == 0 ? 0 : (t == 1 ? ns : ns + na));
-      } else {
-        g = perm[k];
-      }
+      g = REFIT ? bvh_ref_global(ref[k], ns, na) : perm[k];
       cull_union(u, cull[g]);
-      if (g < ns) {
-        ref[k] = (uint32_t)g;
-        const SphereRec r = sph[g];
-        a = make_float4(r.cx, r.cy, r.cz, r.r2);
-        b.z = __int_as_float(r.tid);
-        code = g;
-      } else if (g < ns + na) {
-        ref[k] = (1u << 30) | (uint32_t)(g - ns);
-        const AabbRec r = aabb[g - ns];
-        a = make_float4(r.mnx, r.mny, r.mnz, r.mxx);
-        b = make_float4(r.mxy, r.mxz, __int_as_float(r.tid), 0.0f);
-        code = (1 << 28) | (g - ns);
-      } else {
-        ref[k] = (2u << 30) | (uint32_t)(g - ns - na);
-        const ObbRec r = obb[g - ns - na];
-        a = make_float4(r.cx, r.cy, r.cz, r.qx);
-        b = make_float4(r.qy, r.qz, r.qw, 0.0f);
-        c = make_float4(r.lmnx, r.lmny, r.lmnz, r.lmxx);
-        d = make_float4(r.lmxy, r.lmxz, __int_as_float(r.tid), 0.0f);
-        code = (2 << 28) | (g - ns - na);
+      if (!REFIT) {
+        ref[k] = g < ns ? (uint32_t)g : (g < ns + na ? (1u << 30) | (uint32_t)(g - ns) : (2u << 30) | (uint32_t)(g - ns - na));
+        if (pos) pos[g] = (uint32_t)k;
       }
     }
-    b.w = __int_as_float(code);
-    sl[0] = a; sl[1] = b;
-    if (per == 4) { sl[2] = c; sl[3] = d; }
+    bvh_write_slot(k, g, ns, na, n, sph, aabb, obb, slots);
   }
   leaves[j] = cull_stored(u);
+}
+template <bool REFIT>
+__global__ void bvh_leaf_kernel(const CullRec* __restrict__ cull, const int* __restrict__ perm, int ns, int na, int n,
+                                const SphereRec* __restrict__ sph, const AabbRec* __restrict__ aabb,
+                                const ObbRec* __restrict__ obb, CullRec* __restrict__ leaves, int nleaf,
+                                uint32_t* __restrict__ ref, float4* __restrict__ slots, uint32_t* __restrict__ pos) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < nleaf) bvh_leaf_one<REFIT>(j, cull, perm, ns, na, n, sph, aabb, obb, leaves, ref, slots, pos);
 }
 
 // One inner level l (large trees: levels with more nodes than one workgroup handles quickly).
@@ -899,10 +917,92 @@ int launch_build_bvh(DevScene& sc, const SortBufs& sb, hipStream_t st) {
       return -1;
   }
   hipLaunchKernelGGL(bvh_leaf_kernel<false>, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, sb.perm, sc.ns, sc.na, n,
-                     sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
+                     sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf, sb.bvh_pos);
   launch_bvh_upper(sb.bvh, L, st);
   sc.bvh = sb.bvh; sc.bvh_ref = sb.bvh_ref; sc.bvh_leaf = sb.bvh_leaf; sc.bvh_levels = L; sc.bvh_leaf0 = leaf0;
   return 0;
+}
+
+// A resident-store sync of a scene of up to kSyncRefitMax colliders (art_colliders_sync, round 6)
+// in one workgroup and one launch, touching only what moved: the dirty records written and decoded
+// (scatter_prep_kernel's work, read straight from the pinned host image: no copy), their leaf
+// slots rewritten at their leaf positions (bvh_pos), the boxes of their leaves recomputed, then
+// every ancestor of a changed node, level by level up to the root (a bitmap of changed nodes in
+// LDS). The result equals a full refit (bvh_leaf_kernel<true> + the inner levels): untouched nodes
+// are unions of unchanged children. Config 2's dynamic step: one ~6-us launch in place of a copy,
+// three kernels and their gaps.
+constexpr int kSyncRefitNodes = (int)(kSyncRefitMax / kBvhLeaf) * 4 / 3 + 1;  // nodes of the largest such tree
+__global__ __launch_bounds__(1024) void sync_refit_kernel(ScatterArgs a, DevScene sc, CullRec* __restrict__ nodes,
+                                                          const uint32_t* __restrict__ ref, const uint32_t* __restrict__ pos,
+                                                          float4* __restrict__ slots) {
+  __shared__ uint32_t s_dirty[(kSyncRefitNodes + 31) / 32];
+  const int tid = threadIdx.x;
+  const int n = sc.ns + sc.na + sc.no, leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1;
+  const int nd = a.ds + a.da + a.dob;
+  for (int w = tid; w < (leaf0 + nleaf + 31) / 32; w += blockDim.x) s_dirty[w] = 0u;
+  __syncthreads();
+  for (int j = tid; j < nd; j += blockDim.x) {  // 1. the dirty records
+    int k = j, g;
+    if (k < a.ds) {
+      const int i = a.idx_s[k];
+      const art_sphere r = a.rec_s[k];
+      a.sph[i] = r;
+      prep_sphere(r, i, i, a.osph, a.osphc, a.cull);
+      g = i;
+    } else if ((k -= a.ds) < a.da) {
+      const int i = a.idx_a[k];
+      const art_aabb r = a.rec_a[k];
+      a.aabb[i] = r;
+      prep_aabb(r, i, a.ns + i, a.oaabb, a.oaabbc, a.cull);
+      g = a.ns + i;
+    } else {
+      k -= a.da;
+      const int i = a.idx_o[k];
+      const art_obb r = a.rec_o[k];
+      a.obb[i] = r;
+      prep_obb(r, i, a.ns + a.na + i, a.oobb, a.oobbc, a.cull);
+      g = a.ns + a.na + i;
+    }
+    const int leaf = leaf0 + (int)(pos[g] / kBvhLeaf);
+    atomicOr(&s_dirty[leaf >> 5], 1u << (leaf & 31));
+  }
+  __syncthreads();
+  for (int j = tid; j < nd; j += blockDim.x) {  // 2. their leaf slots, from the records written above
+    int k = j, g;
+    if (k < a.ds) g = a.idx_s[k];
+    else if ((k -= a.ds) < a.da) g = a.ns + a.idx_a[k];
+    else g = a.ns + a.na + a.idx_o[k - a.da];
+    bvh_write_slot((int)pos[g], g, sc.ns, sc.na, n, sc.sph, sc.aabb, sc.obb, slots);
+  }
+  for (int i = tid; i < nleaf; i += blockDim.x) {  // ... and the boxes of their leaves
+    const int node = leaf0 + i;
+    if (!((s_dirty[node >> 5] >> (node & 31)) & 1u)) continue;
+    CullRec u = cull_empty();
+    for (int k = i * kBvhLeaf; k < (i + 1) * kBvhLeaf && k < n; ++k) cull_union(u, sc.cull[bvh_ref_global(ref[k], sc.ns, sc.na)]);
+    nodes[node] = cull_stored(u);
+  }
+  __syncthreads();
+  for (int l = sc.bvh_levels - 2; l >= 0; --l) {  // 3. the changed nodes' ancestors
+    const int first = ((1 << (2 * l)) - 1) / 3, cnt = 1 << (2 * l);
+    for (int i = tid; i < cnt; i += blockDim.x) {
+      const int g = first + i;
+      bool any = false;
+      for (int k = 1; k <= 4; ++k) any |= ((s_dirty[(4 * g + k) >> 5] >> ((4 * g + k) & 31)) & 1u) != 0u;
+      if (!any) continue;
+      CullRec u = cull_empty();
+      for (int k = 1; k <= 4; ++k) cull_union_stored(u, nodes[4 * g + k]);
+      nodes[g] = cull_stored(u);
+      atomicOr(&s_dirty[g >> 5], 1u << (g & 31));
+    }
+    __syncthreads();
+  }
+}
+
+bool launch_sync_refit(const ScatterArgs& a, DevScene& sc, const SortBufs& sb, hipStream_t st) {
+  const long long n = (long long)sc.ns + sc.na + sc.no;
+  if (n == 0 || n > kSyncRefitMax || sc.bvh_levels == 0 || !sb.bvh || !sb.bvh_pos) return false;
+  hipLaunchKernelGGL(sync_refit_kernel, dim3(1), dim3(1024), 0, st, a, sc, sb.bvh, sb.bvh_ref, sb.bvh_pos, sb.bvh_leaf);
+  return true;
 }
 
 // Colliders moved but their counts did not: keep the leaf order and recompute the leaf slots and
@@ -913,7 +1013,8 @@ int launch_refit_scene(DevScene& sc, const SortBufs& sb, hipStream_t st) {
   if (n == 0 || sc.bvh_levels == 0) return launch_sort_scene(sc, sb, st);
   const int leaf0 = sc.bvh_leaf0, nleaf = 3 * leaf0 + 1;  // 4^(L-1) leaves
   hipLaunchKernelGGL(bvh_leaf_kernel<true>, dim3((nleaf + 255) / 256), dim3(256), 0, st, sc.cull, (const int*)nullptr,
-                     sc.ns, sc.na, n, sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf);
+                     sc.ns, sc.na, n, sc.sph, sc.aabb, sc.obb, sb.bvh + leaf0, nleaf, sb.bvh_ref, sb.bvh_leaf,
+                     (uint32_t*)nullptr);
   launch_bvh_upper(sb.bvh, sc.bvh_levels, st);
   return 0;
 }

@@ -110,7 +110,7 @@ struct Frame {
          off_reset = 0, off_order = 0, raw_bytes = 0;
   size_t soa_sph = 0, soa_aabb = 0, soa_obb = 0, soa_sphc = 0, soa_aabbc = 0, soa_obbc = 0, soa_cull = 0, soa_bytes = 0;
   size_t soa_box = 0, soa_keys = 0, soa_keys_s = 0, soa_vals = 0, soa_perm = 0, soa_temp = 0, sort_temp = 0;
-  size_t soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_leaf = 0, soa_kd = 0;
+  size_t soa_bvh = 0, soa_bvh_ref = 0, soa_bvh_pos = 0, soa_bvh_leaf = 0, soa_kd = 0;
   // muffle candidate lists (art_cells.hip)
   size_t soa_ccount = 0, soa_cstart = 0, soa_ccur = 0, soa_cfar = 0, soa_cok = 0, soa_ctemp = 0, soa_cent = 0, soa_cent_s = 0, soa_ckeys = 0, soa_ctot = 0, soa_cbox = 0, cells_temp = 0,
          soa_cgeo = 0;
@@ -132,7 +132,8 @@ struct Device {
   int st_cap[3] = {0, 0, 0};
   DevScene st_sc{};             // collider pointers of the store (counts = last sync)
   bool st_fresh = true;         // capacity (re)allocated: every record must be uploaded
-  hipEvent_t st_done = nullptr; // recorded after the last sync's upload + decode (dv.stream)
+  hipEvent_t st_done = nullptr; // recorded after the last sync's upload + decode (on st_stream)
+  hipStream_t st_stream = nullptr;  // the stream the last sync ran on (dv.stream or a device-path launch stream)
   bool st_pending = false;      // st_done recorded and the host staging may still be read
   hipEvent_t launch_done = nullptr;  // after the last art_launch_device frame (caller's stream)
   bool launch_pending = false;       // work on dv.stream waits for it before reusing the scene / buffers
@@ -482,6 +483,7 @@ void make_frame(const art_frame_desc* d, uint32_t out_flags, Frame& f, const int
     f.soa_temp = s; s = align_up(s + f.sort_temp, 256);
     f.soa_bvh = s; s = align_up(s + bvh_node_count((int)n) * sizeof(CullRec), 256);
     f.soa_bvh_ref = s; s = align_up(s + n * 4, 256);
+    f.soa_bvh_pos = s; s = align_up(s + n * 4, 256);
     f.soa_bvh_leaf = s; s = align_up(s + bvh_slot_count((int)n) * 64, 256);
     f.soa_kd = s; s = align_up(s + kd_scratch_bytes((int)n), 256);
   }
@@ -622,6 +624,7 @@ int upload_scene(art_ctx* c, Device& dv, const Frame& f, const uint8_t* h_in) {
   sb.temp = soa + f.soa_temp; sb.temp_bytes = f.sort_temp;
   sb.bvh = bvh_node_count(f.ns + f.na + f.no) ? reinterpret_cast<CullRec*>(soa + f.soa_bvh) : nullptr;
   sb.bvh_ref = reinterpret_cast<uint32_t*>(soa + f.soa_bvh_ref);
+  sb.bvh_pos = reinterpret_cast<uint32_t*>(soa + f.soa_bvh_pos);
   sb.bvh_leaf = reinterpret_cast<float4*>(soa + f.soa_bvh_leaf);
   sb.kd = kd_scratch_bytes(f.ns + f.na + f.no) ? soa + f.soa_kd : nullptr;
   sc.bvh = nullptr; sc.bvh_ref = nullptr; sc.bvh_leaf = nullptr; sc.bvh_levels = 0;
@@ -1427,7 +1430,7 @@ static int launch_common(art_ctx* c, const float* d_origins, int32_t fan_count, 
     f.L = make_layout(&tmp, out_flags);
   }
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL is the HIP default stream (torch's default)
-  if (f.resident && dv.st_done) HIP_TRY(c, hipStreamWaitEvent(st, dv.st_done, 0));
+  if (f.resident && dv.st_done && st != dv.st_stream) HIP_TRY(c, hipStreamWaitEvent(st, dv.st_done, 0));
   // frames share the context's accumulators and pair buffers: a launch on another stream than the
   // previous one waits for it (on the same stream, stream order already does)
   if (dv.launch_pending && st != dv.launch_stream) {
@@ -1751,26 +1754,39 @@ ART_API int art_colliders_sync(art_ctx* c) {
     auto* oobb = reinterpret_cast<ObbRec*>(soa + s_obb);
     auto* oobbc = reinterpret_cast<ObbCold*>(soa + s_obbc);
     auto* cull = reinterpret_cast<CullRec*>(soa + s_cull);
-    // device-path frames on other streams still read the records / BVH being rewritten: wait for them
-    if (int rc = wait_launch(c, dv)) return rc;
-    if (nd) {
-      HIP_TRY(c, hipMemcpyAsync(up, h, bytes, hipMemcpyHostToDevice, dv.stream));
+    // Device-path frames still read the records / BVH being rewritten. The sync runs on the stream of
+    // the last such frame when its completion is not recorded yet (the stream is valid until this
+    // call, art_device.h): stream order puts it after that frame and before the next launch on the
+    // same stream, with no cross-stream events (each costs the queue ~5-10 us of idle). Otherwise
+    // it runs on the context stream, after the frame's completion event.
+    const hipStream_t ss = (dv.launch_pending && !dv.launch_recorded) ? dv.launch_stream : dv.stream;
+    if (ss == dv.stream)
+      if (int rc = wait_launch(c, dv)) return rc;
+    dv.st_stream = ss;
+    // moved colliders of a bound resident scene: one launch scatters the records from the pinned image
+    // and refits the BVH (launch_sync_refit), below
+    const bool refit_follows = nd && dv.bound && c->fr.resident && !counts_changed;
+    const bool fused = refit_follows && (long long)n[0] + n[1] + n[2] <= kSyncRefitMax && dv.sc.bvh_levels > 0 && dv.sb.bvh;
+    if (nd && !fused) {
+      HIP_TRY(c, hipMemcpyAsync(up, h, bytes, hipMemcpyHostToDevice, ss));
       launch_scatter_prep(reinterpret_cast<const int*>(up + off_idx[0]), reinterpret_cast<const art_sphere*>(up + off_rec[0]),
                           (int)lists[0].size(), reinterpret_cast<const int*>(up + off_idx[1]),
                           reinterpret_cast<const art_aabb*>(up + off_rec[1]), (int)lists[1].size(),
                           reinterpret_cast<const int*>(up + off_idx[2]), reinterpret_cast<const art_obb*>(up + off_rec[2]),
                           (int)lists[2].size(), sph, aabb, obb, n[0], n[1], osph, osphc, oaabb, oaabbc, oobb, oobbc, cull,
-                          dv.stream);
+                          ss);
       HIP_TRY(c, hipGetLastError());
     }
     // a count change moves the bounds of the later kinds (global order spheres, AABBs, OBBs)
     if (counts_changed && !fresh && n[0] + n[1] + n[2] > 0) {
-      launch_prep(sph, n[0], aabb, n[1], obb, n[2], osph, osphc, oaabb, oaabbc, oobb, oobbc, cull, dv.stream);
+      launch_prep(sph, n[0], aabb, n[1], obb, n[2], osph, osphc, oaabb, oaabbc, oobb, oobbc, cull, ss);
       HIP_TRY(c, hipGetLastError());
     }
-    // stream-ordered: frames on dv.stream follow; device-path launches on other streams wait on st_done
+    // stream-ordered: frames on ss follow; device-path launches on other streams wait on st_done (and
+    // work on dv.stream, after a sync on the launch stream, waits through wait_launch). One record
+    // per sync: a refit below records it after its kernels (each record costs the queue ~5 us).
     if (!dv.st_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.st_done, hipEventDisableTiming));
-    HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));
+    if (!refit_follows) HIP_TRY(c, hipEventRecord(dv.st_done, ss));
     dv.st_pending = true;
     DevScene& t = dv.st_sc;
     t.sph = osph; t.sphc = osphc; t.ns = n[0];
@@ -1788,13 +1804,31 @@ ART_API int art_colliders_sync(art_ctx* c) {
         dv.sc.cull = t.cull;
         // moved colliders: refit the sorted copies and the BVH in place (device only, no H2D)
         if (nd) {
-          if (launch_refit_scene(dv.sc, dv.sb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "collider refit failed");
+          if (fused) {
+            void* hd = nullptr;  // the pinned image as the device sees it
+            HIP_TRY(c, hipHostGetDevicePointer(&hd, h, 0));
+            const uint8_t* u = static_cast<const uint8_t*>(hd);
+            ScatterArgs a;
+            a.idx_s = reinterpret_cast<const int*>(u + off_idx[0]); a.rec_s = reinterpret_cast<const art_sphere*>(u + off_rec[0]);
+            a.ds = (int)lists[0].size();
+            a.idx_a = reinterpret_cast<const int*>(u + off_idx[1]); a.rec_a = reinterpret_cast<const art_aabb*>(u + off_rec[1]);
+            a.da = (int)lists[1].size();
+            a.idx_o = reinterpret_cast<const int*>(u + off_idx[2]); a.rec_o = reinterpret_cast<const art_obb*>(u + off_rec[2]);
+            a.dob = (int)lists[2].size();
+            a.sph = sph; a.aabb = aabb; a.obb = obb; a.ns = n[0]; a.na = n[1];
+            a.osph = osph; a.osphc = osphc; a.oaabb = oaabb; a.oaabbc = oaabbc; a.oobb = oobb; a.oobbc = oobbc; a.cull = cull;
+            if (!launch_sync_refit(a, dv.sc, dv.sb, ss)) return fail(c, ART_E_DEVICE, "collider sync refit not applicable");
+            HIP_TRY(c, hipGetLastError());
+          } else if (launch_refit_scene(dv.sc, dv.sb, ss) != 0) {
+            (void)hipEventRecord(dv.st_done, ss);
+            return fail(c, ART_E_DEVICE, "collider refit failed");
+          }
           if (!cells_ok) {
-            if (launch_build_cells(dv.sc, dv.cb, dv.stream) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
+            if (launch_build_cells(dv.sc, dv.cb, ss) != 0) return fail(c, ART_E_DEVICE, "muffle cell lists failed");
             cells_rebuilt = true;
           }
           if (dv.sorted_gen != ~0ull) dv.sorted_gen = c->sync_gen;
-          HIP_TRY(c, hipEventRecord(dv.st_done, dv.stream));  // device-path launches wait for the sort too
+          HIP_TRY(c, hipEventRecord(dv.st_done, ss));  // device-path launches wait for the sort too
         }
       }
     }

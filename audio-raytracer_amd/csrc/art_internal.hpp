@@ -127,6 +127,7 @@ struct SortBufs {
   uint32_t* keys; uint32_t* keys_s; int* vals; int* perm;
   void* temp; size_t temp_bytes;
   CullRec* bvh; uint32_t* bvh_ref;  // BVH nodes (bvh_node_count) and leaf references
+  uint32_t* bvh_pos;                // leaf position of each collider (global order): bvh_ref's inverse
   float4* bvh_leaf;                 // leaf slots (bvh_slot_count)
   void* kd;                         // kd leaf-order scratch (kd_scratch_bytes; NULL: Morton order)
 };
@@ -135,6 +136,23 @@ int dsp_source_params(const art_spatializer_settings& st, const art_audio_source
                       art_dsp_source_params& p);
 void launch_dsp(float* data, unsigned long long data_bytes, const long long* offsets, const int* frames_of,
                 int frames_all, const art_dsp_source_params* params, art_dsp_state* state, int count, hipStream_t st);
+
+// Dirty records of a resident-store sync (art_colliders_sync): the update image (indices and
+// records per kind) and the resident lists and decoded records they are scattered into.
+struct ScatterArgs {
+  const int* idx_s; const art_sphere* rec_s; int ds;
+  const int* idx_a; const art_aabb* rec_a; int da;
+  const int* idx_o; const art_obb* rec_o; int dob;
+  art_sphere* sph; art_aabb* aabb; art_obb* obb;
+  int ns, na;
+  SphereRec* osph; SphereCold* osphc; AabbRec* oaabb; AabbCold* oaabbc; ObbRec* oobb; ObbCold* oobbc; CullRec* cull;
+};
+// Scenes up to this many colliders sync and refit in one workgroup (launch_sync_refit).
+constexpr long long kSyncRefitMax = 1 << 16;
+// The scatter of a sync's dirty records and the refit of the bound scene's BVH in one launch
+// (sc: the bound scene with the store's records); false (nothing launched) for larger scenes or
+// scenes without a BVH.
+bool launch_sync_refit(const ScatterArgs& a, DevScene& sc, const SortBufs& sb, hipStream_t st);
 
 size_t sort_scene_temp_bytes(int n);
 // Spatially sorted copies, chunk bounds and the BVH (art_bvh.hip), built per upload.
