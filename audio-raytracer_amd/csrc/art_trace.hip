@@ -219,8 +219,11 @@ __device__ __forceinline__ bool node_entry_tab(const Seg& s, const NodeTab* tab,
 // entered lane counts them. No ballots: every value is a quad DPP reduction (measured 3 % faster in
 // the nearest traversal; the echo any-hit keeps its ballot form, index order, which measured 6 %
 // faster there than this near-first form).
+#ifndef ART_NEAREST_ONE_ANY
+#define ART_NEAREST_ONE_ANY 1
+#endif
 __device__ __forceinline__ void quad_descend(bool enter, float en, bool force, int qd, int c0, uint32_t* my, int& g,
-                                             int& sp) {
+                                             int& sp, int* bp = nullptr) {
   const uint32_t key = enter ? (((force ? 0u : (uint32_t)__float_as_int(en)) & ~3u) | (uint32_t)qd) : 0xffffffffu;
   const uint32_t k1 = (uint32_t)quad_perm<kQuadRot1>((int)key), k2 = (uint32_t)quad_perm<kQuadXor2>((int)key),
                  k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
@@ -235,6 +238,7 @@ __device__ __forceinline__ void quad_descend(bool enter, float en, bool force, i
     const int t = (int)my[sp > 0 ? sp - 1 : 0];
     g = sp > 0 ? t : -1;
     sp = sp > 0 ? sp - 1 : 0;
+    if (ART_NEAREST_ONE_ANY && bp != nullptr && sp == *bp) sp = *bp = 0;  // the entries below bp were taken
   }
 }
 
@@ -404,8 +408,8 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     }
     const float en = fmaxf(tn, 0.0f);
     const bool enter = force | (h & (en <= lim));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
-    quad_descend(enter, en, force, qd, c0, my, g, sp);
-    if (sp == bp) sp = bp = 0;
+    quad_descend(enter, en, force, qd, c0, my, g, sp, ART_NEAREST_ONE_ANY ? &bp : nullptr);
+    if (!ART_NEAREST_ONE_ANY && sp == bp) sp = bp = 0;  // (else quad_descend's pop keeps sp == bp => 0)
   };
   auto leaf_step = [&](int leaf) {
     ART_DIAG_STEP(nsteps);
@@ -480,7 +484,13 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     for (;;) {
       if (g >= leaf0 && pend < 0) { pend = g; pop(); }
       const bool inner = g >= 0 && g < leaf0;
+#if ART_NEAREST_ONE_ANY
+      // (after the park above, a quad with no parked leaf and a node holds an inner node, so "some
+      // quad has no parked leaf and work" implies "some quad is inner": one ballot decides)
+      if (!__any(pend < 0 && g >= 0)) break;
+#else
       if (!__any(inner) || !__any(pend < 0 && g >= 0)) break;
+#endif
       if (inner) inner_step();
     }
     if (pend >= 0) { leaf_step(pend); pend = -1; }
@@ -1463,12 +1473,17 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
 // only, not all targets' (config 2: echo_muffle traffic 12.9 -> 10.8 MB per frame with the 4-B
 // entries). The muffle blocks there fill the echo traversal's tails; in the standalone muffle_kernel
 // the uneven work per target left XCDs idle (config 5: 171 -> 193 us), so it keeps the plain order.
-// Any other shape keeps the plain (b % M, b / M) order.
+// Any other shape keeps the plain (b % M, b / M) order. Round 6 (ART_MUFFLE_XCD 2, the default
+// when the group count is a multiple of 8): each muffle wave runs on the XCD that traced its 64-ray
+// group's echoes (echo_muffle_kernel), so a group's nearest hits are read from that XCD's L2 and
+// each L2 holds every target's lists: echo+muffle config 4 594.5 -> 585.7 us, config 3 88.5 ->
+// 87.4, config 2 54.2 -> 53.6 (HBM bytes per launch at config 4 73.3 -> 75.1 MB: the time is not
+// set by the traffic).
 #ifndef ART_MUFFLE_XCD
-#define ART_MUFFLE_XCD 1
+#define ART_MUFFLE_XCD 2
 #endif
 __device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uint32_t& rb, int& t) {
-  if (ART_MUFFLE_XCD && 8 % mt == 0 && ((unsigned long long)M * mt) % 8 == 0) {
+  if (ART_MUFFLE_XCD >= 1 && 8 % mt == 0 && ((unsigned long long)M * mt) % 8 == 0) {
     const uint32_t x = b & 7u;
     t = (int)(x % (uint32_t)mt);
     rb = (b >> 3) * (8u / (uint32_t)mt) + x / (uint32_t)mt;
@@ -1522,6 +1537,16 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
     int w;
     split(b, groups, g, w);
     vis_quad_body<OBB, true>(sc, vp, count, EX ? ex : nullptr, g, w, s_stk, nullptr, -1, block, eh);
+    return;
+  }
+  if (ART_MUFFLE_XCD == 2 && groups % 8u == 0u) {
+    // group-local muffle waves (muffle_block's note): the wave of (64-ray group G, target t) runs on the XCD
+    // that traced G's echo rays (workgroup index % 8 == G % 8), so each XCD fetches only its own
+    // groups' nearest hits (from its L2) and every target's cell lists
+    const uint32_t m = b - ne, x = m & 7u, j = m >> 3;
+    const int t = (int)(j % (uint32_t)mt);
+    const uint32_t G = (j / (uint32_t)mt) * 8u + x;
+    muffle_body<EX, OBB, true>(sc, fp, vp, count, acc, eh, G * 64u + threadIdx.x, t, mt);
     return;
   }
   uint32_t mb, rb;
