@@ -770,7 +770,7 @@ def main():
         kernels[fam] = {"instantiation": fam_inst[fam], "ms_per_frame": k_ms, "launches_per_frame": n_l / n_each,
                         "ms_per_launch": keach["kernel_ms"][fam] / n_l, "ops_per_frame": fam_ops[fam],
                         "achieved": tf, "frac": tf / FP32_VALU_PEAK_TFLOPS,
-                        "traffic": next((v for k, v in traffic_by_kernel.items() if k.startswith(fam)), None)}
+                        "traffic": sum(v for k, v in traffic_by_kernel.items() if k.startswith(fam)) or None}
     dom = max(kernels, key=lambda k: kernels[k]["ms_per_frame"]) if kernels else "nearest_first_kernel"
     dk = kernels.get(dom, {"ms_per_frame": 0.0, "achieved": 0.0, "frac": 0.0, "traffic": None, "ops_per_frame": 0.0,
                            "launches_per_frame": 0.0, "instantiation": fam_inst[dom]})

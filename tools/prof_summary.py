@@ -88,9 +88,20 @@ def main():
         H = art.CONFIGS[cfg].H
         per_bounce = ("nearest_first_kernel", "path_kernel", "vis_kernel")
 
+        # round 6: bounce 0 of a frame may run the shared-origin instantiation of the nearest kernel
+        # (nearest_first_kernel<EX, OBB, FOLD, true>, once per frame), the other bounces the plain one
+        tab = any(k.startswith("nearest_first_kernel") and k.endswith(", true>") for k in stage)
+
+        def launches(k):
+            if k.startswith("nearest_first_kernel") and k.endswith(", true>"):
+                return 1
+            if k.startswith("nearest_first_kernel") and tab:
+                return H - 1
+            return H if k.startswith(per_bounce) else 1
+
         def per_frame(k, c):  # mean per dispatch x dispatches per frame
             v = per[k].get(c, [])
-            return sum(v) / len(v) * (H if k.startswith(per_bounce) else 1) if v else 0.0
+            return sum(v) / len(v) * launches(k) if v else 0.0
         fetch_kb = sum(per_frame(k, "FETCH_SIZE") for k in stage)
         write_kb = sum(per_frame(k, "WRITE_SIZE") for k in stage)
         per_kernel = {k: (2.0 * per_frame(k, "FETCH_SIZE") + per_frame(k, "WRITE_SIZE")) * 1024.0 for k in sorted(stage)}
@@ -103,7 +114,7 @@ def main():
             "raytrace_bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0,
             "bytes_per_frame_by_kernel": per_kernel,
             "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024; FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 note",
-            "launches_per_frame": {k: (H if k.startswith(per_bounce) else 1) for k in sorted(stage)},
+            "launches_per_frame": {k: launches(k) for k in sorted(stage)},
             "source": f"profiles/{tag}_pmc.csv (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --config {cfg})",
             "config": cfg,
             "lib_sha256": lib_sha,
