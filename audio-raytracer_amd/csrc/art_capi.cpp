@@ -134,7 +134,8 @@ struct Device {
   bool st_fresh = true;         // capacity (re)allocated: every record must be uploaded
   hipEvent_t st_done = nullptr; // recorded after the last sync's upload + decode (on st_stream)
   hipStream_t st_stream = nullptr;  // the stream the last sync ran on (dv.stream or a device-path launch stream)
-  bool st_pending = false;      // st_done recorded and the host staging may still be read
+  hipEvent_t st_epoch[2] = {nullptr, nullptr};  // after the last sync of an epoch of the update ring
+  bool st_epoch_pending[2] = {false, false};
   hipEvent_t launch_done = nullptr;  // after the last art_launch_device frame (caller's stream)
   bool launch_pending = false;       // work on dv.stream waits for it before reusing the scene / buffers
   hipStream_t launch_stream = nullptr;  // the caller's stream of that frame
@@ -208,7 +209,11 @@ struct art_ctx {
   std::vector<int16_t> synced_tid[3];
   std::vector<int> tid_hist[3];
   art_collider_sync_stats last_sync{};
-  HostBuf h_upd;
+  // pinned update images of art_colliders_sync, a ring (sync s uses slot s % kUpdRing): a slot is
+  // reused only after the previous epoch's syncs are done (one event per epoch, not per sync)
+  static constexpr int kUpdRing = 8;
+  HostBuf h_upd[kUpdRing];
+  uint64_t upd_seq = 0;
   // Host phases of the Unity-facing frame (ART_HOST_TIMES=1 in the environment at art_create:
   // steady_clock marks in art_schedule / art_complete, means printed by art_destroy to stderr).
   struct HostPhases {
@@ -1135,6 +1140,8 @@ ART_API void art_destroy(art_ctx* c) {
     dv.exec.release(); dv.pairs.release(); dv.dsp.release(); dv.cones.release();
     dv.st_raw.release(); dv.st_soa.release(); dv.st_upd.release();
     if (dv.st_done) (void)hipEventDestroy(dv.st_done);
+    for (hipEvent_t e : dv.st_epoch)
+      if (e) (void)hipEventDestroy(e);
     if (dv.launch_done) (void)hipEventDestroy(dv.launch_done);
     for (hipEvent_t e : dv.ev_pool) (void)hipEventDestroy(e);
     if (dv.done) (void)hipEventDestroy(dv.done);
@@ -1151,7 +1158,7 @@ ART_API void art_destroy(art_ctx* c) {
   c->h_in.release();
   c->h_block.release();
   c->h_dsp.release();
-  c->h_upd.release();
+  for (HostBuf& b : c->h_upd) b.release();
   delete c;
 }
 
@@ -1706,16 +1713,23 @@ ART_API int art_colliders_sync(art_ctx* c) {
       }
   }
   bool cells_rebuilt = false;
-  for (Device& dv : c->devs) {  // the previous sync's copy may still read the pinned staging
-    if (dv.st_pending) {
-      HIP_TRY(c, hipSetDevice(dv.id));
-      HIP_TRY(c, hipEventSynchronize(dv.st_done));
-      dv.st_pending = false;
-    }
-  }
+  // The update image goes to ring slot seq % kUpdRing. A new epoch reuses the ring: every sync of the
+  // previous epoch has finished reading its slot once that epoch's event (recorded after its last
+  // sync, on that sync's stream) has completed. Each sync's stream is ordered after the earlier
+  // syncs' (a launch on a new stream waits on the old one, a context-stream sync on the launch
+  // stream), so that one event covers the whole epoch.
+  const uint64_t seq = c->upd_seq++;
+  const int slot = (int)(seq % art_ctx::kUpdRing), ep = (int)((seq / art_ctx::kUpdRing) & 1u);
+  if (slot == 0)
+    for (Device& dv : c->devs)
+      if (dv.st_epoch_pending[ep ^ 1]) {
+        HIP_TRY(c, hipSetDevice(dv.id));
+        HIP_TRY(c, hipEventSynchronize(dv.st_epoch[ep ^ 1]));
+        dv.st_epoch_pending[ep ^ 1] = false;
+      }
   if (c->cpu) bytes = 0;  // the CPU backend keeps no device copy (it snapshots the lists below)
-  if (bytes && !c->h_upd.reserve(bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
-  uint8_t* h = static_cast<uint8_t*>(c->h_upd.p);
+  if (bytes && !c->h_upd[slot].reserve(bytes)) return fail(c, ART_E_NOMEM, "pinned allocation failed");
+  uint8_t* h = static_cast<uint8_t*>(c->h_upd[slot].p);
   for (int k = 0; bytes && k < 3; ++k) {
     const auto& K = c->kinds[k];
     const size_t rs = kRecSize[k];
@@ -1782,12 +1796,13 @@ ART_API int art_colliders_sync(art_ctx* c) {
       launch_prep(sph, n[0], aabb, n[1], obb, n[2], osph, osphc, oaabb, oaabbc, oobb, oobbc, cull, ss);
       HIP_TRY(c, hipGetLastError());
     }
-    // stream-ordered: frames on ss follow; device-path launches on other streams wait on st_done (and
-    // work on dv.stream, after a sync on the launch stream, waits through wait_launch). One record
-    // per sync: a refit below records it after its kernels (each record costs the queue ~5 us).
+    // stream-ordered: frames on ss follow. A sync on the context stream records st_done, which
+    // device-path launches on other streams wait on (a refit below records it after its kernels). A
+    // sync on the launch stream records nothing (each record costs the queue ~5 us): a launch on
+    // another stream waits on that stream's launch_done, work on dv.stream on it through wait_launch.
     if (!dv.st_done) HIP_TRY(c, hipEventCreateWithFlags(&dv.st_done, hipEventDisableTiming));
-    if (!refit_follows) HIP_TRY(c, hipEventRecord(dv.st_done, ss));
-    dv.st_pending = true;
+    const bool lazy = ss != dv.stream;
+    if (!refit_follows && !lazy) HIP_TRY(c, hipEventRecord(dv.st_done, ss));
     DevScene& t = dv.st_sc;
     t.sph = osph; t.sphc = osphc; t.ns = n[0];
     t.aabb = oaabb; t.aabbc = oaabbc; t.na = n[1];
@@ -1828,9 +1843,14 @@ ART_API int art_colliders_sync(art_ctx* c) {
             cells_rebuilt = true;
           }
           if (dv.sorted_gen != ~0ull) dv.sorted_gen = c->sync_gen;
-          HIP_TRY(c, hipEventRecord(dv.st_done, ss));  // device-path launches wait for the sort too
+          if (!lazy) HIP_TRY(c, hipEventRecord(dv.st_done, ss));  // device-path launches wait for the sort too
         }
       }
+    }
+    if (slot == art_ctx::kUpdRing - 1) {  // the epoch's last sync: the event that frees the ring
+      if (!dv.st_epoch[ep]) HIP_TRY(c, hipEventCreateWithFlags(&dv.st_epoch[ep], hipEventDisableTiming));
+      HIP_TRY(c, hipEventRecord(dv.st_epoch[ep], ss));
+      dv.st_epoch_pending[ep] = true;
     }
   }
   if (c->fr.resident) { c->fr.ns = n[0]; c->fr.na = n[1]; c->fr.no = n[2]; }

@@ -1136,7 +1136,11 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       const CullRec r = load_node(br, c0 + qd);
       float tn;
       const bool h = node_entry(s, r, om, tn);
+#ifdef ART_ECHO_CAP_MEAS  // (measurement builds only, wrong outputs: segments traversed only up to this distance)
+      const bool enter = force | (h & (tn <= fminf(maxd, ART_ECHO_CAP_MEAS)));
+#else
       const bool enter = force | (h & (tn <= maxd));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
+#endif
       const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);

@@ -52,6 +52,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=0, help="timed steps (0 = enough for about 1.5 s)")
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--prewarm-s", type=float, default=0.3,
+                   help="untimed frames (launches only, no collective) for this many seconds before the W warmup "
+                        "steps: the GPU clock of a fresh process ramps over its first few hundred frames, which a "
+                        "game's continuous frame loop never sees (0 = off)")
     p.add_argument("--config", type=int, default=None, help="BASELINE config (default: 2; 1 for --path cpu)")
     p.add_argument("--frames", type=int, default=50, help="host-API frames for the p50 frame latency")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -640,6 +644,12 @@ def main():
             art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
 
     torch.cuda.synchronize()
+    prewarm_frames, tp = 0, time.perf_counter()
+    while time.perf_counter() - tp < a.prewarm_s:  # (untimed: the clock ramp of a fresh process)
+        for _ in range(32):
+            ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
+        prewarm_frames += 32
+        torch.cuda.synchronize()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -792,6 +802,9 @@ def main():
         "n_gpus": world,
         "steps": steps,
         "warmup": a.warmup,
+        "prewarm": {"seconds": a.prewarm_s, "frames": prewarm_frames,
+                    "note": "untimed frames before the warmup steps (GPU clock ramp of a fresh process); the timed "
+                            "region holds exactly `steps` frames"},
         "ms_per_step": dt / steps * 1e3,
         "p50_frame_ms": statistics.median(frame_ms) if frame_ms else None,
         "p50_frame_ms_note": "art_schedule..art_complete on rank 0, host arrays, H2D + kernels + D2H (PCIe-inclusive)",
