@@ -68,6 +68,9 @@ def parse():
                    help="N > 1: weak = cfg.S fans per rank; strong = cfg.S fans split over the ranks "
                         "(auto: strong for config 4, as BASELINE.json names it, weak otherwise)")
     p.add_argument("--no-dynamic", action="store_true", help="skip the dynamic-scene and rebuild measurements")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="N > 1 over RCCL: run each frame's all-gather after it on the launch stream instead of "
+                        "beside the next frame's kernels")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo: host-side all-gather, "
                         "e.g. ranks sharing one GPU in tests)")
@@ -530,7 +533,7 @@ def main_cpu(a):
         "threads_n": res["n"], "threads_1": res["one"], "host": host}))
 
 
-def verify_allgather(ctx, dist, backend, world, rank, org_all, S_total, d_org, S, d_blk, stride, dev, sp):
+def verify_allgather(ctx, dist, backend, world, rank, org_all, S_total, d_org, S, d_blk, stride, dev, sp, timed_full=None):
     """N > 1, outside the timed region: the process group has the expected size, every rank sits on
     its own device under RCCL (ranks may share one only over gloo, the CPU tests' setup), and the
     all-gathered result blocks equal, byte for byte, rank 0's own launch of a sample of every rank's
@@ -563,6 +566,9 @@ def verify_allgather(ctx, dist, backend, world, rank, org_all, S_total, d_org, S
         torch.cuda.synchronize()
         got = torch.stack([full[i * stride:(i + 1) * stride] for i in sample])
         ok = bool(torch.equal(got.reshape(-1), d_ref))
+        if timed_full is not None:  # the last timed frame's gather (overlapped with the next frame's kernels)
+            got_t = torch.stack([timed_full[i * stride:(i + 1) * stride] for i in sample])
+            ok = ok and bool(torch.equal(got_t.reshape(-1), d_ref))
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
     tdist.broadcast(flag, 0)
     if not flag.item():
@@ -638,10 +644,34 @@ def main():
     tests_rank = sum(counts.values())
     bf_ops = sum(counts[k] * OPS[k] for k in ("rt_sphere", "rt_aabb", "rt_obb"))
 
+    # N > 1 over RCCL with even shards: frame i's all-gather runs on the collective's stream beside
+    # frame i + 1's kernels. Two result blocks alternate; before frame i + 2 rewrites block i % 2 the
+    # launch stream waits for gather i (Work.wait: a stream wait, the host does not block).
+    overlap = world > 1 and a.dist_backend == "nccl" and not a.no_overlap and S * world == S_total
+    stride = lay["stride"]
+    if overlap:
+        import collections
+        d_blks = [d_blk, torch.zeros_like(d_blk)]
+        g_outs = [torch.empty(S_total * stride, dtype=torch.uint8, device=dev) for _ in range(2)]
+        pend = collections.deque()
+        n_step = [0]
+
     def step():
+        if overlap:
+            b = d_blks[n_step[0] & 1]
+            if len(pend) == 2:
+                pend.popleft().wait()
+            ctx.launch_device(d_org.data_ptr(), S, b.data_ptr(), 0, sp)
+            pend.append(dist.all_gather_into_tensor(g_outs[n_step[0] & 1], b[: S * stride], async_op=True))
+            n_step[0] += 1
+            return
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
         if world > 1:
-            art.dist.all_gather_fan_blocks(d_blk[: S * lay["stride"]], S_total, lay["stride"], world)
+            art.dist.all_gather_fan_blocks(d_blk[: S * stride], S_total, stride, world)
+
+    def drain():  # the pending all-gathers (their output is then ready on the launch stream)
+        while overlap and pend:
+            pend.popleft().wait()
 
     torch.cuda.synchronize()
     prewarm_frames, tp = 0, time.perf_counter()
@@ -652,12 +682,14 @@ def main():
         torch.cuda.synchronize()
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     steps = a.steps
     if steps <= 0:  # about 1.5 s of timed work, so the driver's sampler sees the GPU busy
         tp = time.perf_counter()  # per-step time from 10 steps after the warmup (first-call costs excluded)
         for _ in range(10):
             step()
+        drain()
         torch.cuda.synchronize()
         per = (time.perf_counter() - tp) / 10
         steps = int(min(5000, max(20, 1.5 / max(per, 1e-6))))
@@ -669,14 +701,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    n_step0 = n_step[0] if overlap else 0
     for _ in range(steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    verify = verify_allgather(ctx, dist, a.dist_backend, world, rank, org_all, S_total, d_org, S, d_blk, lay["stride"], dev,
-                              sp) if world > 1 else None
+    # (overlapped gathers: the timed region's last gathered blocks are checked too)
+    last_full = g_outs[(n_step0 + steps - 1) & 1] if overlap else None
+    verify = verify_allgather(ctx, dist, a.dist_backend, world, rank, org_all, S_total, d_org, S, d_blk, stride, dev,
+                              sp, last_full) if world > 1 else None
+    if verify is not None:
+        verify["overlapped_allgather"] = overlap
 
     # Kernel durations: untimed passes of the same launches after the timed region, HIP events on
     # the streams the kernels run on. Pass 1: the frame's stages only (raytrace stage, permeation
@@ -823,8 +861,10 @@ def main():
         "allgather_verified": verify["verified"] if verify else None,
         "allgather_verify": verify,
         "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
-        "allgather_note": f"HIP events on the launch stream around the all-gather of {n_pass} untimed frames after the "
-                          "timed region, max over ranks; the step time includes it" if world > 1 else None,
+        "allgather_note": (f"HIP events on the launch stream around the all-gather of {n_pass} untimed frames after the "
+                           "timed region, max over ranks; " + ("in the timed steps each frame's all-gather runs beside the "
+                           "next frame's kernels (RCCL stream, two result blocks alternating); every gather is inside "
+                           "the timed region" if overlap else "the step time includes it")) if world > 1 else None,
         "roofline": {"bound": "valu", "kernel": dk["instantiation"],
                      "achieved": dk["achieved"], "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": dk["frac"], "traffic": dk["traffic"],
