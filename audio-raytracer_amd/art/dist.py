@@ -38,3 +38,38 @@ def all_gather_fan_blocks(local_block, S: int, stride: int, world: int, group=No
         b, e = shard_range(S, world, r)
         parts.append(full[r * per * stride: (r * per + (e - b)) * stride])
     return torch.cat(parts)
+
+
+class OverlappedGather:
+    """Frames whose all-gather runs beside the next frame's kernels (one process per GPU, RCCL).
+
+    step(): launch(block) writes this frame's result block, then gather(out, block) is issued
+    asynchronously (torch.distributed ..., async_op=True: the collective's stream waits for the
+    launch stream, the launch stream goes on). Two blocks alternate; before frame i + 2 rewrites
+    block i % 2, wait() on gather i makes the launch stream wait for it. drain() waits for every
+    pending gather; last() is the output of the most recent one.
+
+    launch(block) enqueues the frame into `block`; gather(out, block) returns a Work-like object
+    with wait()."""
+
+    def __init__(self, blocks, outs, launch, gather):
+        import collections
+        assert len(blocks) == 2 and len(outs) == 2
+        self.blocks, self.outs, self.launch, self.gather = blocks, outs, launch, gather
+        self.pend = collections.deque()
+        self.n = 0
+
+    def step(self):
+        i = self.n & 1
+        if len(self.pend) == 2:
+            self.pend.popleft().wait()  # gather n - 2 read blocks[i]
+        self.launch(self.blocks[i])
+        self.pend.append(self.gather(self.outs[i], self.blocks[i]))
+        self.n += 1
+
+    def drain(self):
+        while self.pend:
+            self.pend.popleft().wait()
+
+    def last(self):
+        return self.outs[(self.n - 1) & 1] if self.n else None

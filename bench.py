@@ -649,29 +649,24 @@ def main():
     # launch stream waits for gather i (Work.wait: a stream wait, the host does not block).
     overlap = world > 1 and a.dist_backend == "nccl" and not a.no_overlap and S * world == S_total
     stride = lay["stride"]
+    og = None
     if overlap:
-        import collections
-        d_blks = [d_blk, torch.zeros_like(d_blk)]
-        g_outs = [torch.empty(S_total * stride, dtype=torch.uint8, device=dev) for _ in range(2)]
-        pend = collections.deque()
-        n_step = [0]
+        og = art.dist.OverlappedGather(
+            [d_blk, torch.zeros_like(d_blk)], [torch.empty(S_total * stride, dtype=torch.uint8, device=dev) for _ in range(2)],
+            lambda b: ctx.launch_device(d_org.data_ptr(), S, b.data_ptr(), 0, sp),
+            lambda out, b: dist.all_gather_into_tensor(out, b[: S * stride], async_op=True))
 
     def step():
-        if overlap:
-            b = d_blks[n_step[0] & 1]
-            if len(pend) == 2:
-                pend.popleft().wait()
-            ctx.launch_device(d_org.data_ptr(), S, b.data_ptr(), 0, sp)
-            pend.append(dist.all_gather_into_tensor(g_outs[n_step[0] & 1], b[: S * stride], async_op=True))
-            n_step[0] += 1
+        if og is not None:
+            og.step()
             return
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
         if world > 1:
             art.dist.all_gather_fan_blocks(d_blk[: S * stride], S_total, stride, world)
 
     def drain():  # the pending all-gathers (their output is then ready on the launch stream)
-        while overlap and pend:
-            pend.popleft().wait()
+        if og is not None:
+            og.drain()
 
     torch.cuda.synchronize()
     prewarm_frames, tp = 0, time.perf_counter()
@@ -701,7 +696,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_step0 = n_step[0] if overlap else 0
     for _ in range(steps):
         step()
     drain()
@@ -710,7 +704,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     # (overlapped gathers: the timed region's last gathered blocks are checked too)
-    last_full = g_outs[(n_step0 + steps - 1) & 1] if overlap else None
+    last_full = og.last() if og is not None else None
     verify = verify_allgather(ctx, dist, a.dist_backend, world, rank, org_all, S_total, d_org, S, d_blk, stride, dev,
                               sp, last_full) if world > 1 else None
     if verify is not None:

@@ -88,3 +88,98 @@ def test_pack_unpack_roundtrip():
     lay = art.fan_layout(fr, art.abi.ART_OUT_HIT_RESULTS)
     back = art.unpack_block(art.pack_block(out, lay), lay, 3, 64, cfg.H, cfg.T, 1, hits=True, dsp=True)
     assert all(back.equal(out).values())
+
+
+class _FakeWork:
+    def __init__(self, log, i):
+        self.log, self.i = log, i
+
+    def wait(self):
+        self.log.append(("wait", self.i))
+
+
+def test_overlapped_gather_order():
+    """art.dist.OverlappedGather (bench.py's N > 1 frames over RCCL): frame i writes block i % 2 and
+    its gather is issued right after; a block is rewritten only after the gather that read it two
+    frames earlier has been waited for; drain() waits for the rest; last() is the newest output."""
+    log = []
+    blocks, outs = ["b0", "b1"], ["o0", "o1"]
+    n = [0]
+
+    def launch(b):
+        log.append(("launch", b))
+
+    def gather(o, b):
+        log.append(("gather", o, b))
+        n[0] += 1
+        return _FakeWork(log, n[0] - 1)
+
+    og = art.dist.OverlappedGather(blocks, outs, launch, gather)
+    for _ in range(5):
+        og.step()
+    assert og.last() == "o0"
+    og.drain()
+    assert log == [("launch", "b0"), ("gather", "o0", "b0"),
+                   ("launch", "b1"), ("gather", "o1", "b1"),
+                   ("wait", 0), ("launch", "b0"), ("gather", "o0", "b0"),
+                   ("wait", 1), ("launch", "b1"), ("gather", "o1", "b1"),
+                   ("wait", 2), ("launch", "b0"), ("gather", "o0", "b0"),
+                   ("wait", 3), ("wait", 4)]
+
+
+def _overlap_worker(rank, world, port, S, frames, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "audio-raytracer_amd"))
+    import art as A
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = A.CONFIGS[2]
+        scene, org, params = A.synth(cfg, S=S * world, R=64, C_scale=0.05)
+        b, e = A.dist.shard_range(S * world, world, rank)
+        out = A.FanOutputs(e - b, 64, cfg.H, cfg.T, 1)
+        fr = A.Frame(scene, params, np.ascontiguousarray(org[b:e]), out)
+        lay = A.fan_layout(fr)
+        stride = lay["stride"]
+        blocks = [torch.zeros(S * stride, dtype=torch.uint8) for _ in range(2)]
+        outs = [torch.empty(world * S * stride, dtype=torch.uint8) for _ in range(2)]
+        with A.Context(0) as cpu:  # libart's CPU backend writes each frame into the block
+
+            def launch(blk):
+                cpu.run(fr)
+                blk.copy_(torch.from_numpy(A.pack_block(out, lay)))
+
+            og = A.dist.OverlappedGather(blocks, outs, launch,
+                                         lambda o, blk: dist.all_gather_into_tensor(o, blk, async_op=True))
+            for _ in range(frames):
+                og.step()
+            og.drain()
+        if rank == 0:
+            q.put(og.last().numpy().tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_gather_gloo_equals_single_process():
+    """The same helper over a real gloo group (world 2, async all_gather_into_tensor, 3 frames):
+    the last gathered blocks equal one process's frame over all fans, byte for byte."""
+    world, S = 2, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, S, 3, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cfg = art.CONFIGS[2]
+    scene, org, params = art.synth(cfg, S=S * world, R=64, C_scale=0.05)
+    out = art.FanOutputs(S * world, 64, cfg.H, cfg.T, 1)
+    fr = art.Frame(scene, params, org, out)
+    with art.Context(0) as cpu:
+        cpu.run(fr)
+    assert got == art.pack_block(out, art.fan_layout(fr)).tobytes()
