@@ -329,9 +329,10 @@ template <bool EX, bool OBB>
 constexpr int kNearestWaves = EX ? 6 : (OBB ? ART_NEAREST_OBB_WAVES : 8);
 template <bool EX, bool OBB>
 constexpr int kEchoWaves = EX ? 6 : (OBB ? 7 : 8);
-// echo_muffle_kernel<false, true>: 8 waves per SIMD (64 VGPRs) without spills
+// echo_muffle_kernel<false, true>: 7 waves per SIMD (72 VGPRs: the muffle rays' prefetching list
+// walks, muffle_blocked) without spills (round 6; 8 waves before them)
 #ifndef ART_ECHO_MUFFLE_OBB_WAVES
-#define ART_ECHO_MUFFLE_OBB_WAVES 8
+#define ART_ECHO_MUFFLE_OBB_WAVES 7
 #endif
 // Work sharing's pairing: the quad base lane (l4) of the donor whose rank among the donors equals
 // this thief's rank ir. Two cross-lane moves instead of a select-bit search: lane 0 of each robbed
@@ -1324,6 +1325,9 @@ __device__ bool muffle_brute(const DevScene& sc, const Seg& s, float maxd, int t
 // bound, stopping at the first entry past the segment; a segment longer than the lists' cell_far,
 // a degenerate one or a dropped target tests every collider in reference order. nt / ne / nfb
 // count exact tests, list entries and fallback rays (EX).
+#ifndef ART_MUFFLE_PREFETCH
+#define ART_MUFFLE_PREFETCH 2  // (0: the round-6 walks, each list's entries fetched step by step; 1: OBB scenes prefetch the sphere list only; for A/B runs)
+#endif
 template <bool EX, bool OBB>
 __device__ __forceinline__ bool muffle_blocked(const DevScene& sc, vec3 off, vec3 tp, float maxd, int t, unsigned* nt,
                                                unsigned& ne, unsigned& nfb) {
@@ -1353,6 +1357,75 @@ __device__ __forceinline__ bool muffle_blocked(const DevScene& sc, vec3 off, vec
         idx = v.x & 0x0fffffffu; key = near_key(v.y); nearf = __uint_as_float(v.y);
       }
     };
+#if ART_MUFFLE_PREFETCH
+    if (sc.cell_compact) {  // (wave-uniform; 8-B entries take the step-by-step walks below)
+    // Software-pipelined walks over the 4-B entries: the first entries of all three lists are
+    // fetched together as soon as the cell's starts arrive, and each step fetches the next step's
+    // entries beside its records, so a walk costs one dependent fetch per step instead of two and
+    // the AABB and OBB walks start without an entry fetch of their own. An entry past its list's
+    // end reads as 0xffffffff (key 0xffff, beyond every segment) without a fetch.
+    auto fetch = [&](uint32_t k, uint32_t e) { return k < e ? sc.cell_ent32[k] : 0xffffffffu; };
+    auto nearf_of = [](uint32_t v) { return __uint_as_float(v & 0xffff0000u); };
+    // (ART_MUFFLE_PREFETCH 1: with OBBs in the scene the AABB list's first entries are fetched when
+    // its walk starts and the OBB walk fetches entry by entry, which needs fewer live registers.
+    // Measured: keeping the cell's bounds and first entries in one 48-B head per cell, fetched at
+    // once, gained nothing further: the entries are already fetched beside one another)
+    constexpr bool kAll = ART_MUFFLE_PREFETCH >= 2 || !OBB;
+    const uint32_t s0 = fetch(se.x, se.y), s1 = fetch(se.x + 1, se.y);
+    uint32_t a0 = 0u, a1 = 0u, o0 = 0xffffffffu;
+    if (kAll) { a0 = fetch(se.y, se.z); a1 = fetch(se.y + 1, se.z); }
+    if (kAll && OBB) o0 = fetch(se.z, se.w);
+    auto walk2 = [&](uint32_t b, uint32_t e, uint32_t c0, uint32_t c1, auto load, auto test) {
+      for (uint32_t k = b; k < e; k += 2) {  // c0, c1 = entries k, k + 1
+        if ((c0 >> 16) > klim) break;        // this and every later entry lie beyond the segment
+        const bool use1 = (c1 >> 16) <= klim;
+        const auto r0 = load(c0 & 0xffffu);
+        const auto r1 = load((use1 ? c1 : c0) & 0xffffu);
+        const uint32_t n0 = fetch(k + 2, e), n1 = fetch(k + 3, e);  // (beside the records)
+        if (EX) ne += use1 ? 2u : 1u;
+        if (!(nearf_of(c0) > lim) && test(r0)) { blocked = true; break; }
+        if (!use1) break;
+        if (!(nearf_of(c1) > lim) && test(r1)) { blocked = true; break; }
+        c0 = n0; c1 = n1;
+      }
+    };
+    walk2(se.x, se.y, s0, s1,
+          [&](uint32_t idx) {
+            const float4 a = *reinterpret_cast<const float4*>(sc.sph + idx);
+            SphereRec r;
+            r.cx = a.x; r.cy = a.y; r.cz = a.z; r.r2 = a.w;
+            return r;
+          },
+          [&](const SphereRec& r) {
+            ++nt[0];
+            float d;
+            return sphere_hit_dist(s, r, d) && d < maxd;
+          });
+    if (!kAll && !blocked) { a0 = fetch(se.y, se.z); a1 = fetch(se.y + 1, se.z); }
+    if (!blocked)
+      walk2(se.y, se.z, a0, a1, [&](uint32_t idx) { return sc.aabb[idx]; },
+            [&](const AabbRec& r) {
+              ++nt[1];
+              float d;
+              return aabb_test<false>(s, r, d) && d < maxd;
+            });
+    if (OBB && !blocked) {  // OBB records (64 B) one at a time (kAll: the next entry fetched beside each test)
+      uint32_t c = o0;
+      for (uint32_t k = se.z; k < se.w; ++k) {
+        if (!kAll) c = sc.cell_ent32[k];
+        if ((c >> 16) > klim) break;
+        if (EX) ++ne;
+        const uint32_t n = kAll ? fetch(k + 1, se.w) : 0u;
+        if (!(nearf_of(c) > lim)) {
+          ++nt[2];
+          float d;
+          if (obb_test_staged(s, sc.obb + (c & 0xffffu), d) && d < maxd) { blocked = true; break; }
+        }
+        c = n;
+      }
+    }
+    } else {
+#endif
     auto walk = [&](uint32_t b, uint32_t e, auto load, auto test, auto pair) {
       uint32_t i0, k0, i1, k1;
       float n0, n1;
@@ -1407,6 +1480,9 @@ __device__ __forceinline__ bool muffle_blocked(const DevScene& sc, vec3 off, vec
              return obb_test_staged(s, r, d) && d < maxd;
            },
            std::false_type{});
+#if ART_MUFFLE_PREFETCH
+    }
+#endif
   } else {
     if (EX) ++nfb;
     blocked = muffle_brute<OBB>(sc, s, maxd, t, nt);
@@ -1436,8 +1512,10 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
     valid = valid && hit_from_pre(sc, eh, i >> 6, (int)(i & 63u), slot_ok, fan, ray, O, o, off, type, idx);
     dbase = (uint32_t)fan * (uint32_t)fp.T;
   } else {
-    if (vp.fixed) valid = valid && vp.out[i].y != kNoRecord;  // (compact records: fold_path)
-    const float4 r = vp.hrec[valid ? i : 0u];
+    // (compact records: fold_path; the hit record is fetched beside the marker, not after it: a
+    // slot without a record holds a stale one, never used)
+    const float4 r = vp.hrec[i < n ? i : 0u];
+    if (vp.fixed) valid = valid && vp.out[i].y != kNoRecord;
     off = mk3(r.x, r.y, r.z);
     dbase = __float_as_uint(r.w);
     valid = valid && dbase != kNoRecord;
@@ -1499,7 +1577,10 @@ __device__ __forceinline__ void muffle_block(uint32_t b, uint32_t M, int mt, uin
 
 // 8 waves per SIMD; the counting OBB instantiations at 7, where they need no spills
 template <bool EX, bool OBB, bool HM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EX && OBB ? 7 : 8))) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
+#ifndef ART_MUFFLE_OBB_WAVES
+#define ART_MUFFLE_OBB_WAVES 7  // (the prefetching walks need 72 VGPRs with OBB tests)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EX && OBB ? 5 : (OBB ? ART_MUFFLE_OBB_WAVES : (EX ? 7 : 8))))) void muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp,
                                                      const uint32_t* __restrict__ count, uint32_t* __restrict__ acc,
                                                      EchoFromHits eh) {
   muffle_body<EX, OBB, HM>(sc, fp, vp, count, acc, eh, blockIdx.x * 256u + threadIdx.x, (int)blockIdx.y, (int)gridDim.y);
