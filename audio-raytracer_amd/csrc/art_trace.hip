@@ -303,6 +303,9 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
 #ifndef ART_VIS_STEAL
 #define ART_VIS_STEAL 1
 #endif
+#ifndef ART_ECHO_PARK
+#define ART_ECHO_PARK 1  // (0: echo_muffle_kernel's echo traversal tests a leaf as soon as its quad reaches it, for A/B runs)
+#endif
 #ifndef ART_NEAREST_STEAL
 #define ART_NEAREST_STEAL 1
 #endif
@@ -1074,7 +1077,7 @@ __device__ __forceinline__ bool echo_seg_from_hit(const DevScene& sc, const Echo
 // owner = the target). `valid` must be quad-uniform; an invalid segment is reported visible.
 // Work sharing as in the nearest traversal (a blocker of a shared segment ends every traversal of
 // it); nt / nnode accumulate the exact tests and node visits (EX counters).
-template <bool OBB>
+template <bool OBB, bool PARK = false>
 __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float maxd, int owner, bool valid, int lane,
                                                uint32_t* s_wave, unsigned* nt, unsigned& nnode) {
   const int qd = lane & 3, wq = lane >> 2;
@@ -1099,8 +1102,15 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
     sp = has ? sp - 1 : sp;
     if (sp == bp) sp = bp = 0;
   };
+  // PARK: the speculative while-while of the nearest traversal (a quad that reaches a leaf parks it
+  // and keeps descending; the wave tests leaves once every quad with work holds one), so a quad
+  // that found its leaf early does not idle while the others descend. Any-hit needs every entered
+  // leaf tested anyway, so the order changes nothing but the lanes' occupancy. Measured (round 6):
+  // the echo half of echo_muffle_kernel config 2 53.0 -> 50.9 us, config 4 495 -> 490 us; the
+  // folded frames' vis_kernel (config 5) 440 -> 444 us, so vis_kernel keeps the plain loop.
+  int pend = -1;
   for (;;) {
-    const unsigned long long act = __ballot(g >= 0) & kQuad0;
+    const unsigned long long act = __ballot(g >= 0 || (PARK && pend >= 0)) & kQuad0;
     if (!act) break;
     const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
     if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
@@ -1108,7 +1118,7 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       asm volatile("" : "+v"(l4));  // (recomputed here, not hoisted out of the loop)
       const unsigned long long below = (1ull << l4) - 1ull;
       const int ir = __popcll(idle & below), dr = __popcll(donors & below);
-      const bool thief = g < 0 && ir < __popcll(donors);
+      const bool thief = (act >> l4 & 1ull) == 0ull && ir < __popcll(donors);
       const bool robbed = g >= 0 && sp > bp && dr < __popcll(idle);
       const int match = rank_match(l4, qd, robbed, dr, ir);  // (every lane takes part)
       const int src = (thief ? match : l4) + qd;
@@ -1130,7 +1140,15 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       }
       if (robbed && ++bp == sp) sp = bp = 0;
     }
-    while (g >= 0 && g < leaf0) {  // quad-uniform
+    for (;;) {  // quad-uniform steps
+      if (PARK) {
+        if (g >= leaf0 && pend < 0) { pend = g; pop(); }
+        // (after the park, a quad with no parked leaf and a node holds an inner node)
+        if (!__any(pend < 0 && g >= 0)) break;
+        if (!(g >= 0 && g < leaf0)) continue;
+      } else if (!(g >= 0 && g < leaf0)) {
+        break;
+      }
       const int c0 = 4 * g + 1;
       if (qd == 0) ++nnode;
       ART_DIAG_STEP(nsteps);
@@ -1154,15 +1172,17 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       }
     }
     bool hit_quad = false;
-    if (g >= leaf0) {
+    const int leaf = PARK ? pend : g;
+    if (leaf >= leaf0) {
       ART_DIAG_STEP(nsteps);
       int cc, tid;
       float d;
-      const bool hh = leaf_slot_test<OBB>(s, br, (g - leaf0) * kBvhLeaf + qd, cc, d, tid, nt);
+      const bool hh = leaf_slot_test<OBB>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, d, tid, nt);
       const bool blk_here = hh && d < maxd && tid != owner;  // :373-394, :411-447
       hit_quad = ((uint32_t)(__ballot(blk_here) >> qshift) & 0xFu) != 0u;
-      if (!hit_quad) pop();
+      if (!PARK && !hit_quad) pop();
     }
+    pend = -1;
     for (unsigned long long bq = __ballot(hit_quad) & kQuad0; bq; bq &= bq - 1ull)
       wblocked |= 1u << __builtin_amdgcn_readlane(home, __builtin_ctzll(bq));
     if ((wblocked >> home) & 1u) { g = -1; sp = bp = 0; }  // the segment is decided: every quad on it stops
@@ -1233,7 +1253,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     }
   }
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
-  const bool visible = quad_echo_core<OBB>(sc, s, maxd, owner, valid, lane, s_wave, nt, nnode);
+  const bool visible = quad_echo_core<OBB, HM && ART_ECHO_PARK>(sc, s, maxd, owner, valid, lane, s_wave, nt, nnode);
   if (HM) {
     if (valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = visible ? out_val : (uint16_t)0;  // :76, :142-144
   } else if (vp.fixed) {
