@@ -394,6 +394,9 @@ __global__ __launch_bounds__(kPermBlock) void perm_count_kernel(DevScene sc, Fra
 // slots, uploaded with the origins, in place of the block's (which then stay unwritten and are not
 // copied back). host_out (host-API frames): the fan's whole result record is also stored into the
 // pinned host staging (the frame's D2H copy, done by the kernel that finishes the frame).
+#ifndef ART_REDUCE_PACK
+#define ART_REDUCE_PACK 1
+#endif
 __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp, FanLayout L, uint8_t* __restrict__ block,
                                                     const uint32_t* __restrict__ muffle_acc,
                                                     const uint8_t* __restrict__ muffle_reset, const float* __restrict__ perm_in,
@@ -411,11 +414,13 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
 
   const uint16_t* echo = reinterpret_cast<const uint16_t*>(fb + L.echo_off);
   const int n = fp.R * fp.H;
-  // The echo sum (:42-47) must add in index order. Zeros only count as returned, but adding a
-  // zero leaves the running sum unchanged (it starts at +0 and a round-to-nearest sum of non-zero
-  // terms is never -0), so every element is added: the wave converts a chunk to floats in LDS
-  // (coalesced loads, parallel conversion) and lane 0 accumulates it from 16-B LDS reads, with
-  // no cross-lane step per element.
+  // The echo sum (:42-47) must add in index order. Zeros only count as returned, and adding a zero
+  // leaves the running sum unchanged (it starts at +0 and a round-to-nearest sum of non-zero terms
+  // is never -0), so only the non-zero terms are added: the wave converts a chunk to floats and
+  // packs its non-zero ones, in index order, into LDS (coalesced loads, parallel conversion, one
+  // ballot per 64 elements), and lane 0 accumulates them from 16-B LDS reads, with no cross-lane
+  // step per element. (Round 6: every element was added; the serial chain is now as long as the
+  // frame's visible echoes.)
   constexpr int kChunkF = 4096;
   __shared__ float4 s_f4[kChunkF / 4];
   float* s_f = reinterpret_cast<float*>(s_f4);
@@ -423,6 +428,7 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
   uint32_t zeros = 0;
   for (int base = 0; base < n; base += kChunkF) {
     const int m = min(kChunkF, n - base);
+    int packed = 0;  // wave-uniform: non-zero terms of this chunk so far
     for (int i0 = 0; i0 < m; i0 += 8 * 64) {  // 8 independent loads per lane in flight
       uint16_t h[8];
 #pragma unroll
@@ -435,12 +441,20 @@ __global__ __launch_bounds__(64) void reduce_kernel(DevScene sc, FrameParams fp,
         const int i = i0 + 64 * j + lane;
         const bool in = i < m;
         const float e = f16tof32(h[j]);
-        if (in) s_f[i] = e;
+        if (ART_REDUCE_PACK) {
+          const unsigned long long nz = __ballot(in && e != 0.0f);  // (NaN included)
+          if (in && e != 0.0f) s_f[packed + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u))] = e;
+          packed += __popcll(nz);
+        } else {
+          if (in) s_f[i] = e;
+        }
         zeros += __popcll(__ballot(in && e == 0.0f));
       }
     }
     __syncthreads();
+    const int mm = ART_REDUCE_PACK ? packed : m;
     if (lane == 0) {  // 8 LDS reads in flight ahead of the 32 dependent adds they feed
+      const int m = mm;
       int i = 0;
       for (; i + 32 <= m; i += 32) {
         float4 v[8];
