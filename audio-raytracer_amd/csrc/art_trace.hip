@@ -224,12 +224,13 @@ __device__ __forceinline__ bool node_entry_tab(const Seg& s, const NodeTab* tab,
 #endif
 __device__ __forceinline__ void quad_descend(bool enter, float en, bool force, int qd, int c0, uint32_t* my, int& g,
                                              int& sp, int* bp = nullptr) {
-  const uint32_t key = enter ? (((force ? 0u : (uint32_t)__float_as_int(en)) & ~3u) | (uint32_t)qd) : 0xffffffffu;
+  const uint32_t key = enter ? (((uint32_t)__float_as_int(en) & (force ? 0u : ~3u)) | (uint32_t)qd) : 0xffffffffu;
   const uint32_t k1 = (uint32_t)quad_perm<kQuadRot1>((int)key), k2 = (uint32_t)quad_perm<kQuadXor2>((int)key),
                  k3 = (uint32_t)quad_perm<kQuadRot3>((int)key);
   const int rank = (int)(k1 < key) + (int)(k2 < key) + (int)(k3 < key);
   const uint32_t kmin = min(min(key, k1), min(k2, k3));
-  const int nent = __popc((uint32_t)(__ballot(enter) >> (__lane_id() & ~3)) & 0xFu);  // entered children (one ballot)
+  // entered children (one ballot of the key itself: an entered key is at most 0x7f800003, en >= 0)
+  const int nent = __popc((uint32_t)(__builtin_amdgcn_ballot_w64(key != 0xffffffffu) >> (__lane_id() & ~3)) & 0xFu);
   if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
   if (nent) {
     g = c0 + (int)(kmin & 3u);
@@ -379,6 +380,9 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   unsigned nt[3] = {0u, 0u, 0u}, nnode = 0;
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
   bool force = force_all(s, om);
+  // the forced lanes as a lane mask (wave-uniform, kept in SGPRs): a node test ORs it in with scalar
+  // instructions (__builtin_amdgcn_inverse_ballot_w64) instead of a per-lane 0/1 value
+  unsigned long long fmk = __builtin_amdgcn_ballot_w64(force);
   const int leaf0 = sc.bvh_leaf0;
   const BvhRes br = bvh_res(sc);
   int g = alive ? 0 : -1, sp = 0, bp = 0, home = wq;
@@ -411,7 +415,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
       h = node_entry(s, r, om, tn);
     }
     const float en = fmaxf(tn, 0.0f);
-    const bool enter = force | (h & (en <= lim));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
+    const bool enter = __builtin_amdgcn_inverse_ballot_w64(fmk) | (h & (en <= lim));  // (empty nodes: art_bvh.hip cull_stored)
     quad_descend(enter, en, force, qd, c0, my, g, sp, ART_NEAREST_ONE_ANY ? &bp : nullptr);
     if (!ART_NEAREST_ONE_ANY && sp == bp) sp = bp = 0;  // (else quad_descend's pop keeps sp == bp => 0)
   };
@@ -436,7 +440,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   // run with most quads busy. The order in which leaves are tested does not change the minimum.
   int pend = -1;
   for (;;) {
-    const unsigned long long act = __ballot(g >= 0 || pend >= 0) & kQuad0;
+    const unsigned long long act = __builtin_amdgcn_ballot_w64(g >= 0 || pend >= 0) & kQuad0;
     if (!act) break;
     {  // Wave priority by unfinished rays: the waves with the most rays left (the ones that set the
        // kernel's length) issue first, the nearly finished ones fill the gaps (s_setprio, 0..3)
@@ -447,7 +451,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
       else __builtin_amdgcn_s_setprio(0);
     }
     if (ART_NEAREST_STEAL) {
-      const unsigned long long donors = __ballot(sp > bp) & kQuad0, idle = ~act & kQuad0;
+      const unsigned long long donors = __builtin_amdgcn_ballot_w64(sp > bp) & kQuad0, idle = ~act & kQuad0;
       if (donors && __popcll(idle) >= ART_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
         if (!shared) {       // publish every ray's bound once
           shared = true;
@@ -481,6 +485,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
           lim = dlim;
           mykey = ~0ull;  // (the finished ray's result went to its key above)
         }
+        fmk = __builtin_amdgcn_ballot_w64(force);
         if (robbed && ++bp == sp) sp = bp = 0;
       }
       if (shared) lim = fminf(lim, __int_as_float(s_bound[home]));
@@ -491,7 +496,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
 #if ART_NEAREST_ONE_ANY
       // (after the park above, a quad with no parked leaf and a node holds an inner node, so "some
       // quad has no parked leaf and work" implies "some quad is inner": one ballot decides)
-      if (!__any(pend < 0 && g >= 0)) break;
+      if (__builtin_amdgcn_ballot_w64((pend & ~g) < 0) == 0ull) break;  // pend < 0 && g >= 0, one compare
 #else
       if (!__any(inner) || !__any(pend < 0 && g >= 0)) break;
 #endif
@@ -741,7 +746,7 @@ __global__ __launch_bounds__(TAB ? 1024 : 256) __attribute__((amdgpu_waves_per_e
     out = (uint32_t)g * 64u + (uint32_t)rr;
   }
   if (EX && step < kExecBounces)  // live rays traced this bounce (one per quad)
-    exec_add(ex, kExecBounce0 + step, (unsigned long long)__popcll(__ballot(alive) & kQuad0));
+    exec_add(ex, kExecBounce0 + step, (unsigned long long)__popcll(__builtin_amdgcn_ballot_w64(alive) & kQuad0));
 #ifdef ART_DIAG
   const unsigned long long t0 = clock64();
 #endif
@@ -773,7 +778,7 @@ __global__ __launch_bounds__(TAB ? 1024 : 256) __attribute__((amdgpu_waves_per_e
         alive = slot_ok && ((__float_as_int(b.w) >> 8) & 1) != 0;
       }
     }
-    if (EX) exec_add(fp.exec, kExecEchoPairs, (unsigned long long)__popcll(__ballot(alive && code != kNoHit) & kQuad0));
+    if (EX) exec_add(fp.exec, kExecEchoPairs, (unsigned long long)__popcll(__builtin_amdgcn_ballot_w64(alive && code != kNoHit) & kQuad0));
     fold_path(sc, fp, L, block, origins, vp, state, step, out, fan, ray, slot_ok, o, d, life, nhits, alive, best, code,
               (lane & 3) == 0);
     return;
@@ -930,7 +935,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
     const vec3 off = o - d * kEps;                 // :124, :158
     const float dist0 = distance(O, o);            // :130 (un-offset hit point)
     {
-      const unsigned long long me = __ballot(live_slot), mr = __ballot(hit);
+      const unsigned long long me = __builtin_amdgcn_ballot_w64(live_slot), mr = __builtin_amdgcn_ballot_w64(hit);
       exec_add(fp.exec, kExecEchoPairs, (unsigned long long)__popcll(me));
       uint32_t eb, rb;
       reserve(emit_echo ? (uint32_t)__popcll(me) : 0u, (uint32_t)__popcll(mr), pair_count, eb, rb);
@@ -970,7 +975,7 @@ __global__ __launch_bounds__(64 * kPathWaves) __attribute__((amdgpu_waves_per_eu
       uint32_t* live = live_list(state, ngroups);
       uint32_t* live_n = live + (size_t)ngroups * 64;
       const bool app = valid && alive && step + 1 < fp.H;
-      const unsigned long long m = __ballot(app);
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(app);
       const int par = agg_round++ & 1;
       if (lane == 0) s_live[par][w] = (uint32_t)__popcll(m);
       __syncthreads();
@@ -1084,6 +1089,7 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
   if (sc.bvh_levels == 0) return true;                         // no colliders: nothing blocks
   float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z) + maxd;
   bool force = force_all(s, om);
+  unsigned long long fmk = __builtin_amdgcn_ballot_w64(force);  // (the forced lanes as a lane mask, as in the nearest core)
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
   const BvhRes br = bvh_res(sc);
   uint32_t* const my = s_wave + wq * kBvhStack;                // entries [bp, sp) pending
@@ -1110,9 +1116,9 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
   // folded frames' vis_kernel (config 5) 440 -> 444 us, so vis_kernel keeps the plain loop.
   int pend = -1;
   for (;;) {
-    const unsigned long long act = __ballot(g >= 0 || (PARK && pend >= 0)) & kQuad0;
+    const unsigned long long act = __builtin_amdgcn_ballot_w64(g >= 0 || (PARK && pend >= 0)) & kQuad0;
     if (!act) break;
-    const unsigned long long donors = __ballot(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
+    const unsigned long long donors = __builtin_amdgcn_ballot_w64(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
     if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
       int l4 = lane & ~3;
       asm volatile("" : "+v"(l4));  // (recomputed here, not hoisted out of the loop)
@@ -1138,13 +1144,14 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
         om = dom;
         force = dforce != 0;
       }
+      fmk = __builtin_amdgcn_ballot_w64(force);
       if (robbed && ++bp == sp) sp = bp = 0;
     }
     for (;;) {  // quad-uniform steps
       if (PARK) {
         if (g >= leaf0 && pend < 0) { pend = g; pop(); }
         // (after the park, a quad with no parked leaf and a node holds an inner node)
-        if (!__any(pend < 0 && g >= 0)) break;
+        if (__builtin_amdgcn_ballot_w64((pend & ~g) < 0) == 0ull) break;  // pend < 0 && g >= 0, one compare
         if (!(g >= 0 && g < leaf0)) continue;
       } else if (!(g >= 0 && g < leaf0)) {
         break;
@@ -1158,9 +1165,9 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
 #ifdef ART_ECHO_CAP_MEAS  // (measurement builds only, wrong outputs: segments traversed only up to this distance)
       const bool enter = force | (h & (tn <= fminf(maxd, ART_ECHO_CAP_MEAS)));
 #else
-      const bool enter = force | (h & (tn <= maxd));  // bitwise: no branch (empty nodes: art_bvh.hip cull_stored)
+      const bool enter = __builtin_amdgcn_inverse_ballot_w64(fmk) | (h & (tn <= maxd));  // (empty nodes: art_bvh.hip cull_stored)
 #endif
-      const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
+      const uint32_t eb = (uint32_t)(__builtin_amdgcn_ballot_w64(enter) >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);
         const uint32_t rest = eb & (eb - 1u);
@@ -1179,11 +1186,11 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       float d;
       const bool hh = leaf_slot_test<OBB>(s, br, (leaf - leaf0) * kBvhLeaf + qd, cc, d, tid, nt);
       const bool blk_here = hh && d < maxd && tid != owner;  // :373-394, :411-447
-      hit_quad = ((uint32_t)(__ballot(blk_here) >> qshift) & 0xFu) != 0u;
+      hit_quad = ((uint32_t)(__builtin_amdgcn_ballot_w64(blk_here) >> qshift) & 0xFu) != 0u;
       if (!PARK && !hit_quad) pop();
     }
     pend = -1;
-    for (unsigned long long bq = __ballot(hit_quad) & kQuad0; bq; bq &= bq - 1ull)
+    for (unsigned long long bq = __builtin_amdgcn_ballot_w64(hit_quad) & kQuad0; bq; bq &= bq - 1ull)
       wblocked |= 1u << __builtin_amdgcn_readlane(home, __builtin_ctzll(bq));
     if ((wblocked >> home) & 1u) { g = -1; sp = bp = 0; }  // the segment is decided: every quad on it stops
   }
@@ -1214,7 +1221,7 @@ __device__ __forceinline__ void vis_quad_body(const DevScene& sc, const VisPairs
     valid = echo_seg_from_hit(sc, eh, blk, slot, s, maxd, out_at, out_val, slot_ok);
     if (eh.no_path) {  // the path kernel's duties for this frame: a miss keeps the reset 0 (:76, :200-207)
       if (slot_ok && !valid && qd == 0) reinterpret_cast<uint16_t*>(block)[out_at] = 0;
-      if (ex) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__ballot(valid) & kQuad0));
+      if (ex) exec_add(ex, kExecEchoPairs, (unsigned long long)__popcll(__builtin_amdgcn_ballot_w64(valid) & kQuad0));
     }
     if (!__any(valid)) return;
   } else {
@@ -1550,11 +1557,11 @@ __device__ __forceinline__ void muffle_body(const DevScene& sc, const FrameParam
       blocked = muffle_blocked<EX, OBB>(sc, off, tp, maxd, t, nt, ne, nfb);
     }
     const bool vis = act && !blocked;                                 // :171
-    unsigned long long mv = __ballot(vis);
+    unsigned long long mv = __builtin_amdgcn_ballot_w64(vis);
     const uint32_t dest = dbase + (uint32_t)t;
     while (mv) {
       const uint32_t d0 = __builtin_amdgcn_readlane(dest, __builtin_ctzll(mv));
-      const unsigned long long eq = __ballot(vis && dest == d0);
+      const unsigned long long eq = __builtin_amdgcn_ballot_w64(vis && dest == d0);
       if (lane == 0) atomicAdd(&acc[d0], (uint32_t)__popcll(eq));
       mv &= ~eq;
     }
@@ -1713,7 +1720,7 @@ __device__ float loss_sum_wave(const DevScene& sc, const Seg& s, int t) {
   float sum = 0.0f;
   for (int base = 0; base < ctot; base += 64) {
     const float term = base + lane < ctot ? loss_term_global(sc, s, base + lane, t) : 0.0f;
-    for (unsigned long long m = __ballot(term != 0.0f); m; m &= m - 1ull)
+    for (unsigned long long m = __builtin_amdgcn_ballot_w64(term != 0.0f); m; m &= m - 1ull)
       sum += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, term), __builtin_ctzll(m)));
   }
   return sum;
@@ -1776,7 +1783,7 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
     int c;
     quad_nearest_core<false, OBB, true>(sc, make_seg(O, load_dir(sc.dirs, alive ? ray : br.x)), alive, lane, my, s_bound,
                                         s_key, best, c, nullptr);
-    const unsigned long long hq = __ballot(qd == 0 && alive && c != kNoHit);
+    const unsigned long long hq = __builtin_amdgcn_ballot_w64(qd == 0 && alive && c != kNoHit);
     if (hq) {  // the lowest such quad holds the highest ray index
       const int src = __builtin_ctzll(hq);
       found = r0 - (src >> 2);
@@ -1818,7 +1825,7 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
         float tn;
         const bool h = node_entry(s, r, om, tn);
         const bool enter = force | (h & (tn < INFINITY));  // (an empty node's entry is +inf: cull_stored)
-        const uint32_t eb = (uint32_t)(__ballot(enter) >> qshift) & 0xFu;
+        const uint32_t eb = (uint32_t)(__builtin_amdgcn_ballot_w64(enter) >> qshift) & 0xFu;
         if (eb) {
           const int first = __builtin_ctz(eb);
           const uint32_t rest = eb & (eb - 1u);
@@ -1832,7 +1839,7 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
       if (g >= leaf0) {
         int cc;
         const float term = leaf_loss_term<OBB>(sc, s, bres, (g - leaf0) * kBvhLeaf + qd, t, cc);
-        const uint32_t nz = (uint32_t)(__ballot(term != 0.0f) >> qshift) & 0xFu;
+        const uint32_t nz = (uint32_t)(__builtin_amdgcn_ballot_w64(term != 0.0f) >> qshift) & 0xFu;
         const int at = n + __popc(nz & ((1u << qd) - 1u));
         if (term != 0.0f && at < kLossCap) { s_code[wq][at] = (uint32_t)cc; s_term[wq][at] = term; }
         n += __popc(nz);
@@ -1861,7 +1868,7 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
       for (int i = 0; i < n; ++i) sum += s_sorted[wq][i];
       if (qd == 0) ppr[slot * T + t] = (float)fp.R * fp.perm_strength - sum;  // :260
     }
-    for (unsigned long long ov = __ballot(qd == 0 && valid && !fits); ov; ov &= ov - 1ull) {  // (wave-uniform)
+    for (unsigned long long ov = __builtin_amdgcn_ballot_w64(qd == 0 && valid && !fits); ov; ov &= ov - 1ull) {  // (wave-uniform)
       const int src = __builtin_ctzll(ov), tt = t0 + (src >> 2);
       const Seg so = make_seg(off, normalize(load3(sc.targets, tt) - off));
       const float sum = loss_sum_wave(sc, so, tt);
