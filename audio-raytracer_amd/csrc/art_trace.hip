@@ -231,10 +231,11 @@ __device__ __forceinline__ void quad_descend(bool enter, float en, bool force, i
   const uint32_t kmin = min(min(key, k1), min(k2, k3));
   // entered children (one ballot of the key itself: an entered key is at most 0x7f800003, en >= 0)
   const int nent = __popc((uint32_t)(__builtin_amdgcn_ballot_w64(key != 0xffffffffu) >> (__lane_id() & ~3)) & 0xFu);
-  if (enter && rank > 0) my[sp + nent - 1 - rank] = (uint32_t)(c0 + qd);
+  const int spn = sp + nent - 1;  // the stack pointer after the push (one add shared by both uses)
+  if (enter && rank > 0) my[spn - rank] = (uint32_t)(c0 + qd);
   if (nent) {
     g = c0 + (int)(kmin & 3u);
-    sp += nent - 1;
+    sp = spn;
   } else {  // branch-free pop: the stack slot is read unconditionally (clamped), -1 when empty
     const int t = (int)my[sp > 0 ? sp - 1 : 0];
     g = sp > 0 ? t : -1;
@@ -440,7 +441,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
   // run with most quads busy. The order in which leaves are tested does not change the minimum.
   int pend = -1;
   for (;;) {
-    const unsigned long long act = __builtin_amdgcn_ballot_w64(g >= 0 || pend >= 0) & kQuad0;
+    const unsigned long long act = __builtin_amdgcn_ballot_w64((g & pend) >= 0) & kQuad0;  // g >= 0 || pend >= 0
     if (!act) break;
     {  // Wave priority by unfinished rays: the waves with the most rays left (the ones that set the
        // kernel's length) issue first, the nearly finished ones fill the gaps (s_setprio, 0..3)
@@ -1116,7 +1117,7 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
   // folded frames' vis_kernel (config 5) 440 -> 444 us, so vis_kernel keeps the plain loop.
   int pend = -1;
   for (;;) {
-    const unsigned long long act = __builtin_amdgcn_ballot_w64(g >= 0 || (PARK && pend >= 0)) & kQuad0;
+    const unsigned long long act = __builtin_amdgcn_ballot_w64((g & (PARK ? pend : -1)) >= 0) & kQuad0;  // g >= 0 || (PARK && pend >= 0)
     if (!act) break;
     const unsigned long long donors = __builtin_amdgcn_ballot_w64(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
     if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
@@ -1164,10 +1165,14 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
       const bool h = node_entry(s, r, om, tn);
 #ifdef ART_ECHO_CAP_MEAS  // (measurement builds only, wrong outputs: segments traversed only up to this distance)
       const bool enter = force | (h & (tn <= fminf(maxd, ART_ECHO_CAP_MEAS)));
+      const unsigned long long em = __builtin_amdgcn_ballot_w64(enter);
 #else
-      const bool enter = __builtin_amdgcn_inverse_ballot_w64(fmk) | (h & (tn <= maxd));  // (empty nodes: art_bvh.hip cull_stored)
+      // the entered lanes as a mask of scalar ANDs / ORs of single-compare ballots (a ballot of the
+      // combined flag would round-trip it through a 0/1 VGPR); empty nodes: art_bvh.hip cull_stored
+      const unsigned long long em = fmk | (__builtin_amdgcn_ballot_w64(h) & __builtin_amdgcn_ballot_w64(tn <= maxd));
+      const bool enter = __builtin_amdgcn_inverse_ballot_w64(em);
 #endif
-      const uint32_t eb = (uint32_t)(__builtin_amdgcn_ballot_w64(enter) >> qshift) & 0xFu;
+      const uint32_t eb = (uint32_t)(em >> qshift) & 0xFu;
       if (eb) {
         const int first = __builtin_ctz(eb);
         const uint32_t rest = eb & (eb - 1u);
