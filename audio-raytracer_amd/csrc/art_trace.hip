@@ -298,6 +298,12 @@ __device__ __forceinline__ bool leaf_slot_test(const Seg& s, const BvhRes& br, i
   return hit;
 }
 
+// Population count of a 64-bit lane mask as two 32-bit counts: an int result that compares with
+// 32-bit scalar / vector compares (a 64-bit count compares with VALU 64-bit compares).
+__device__ __forceinline__ int pop64(unsigned long long x) {
+  return __builtin_popcount((uint32_t)x) + __builtin_popcount((uint32_t)(x >> 32));
+}
+
 // Work sharing inside a wave (nearest and echo traversals): a wave lasts as long as its longest
 // traversal, so a quad whose traversal has ended takes over the bottom entry of a busy quad's
 // stack (the largest pending subtree) together with that quad's ray, and traverses it for the
@@ -445,7 +451,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     if (!act) break;
     {  // Wave priority by unfinished rays: the waves with the most rays left (the ones that set the
        // kernel's length) issue first, the nearly finished ones fill the gaps (s_setprio, 0..3)
-      const int na = __popcll(act);
+      const int na = pop64(act);
       if (na > 12) __builtin_amdgcn_s_setprio(3);
       else if (na > 8) __builtin_amdgcn_s_setprio(2);
       else if (na > 4) __builtin_amdgcn_s_setprio(1);
@@ -453,7 +459,7 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
     }
     if (ART_NEAREST_STEAL) {
       const unsigned long long donors = __builtin_amdgcn_ballot_w64(sp > bp) & kQuad0, idle = ~act & kQuad0;
-      if (donors && __popcll(idle) >= ART_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
+      if (donors && pop64(idle) >= ART_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
         if (!shared) {       // publish every ray's bound once
           shared = true;
           if (qd == 0) s_bound[wq] = __float_as_int(lim);
@@ -462,9 +468,9 @@ __device__ __forceinline__ void quad_nearest_core(const DevScene& sc, Seg s, boo
         int l4 = lane & ~3;
         asm volatile("" : "+v"(l4));
         const unsigned long long below = (1ull << l4) - 1ull;
-        const int ir = __popcll(idle & below), dr = __popcll(donors & below);
-        const bool thief = (act >> l4 & 1ull) == 0ull && ir < __popcll(donors);
-        const bool robbed = sp > bp && dr < __popcll(idle);
+        const int ir = pop64(idle & below), dr = pop64(donors & below);
+        const bool thief = (act >> l4 & 1ull) == 0ull && ir < pop64(donors);
+        const bool robbed = sp > bp && dr < pop64(idle);
         const int match = rank_match(l4, qd, robbed, dr, ir);  // (every lane takes part)
         const int src = (thief ? match : l4) + qd;
         const int dbp = __shfl(bp, src), dhome = __shfl(home, src);
@@ -1120,13 +1126,13 @@ __device__ __forceinline__ bool quad_echo_core(const DevScene& sc, Seg s, float 
     const unsigned long long act = __builtin_amdgcn_ballot_w64((g & (PARK ? pend : -1)) >= 0) & kQuad0;  // g >= 0 || (PARK && pend >= 0)
     if (!act) break;
     const unsigned long long donors = __builtin_amdgcn_ballot_w64(g >= 0 && sp > bp) & kQuad0, idle = ~act & kQuad0;
-    if (ART_VIS_STEAL && donors && __popcll(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
+    if (ART_VIS_STEAL && donors && pop64(idle) >= ART_VIS_STEAL_MIN_IDLE) {  // wave-uniform: the k-th idle quad takes the k-th donor's stack bottom
       int l4 = lane & ~3;
       asm volatile("" : "+v"(l4));  // (recomputed here, not hoisted out of the loop)
       const unsigned long long below = (1ull << l4) - 1ull;
-      const int ir = __popcll(idle & below), dr = __popcll(donors & below);
-      const bool thief = (act >> l4 & 1ull) == 0ull && ir < __popcll(donors);
-      const bool robbed = g >= 0 && sp > bp && dr < __popcll(idle);
+      const int ir = pop64(idle & below), dr = pop64(donors & below);
+      const bool thief = (act >> l4 & 1ull) == 0ull && ir < pop64(donors);
+      const bool robbed = g >= 0 && sp > bp && dr < pop64(idle);
       const int match = rank_match(l4, qd, robbed, dr, ir);  // (every lane takes part)
       const int src = (thief ? match : l4) + qd;
       const int dbp = __shfl(bp, src), dhome = __shfl(home, src), downer = __shfl(owner, src);
