@@ -71,6 +71,14 @@ def parse():
     p.add_argument("--no-overlap", action="store_true",
                    help="N > 1 over RCCL: run each frame's all-gather after it on the launch stream instead of "
                         "beside the next frame's kernels")
+    p.add_argument("--overlap", choices=("auto", "on"), default="auto",
+                   help="N > 1 over RCCL with even shards: auto = time the overlapped and the serial all-gather "
+                        "before the timed region and run the faster; on = always overlap (--no-overlap: never)")
+    p.add_argument("--nccl-priority", choices=("normal", "high"), default="normal",
+                   help="N > 1 over RCCL: priority of the collective's stream")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the N > 1 code path (process group, all-gathers, overlap, self-check) even with one "
+                        "rank: a one-GPU rehearsal of the RCCL branch; launch under torch.distributed.run")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo: host-side all-gather, "
                         "e.g. ranks sharing one GPU in tests)")
@@ -600,12 +608,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # --force-dist: the N > 1 code path (process group, all-gathers, overlap, self-check) at any N,
+    # so a one-GPU box can run the RCCL branch with one rank (a rehearsal of the driver's N > 1 runs)
+    dist_on = world > 1 or a.force_dist
+    if dist_on:
         import torch.distributed as dist
         gpu = local % max(1, torch.cuda.device_count())  # ranks may share a GPU (gloo tests)
         torch.cuda.set_device(gpu)
         if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            # --nccl-priority high puts the collective's stream at high priority (measured with one rank:
+            # the overlapped form 0.1106 -> 0.1124 ms per step, so the default stays normal)
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = a.nccl_priority == "high"
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), pg_options=opts)
         else:
             dist.init_process_group("gloo")
     else:
@@ -647,21 +662,23 @@ def main():
     # N > 1 over RCCL with even shards: frame i's all-gather runs on the collective's stream beside
     # frame i + 1's kernels. Two result blocks alternate; before frame i + 2 rewrites block i % 2 the
     # launch stream waits for gather i (Work.wait: a stream wait, the host does not block).
-    overlap = world > 1 and a.dist_backend == "nccl" and not a.no_overlap and S * world == S_total
+    overlap = dist_on and a.dist_backend == "nccl" and not a.no_overlap and S * world == S_total
     stride = lay["stride"]
     og = None
-    if overlap:
+    if overlap:  # (--overlap auto: kept only if it measures faster than the serial form, below)
         og = art.dist.OverlappedGather(
             [d_blk, torch.zeros_like(d_blk)], [torch.empty(S_total * stride, dtype=torch.uint8, device=dev) for _ in range(2)],
             lambda b: ctx.launch_device(d_org.data_ptr(), S, b.data_ptr(), 0, sp),
             lambda out, b: dist.all_gather_into_tensor(out, b[: S * stride], async_op=True))
 
+    mode = {"og": og is not None}
+
     def step():
-        if og is not None:
+        if mode["og"]:
             og.step()
             return
         ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
-        if world > 1:
+        if dist_on:
             art.dist.all_gather_fan_blocks(d_blk[: S * stride], S_total, stride, world)
 
     def drain():  # the pending all-gathers (their output is then ready on the launch stream)
@@ -679,6 +696,32 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
+    # --overlap auto (RCCL, even shards): the overlapped and the serial all-gather are each timed over
+    # untimed frames (twice, alternating; max over ranks) and the faster form runs the timed region.
+    # Measured on one GPU with one rank (--force-dist), the overlap's cross-stream waits cost ~13 us per
+    # frame against ~0.4 us for a serial one-rank gather; across GPUs the serial gather carries the
+    # xGMI transfer, so which form wins depends on N and is measured, not assumed.
+    overlap_tune = None
+    if og is not None and a.overlap == "auto":
+        def trial(use):
+            mode["og"] = use
+            dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(48):
+                step()
+            drain()
+            torch.cuda.synchronize()
+            return float(allreduce(time.perf_counter() - t, torch.float64, dist.ReduceOp.MAX)) / 48 * 1e3
+        ser = [trial(False), None]
+        ovl = [trial(True), None]
+        ser[1], ovl[1] = trial(False), trial(True)
+        mode["og"] = min(ovl) < min(ser)
+        overlap_tune = {"serial_ms_per_step": min(ser), "overlapped_ms_per_step": min(ovl),
+                        "chosen": "overlapped" if mode["og"] else "serial",
+                        "note": "untimed trials of 48 frames each (twice, alternating, max over ranks) before the "
+                                "timed region; the faster all-gather form runs the timed steps"}
+    overlap = mode["og"]
     steps = a.steps
     if steps <= 0:  # about 1.5 s of timed work, so the driver's sampler sees the GPU busy
         tp = time.perf_counter()  # per-step time from 10 steps after the warmup (first-call costs excluded)
@@ -688,11 +731,11 @@ def main():
         torch.cuda.synchronize()
         per = (time.perf_counter() - tp) / 10
         steps = int(min(5000, max(20, 1.5 / max(per, 1e-6))))
-        if world > 1:
+        if dist_on:
             steps = int(allreduce(steps, torch.int64, dist.ReduceOp.MAX))
     # The timed region: K frames and nothing else between them (no event records, each of which
     # costs a few us of GPU idle: kernel durations are measured in the passes after it).
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -700,15 +743,17 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
     # (overlapped gathers: the timed region's last gathered blocks are checked too)
-    last_full = og.last() if og is not None else None
+    last_full = og.last() if mode["og"] else None
     verify = verify_allgather(ctx, dist, a.dist_backend, world, rank, org_all, S_total, d_org, S, d_blk, stride, dev,
-                              sp, last_full) if world > 1 else None
+                              sp, last_full) if dist_on else None
     if verify is not None:
         verify["overlapped_allgather"] = overlap
+        if overlap_tune is not None:
+            verify["overlap_tune"] = overlap_tune
 
     # Kernel durations: untimed passes of the same launches after the timed region, HIP events on
     # the streams the kernels run on. Pass 1: the frame's stages only (raytrace stage, permeation
@@ -729,7 +774,7 @@ def main():
         raise RuntimeError(f"per-kernel timing dropped {keach['kernel_marks_dropped']} launch marks")
     # the all-gather alone: HIP events on the launch stream around the collective of n_pass frames
     allgather_ms = None
-    if world > 1:
+    if dist_on:
         evs = []
         for _ in range(n_pass):
             ctx.launch_device(d_org.data_ptr(), S, d_blk.data_ptr(), 0, sp)
@@ -748,7 +793,7 @@ def main():
     torch.cuda.synchronize()
     executed = ctx.executed_counts()
     ctx.set_flags(0)
-    if world > 1:
+    if dist_on:
         dt = float(allreduce(dt, torch.float64, dist.ReduceOp.MAX))
         tests_all = float(allreduce(tests_rank, torch.float64))
     else:
@@ -772,7 +817,7 @@ def main():
         dyn = dynamic_step(cfg, scene, params, org, S, steps, a.warmup, sp)
 
     if rank != 0:
-        if world > 1:
+        if dist_on:
             dist.destroy_process_group()
         return
 
@@ -850,15 +895,15 @@ def main():
                    "rays": cfg.R, "colliders": cfg.C, "targets": cfg.T, "max_hits_per_ray": cfg.H,
                    "reference_tests_per_frame_rank0": tests_rank, "reference_tests_per_frame_all": tests_all,
                    "parallelism": f"fan-sharded x{world}" + (f" + all-gather ({'RCCL' if a.dist_backend == 'nccl' else 'gloo'})"
-                                                              if world > 1 else "")},
+                                                              if dist_on else "")},
         "allgather_ms": allgather_ms,
         "allgather_verified": verify["verified"] if verify else None,
         "allgather_verify": verify,
-        "allgather_bytes": (S_total * lay["stride"]) if world > 1 else None,
+        "allgather_bytes": (S_total * lay["stride"]) if dist_on else None,
         "allgather_note": (f"HIP events on the launch stream around the all-gather of {n_pass} untimed frames after the "
                            "timed region, max over ranks; " + ("in the timed steps each frame's all-gather runs beside the "
                            "next frame's kernels (RCCL stream, two result blocks alternating); every gather is inside "
-                           "the timed region" if overlap else "the step time includes it")) if world > 1 else None,
+                           "the timed region" if overlap else "the step time includes it")) if dist_on else None,
         "roofline": {"bound": "valu", "kernel": dk["instantiation"],
                      "achieved": dk["achieved"], "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": dk["frac"], "traffic": dk["traffic"],
@@ -912,7 +957,7 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(res))
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
