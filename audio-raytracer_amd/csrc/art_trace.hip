@@ -1698,6 +1698,12 @@ void echo_muffle_kernel(DevScene sc, FrameParams fp, VisPairs vp, const uint32_t
 // ray meeting more than kLossCap colliders is summed by the whole wave over every collider instead.
 // ------------------------------------------------------------------------------------------
 constexpr int kLossCap = 48;  // kept (code, term) entries per loss ray
+#ifndef ART_PERM_LAST1
+#define ART_PERM_LAST1 1  // (0: the first-hit search casts 16 rays from the first iteration on, for A/B runs)
+#endif
+#ifndef ART_PERM_SPLIT
+#define ART_PERM_SPLIT 1  // (0: one quad per loss ray, for A/B runs)
+#endif
 
 // Loss term of global collider g (Sphere, AABB, OBB ranges) for segment s and target t (0 when t
 // owns it), the reference expressions (:225-328).
@@ -1787,7 +1793,22 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
   // 1. the highest-index ray of [br.x, br.y) with a permeation first hit (ShootRayCast :58)
   int found = -1, code = kNoHit;
   float dist = 0.0f;
-  for (int r0 = br.y - 1; r0 >= br.x && found < 0; r0 -= 16) {  // (wave-uniform)
+  int rtop = br.y - 1;  // the highest ray not yet cast
+  if (ART_PERM_LAST1) {  // the batch's last ray alone first (it usually hits): quad 0 casts it and the
+                         // wave's 15 idle quads share its traversal (the work sharing of quad_nearest_core)
+    float best;
+    int c;
+    quad_nearest_core<false, OBB, true>(sc, make_seg(O, load_dir(sc.dirs, rtop)), wq == 0, lane, my, s_bound, s_key, best,
+                                        c, nullptr);
+    const int c0 = __builtin_amdgcn_readlane(c, 0);
+    if (c0 != kNoHit) {
+      found = rtop;
+      code = c0;
+      dist = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, best), 0));
+    }
+    --rtop;
+  }
+  for (int r0 = rtop; r0 >= br.x && found < 0; r0 -= 16) {  // (wave-uniform)
     const int ray = r0 - wq;
     const bool alive = ray >= br.x;
     float best;
@@ -1819,12 +1840,20 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
   const vec3 o = O + d * dist;  // :61
   const vec3 off = o - d * kEps;
 
-  // 2. the T loss rays (:67-85), one per quad
+  // 2. the T loss rays (:67-85). P quads per ray (ART_PERM_SPLIT; P = 16 / rays in the chunk, at
+  // most 4, with an inner root): quad j of a ray traverses the root's children c with c % P == j, so
+  // the ray's subtrees run side by side instead of leaving 16 - T quads idle (config 4: the job's
+  // waves hold wave slots beside the nearest traversal for their whole length). The subtrees are
+  // disjoint, so the ray's kept terms are its quads' lists together, ranked by order code across
+  // them and summed serially in reference order as before.
   const BvhRes bres = bvh_res(sc);
   const int leaf0 = sc.bvh_leaf0, qshift = lane & ~3;
-  for (int t0 = 0; t0 < T; t0 += 16) {  // (wave-uniform)
-    const int t = t0 + wq;
-    const bool valid = t < T;
+  for (int t0 = 0; t0 < T;) {  // (wave-uniform)
+    const int P = (ART_PERM_SPLIT && leaf0 > 0) ? min(4, 16 / min(16, T - t0)) : 1;  // quads per ray
+    const int nr = min(T - t0, 16 / P);                                              // rays in this chunk
+    const int rq = wq / P, j = wq - rq * P, wq0 = rq * P;                            // ray, part, its first quad
+    const int t = t0 + rq;
+    const bool valid = rq < nr;
     const Seg s = make_seg(off, normalize(load3(sc.targets, valid ? t : 0) - off));
     const float om = fabsf(s.o.x) + fabsf(s.o.y) + fabsf(s.o.z);
     const bool force = force_all(s, om);
@@ -1835,7 +1864,8 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
         const CullRec r = load_node(bres, c0 + qd);
         float tn;
         const bool h = node_entry(s, r, om, tn);
-        const bool enter = force | (h & (tn < INFINITY));  // (an empty node's entry is +inf: cull_stored)
+        // (an empty node's entry is +inf: cull_stored); at the root, this quad's share of the children
+        const bool enter = (force | (h & (tn < INFINITY))) & (g != 0 || qd % P == j);
         const uint32_t eb = (uint32_t)(__builtin_amdgcn_ballot_w64(enter) >> qshift) & 0xFu;
         if (eb) {
           const int first = __builtin_ctz(eb);
@@ -1857,34 +1887,44 @@ __global__ __launch_bounds__(64) void permeate_bvh_kernel(DevScene sc, FramePara
         g = sp > 0 ? (int)my[--sp] : -1;
       }
     }
-    // rank the kept terms by order code (the four lanes of the quad share the entries), then sum
-    // them serially in that order in lane 0
-    const bool fits = n <= kLossCap;
-    // (lanes of the quad read each other's LDS entries: order the leaf loop's writes before the
-    // ranking and the ranks' scatter before the sum, as kd_wave_kernel does)
+    // the ray's lists: the P quads' counts (every lane takes part in the shuffles)
+    int nk[4], ntot = 0;
+    bool fits = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      nk[k] = __shfl(n, 4 * min(wq0 + k, 15));
+      if (k < P) { ntot += nk[k]; fits = fits && nk[k] <= kLossCap; }
+    }
+    // rank the kept terms by order code across the ray's lists (the lanes of its quads share the
+    // entries), then sum them serially in that order in the ray's first lane
+    // (lanes read each other's LDS entries: order the leaf loop's writes before the ranking and the
+    // ranks' scatter before the sum, as kd_wave_kernel does)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
+    float* const srt = &s_sorted[0][0] + wq0 * kLossCap;  // the ray's P x kLossCap sorted entries
     if (valid && fits) {
       for (int i = qd; i < n; i += 4) {
         const uint32_t ci = s_code[wq][i];
         int rank = 0;
-        for (int j = 0; j < n; ++j) rank += s_code[wq][j] < ci ? 1 : 0;
-        s_sorted[wq][rank] = s_term[wq][i];
+        for (int k = 0; k < P; ++k)
+          for (int jj = 0; jj < nk[k]; ++jj) rank += s_code[wq0 + k][jj] < ci ? 1 : 0;
+        srt[rank] = s_term[wq][i];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
-    if (valid && fits) {
+    if (valid && fits && j == 0) {
       float sum = 0.0f;
-      for (int i = 0; i < n; ++i) sum += s_sorted[wq][i];
+      for (int i = 0; i < ntot; ++i) sum += srt[i];
       if (qd == 0) ppr[slot * T + t] = (float)fp.R * fp.perm_strength - sum;  // :260
     }
-    for (unsigned long long ov = __builtin_amdgcn_ballot_w64(qd == 0 && valid && !fits); ov; ov &= ov - 1ull) {  // (wave-uniform)
-      const int src = __builtin_ctzll(ov), tt = t0 + (src >> 2);
+    for (unsigned long long ov = __builtin_amdgcn_ballot_w64(qd == 0 && j == 0 && valid && !fits); ov; ov &= ov - 1ull) {  // (wave-uniform)
+      const int src = __builtin_ctzll(ov), tt = t0 + (src >> 2) / P;
       const Seg so = make_seg(off, normalize(load3(sc.targets, tt) - off));
       const float sum = loss_sum_wave(sc, so, tt);
       if (lane == 0) ppr[slot * T + tt] = (float)fp.R * fp.perm_strength - sum;
     }
+    t0 += nr;
   }
 }
 
