@@ -9,12 +9,15 @@ pkg=$root/audio-raytracer_amd
 tmp=$(mktemp -d)
 mkdir -p "$root/variants"
 flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden "$@")
-for f in art_kernels art_trace art_bvh art_cells art_dsp; do
-  hipcc "${flags[@]}" -c "$pkg/csrc/$f.hip" -o "$tmp/$f.o" &
+# the shipped build's scheduler (audio-raytracer_amd/Makefile SCHED; ART_SCHED= for the default one)
+sched=(${ART_SCHED--mllvm -amdgpu-sched-strategy=max-ilp})
+for f in art_kernels art_trace art_cells art_dsp; do
+  hipcc "${flags[@]}" "${sched[@]}" -c "$pkg/csrc/$f.hip" -o "$tmp/$f.o" &
 done
-hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_capi.cpp" -o "$tmp/art_capi.o" &
-hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_synth.cpp" -o "$tmp/art_synth.o" &
-hipcc "${flags[@]}" -x hip -c "$pkg/csrc/art_cpu.cpp" -o "$tmp/art_cpu.o" &
+hipcc "${flags[@]}" -c "$pkg/csrc/art_bvh.hip" -o "$tmp/art_bvh.o" &
+hipcc "${flags[@]}" "${sched[@]}" -x hip -c "$pkg/csrc/art_capi.cpp" -o "$tmp/art_capi.o" &
+hipcc "${flags[@]}" "${sched[@]}" -x hip -c "$pkg/csrc/art_synth.cpp" -o "$tmp/art_synth.o" &
+hipcc "${flags[@]}" "${sched[@]}" -x hip -c "$pkg/csrc/art_cpu.cpp" -o "$tmp/art_cpu.o" &
 wait
 hipcc --offload-arch=gfx950 -shared -fPIC -rdynamic -o "$root/variants/libart_$name.so" "$tmp"/*.o
 rm -rf "$tmp"
